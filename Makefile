@@ -1,0 +1,31 @@
+# Builds the gfx950 product library (hipcc) and the CPU oracle (gcc, test infra).
+# -ffp-contract=off and no fast-math on every compile: the HIP kernels and the
+# oracle must round identically.
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+PKG     := mc-path-tracer_amd
+BUILD   := $(PKG)/build
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+            -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -Iinclude -I$(PKG)/csrc
+SRCS := $(PKG)/csrc/kernels.hip $(PKG)/csrc/runtime.cpp \
+        $(PKG)/csrc/host/scene.cpp $(PKG)/csrc/host/proxies.cpp $(PKG)/csrc/host/capi_host.cpp
+OBJS := $(patsubst $(PKG)/csrc/%,$(BUILD)/%.o,$(SRCS))
+HDRS := include/mcpt.h $(PKG)/csrc/kernels.hpp $(PKG)/csrc/device/mcpt_core.hpp $(PKG)/csrc/host/host_internal.hpp
+
+all: $(PKG)/libmcpt.so oracle/liboracle.so
+
+$(BUILD)/%.o: $(PKG)/csrc/% $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(PKG)/libmcpt.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle/liboracle.so: oracle/mcpt_oracle.c oracle/mcpt_oracle.h
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(BUILD) $(PKG)/libmcpt.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean

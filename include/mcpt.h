@@ -1,0 +1,156 @@
+/*
+ * mcpt.h -- C ABI of the MI355X-native wavefront path-tracing backend.
+ *
+ * Drop-in for the reference's CUDA path (JakeKurtz/MC-Path-Tracer):
+ *   wavefront_pathtrace(...)   CUDA-RayTracer/wavefront_kernels.cuh:24-31 (body :377-442)
+ *   clear_dfilm(dFilm*)        CUDA-RayTracer/wavefront_kernels.cuh:18   (body :55-76)
+ *   draw_to_surface            CUDA-RayTracer/wavefront_kernels.cu:6-40
+ *   PathTracer::render_image   CUDA-RayTracer/PathTracer.cpp:112-130
+ *   Scene::load / set_environment_light / add_light   CUDA-RayTracer/Scene.h:40-58
+ *   Camera::update (matrices)  CUDA-RayTracer/Camera.cu:194-224, PerspectiveCamera.cpp:49
+ *
+ * Conventions: every call returns 0 on success or a negative MCPT_E* code and
+ * stores a message retrievable with mcpt_last_error(); nothing calls exit()
+ * (the reference's checkCudaErrors exits with 99, CudaHelpers.cpp:3-11).
+ * Host buffers passed in are copied; device memory is owned by the context.
+ * Plain pointers and sizes only.
+ */
+#ifndef MCPT_H
+#define MCPT_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCPT_ABI_VERSION 1
+
+enum {
+    MCPT_OK = 0,
+    MCPT_E_INVALID = -1,   /* bad argument / state */
+    MCPT_E_HIP = -2,       /* HIP runtime error */
+    MCPT_E_IO = -3,        /* file could not be read / parsed */
+    MCPT_E_NOMEM = -4,
+    MCPT_E_NODEVICE = -5   /* no gfx950 device: the product never falls back to the CPU */
+};
+
+/* Integrator configuration.  Reference mode reproduces the hard-coded values of
+ * wavefront_kernels.cu: max_depth 5 (:142), rr_depth 3 (:189), spp <= 250 (:124). */
+typedef struct mcpt_config {
+    uint64_t seed;       /* keyed RNG seed; default 0x5EED2026 */
+    int32_t spp;         /* samples per pixel: gates processing and new samples */
+    int32_t max_depth;   /* 'path_length > max_depth' terminates */
+    int32_t rr_depth;    /* Russian roulette when 'path_length > rr_depth' */
+    int32_t tile_w;      /* film tile (Film.cu:17: 256x256) */
+    int32_t tile_h;
+    int32_t flags;       /* reserved, 0 */
+} mcpt_config;
+
+/* Scene as flat, BVH-ordered arrays (the device data model of Scene.h:24-33,
+ * BVH.h:63-72, Triangle.h:11-23, dMaterial.cuh:11-33, EnvironmentLight.h:17-40). */
+typedef struct mcpt_scene_desc {
+    int32_t ntri;
+    const float *v0, *v1, *v2;    /* 3*ntri world-space positions */
+    const float *n0, *n1, *n2;    /* 3*ntri vertex normals */
+    const int32_t *mat;           /* ntri material ids */
+    int32_t nnodes;               /* LinearBVHNode array, depth-first */
+    const float *bmin, *bmax;     /* 3*nnodes */
+    const int32_t *offset;        /* primitivesOffset (leaf) / secondChildOffset (interior) */
+    const int32_t *nprims;        /* 0 => interior */
+    const int32_t *axis;
+    int32_t nmat;
+    const float *mat_params;      /* nmat*8: base rgb, fresnel rgb, roughness, metallic */
+    int32_t ndir;                 /* directional lights (light ids 1..ndir; env is light 0) */
+    const float *dir_params;      /* ndir*7: dir xyz, color rgb, ls */
+    int32_t env_mode;             /* 0 = Color, 1 = HRDI */
+    float env_color[3];
+    float env_ls;
+    int32_t env_w, env_h;
+    const float *env_tex;         /* env_h*env_w*4 RGBA32F, row 0 = top */
+    const float *env_marginal_y;  /* env_h */
+    const float *env_conds_y;     /* env_h*env_w */
+    const float *env_pdf;         /* env_h*env_w */
+} mcpt_scene_desc;
+
+/* dCamera (Camera.h:34-46): column-major m[c][r] = m[c*4+r]. */
+typedef struct mcpt_camera {
+    float inv_view_proj[16];
+    float inv_view[16];
+    float lens_radius;
+    float focal;
+} mcpt_camera;
+
+/* PerspectiveCamera parameters (Camera.h:98-117, PerspectiveCamera.cpp:30-49). */
+typedef struct mcpt_camera_params {
+    float position[3];
+    float yaw_deg, pitch_deg;     /* Camera.cu:210-224 */
+    float fovy_rad, aspect, znear, zfar;
+    float lens_radius, focal;     /* defaults 1e-4, 35 (Camera.h:115-116) */
+} mcpt_camera_params;
+
+typedef struct mcpt_stage_stats {
+    uint64_t extend_rays;   /* closest-hit rays traced */
+    uint64_t shadow_rays;   /* light-sample shadow rays */
+    uint64_t vis_rays;      /* BRDF-sample visibility rays (wavefront_kernels.cu:334-336) */
+    uint64_t iterations;    /* wavefront iterations executed */
+    uint64_t live_paths;    /* paths still in flight after the call */
+    float ms_total;         /* device time of logic+generate+material+extend+shadow */
+    float ms_shade, ms_extend, ms_shadow;
+} mcpt_stage_stats;
+
+enum { MCPT_STAGE_LOGIC = 0, MCPT_STAGE_GENERATE = 1, MCPT_STAGE_MATERIAL = 2,
+       MCPT_STAGE_EXTEND = 3, MCPT_STAGE_SHADOW = 4 };
+
+/* Caller SoA buffers for mcpt_stage_run (host memory). */
+typedef struct mcpt_soa_view {
+    const float *ray_o;     /* 3*n */
+    const float *ray_d;     /* 3*n */
+    float *hit_pos_t;       /* EXTEND out: 4*n pos.xyz, t */
+    float *hit_nrm_mat;     /* EXTEND out: 4*n normal.xyz, (float)material (-1 miss) */
+    int32_t *hit_tri;       /* EXTEND out: n triangle index or -1 */
+    uint8_t *visible;       /* SHADOW out: n */
+} mcpt_soa_view;
+
+typedef struct mcpt_ctx mcpt_ctx;     /* device context: one per GPU, not thread-safe */
+typedef struct mcpt_scene mcpt_scene; /* host scene builder (Scene.cu) */
+
+/* ---- device context (replaces wavefront_pathtrace / clear_dfilm) ---- */
+int mcpt_create(int device, const mcpt_config *cfg, mcpt_ctx **out);
+void mcpt_destroy(mcpt_ctx *ctx);
+const char *mcpt_last_error(const mcpt_ctx *ctx);   /* ctx may be NULL: last global error */
+int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_scene_desc *desc);
+int mcpt_camera_set(mcpt_ctx *ctx, const mcpt_camera *cam);
+int mcpt_film_resize(mcpt_ctx *ctx, uint32_t w, uint32_t h, uint32_t tile_w, uint32_t tile_h);
+int mcpt_film_clear(mcpt_ctx *ctx);                                          /* == clear_dfilm */
+int mcpt_set_tiles(mcpt_ctx *ctx, const uint32_t *tile_xy, uint32_t ntiles); /* batch tile set; NULL = all */
+int mcpt_wavefront_step(mcpt_ctx *ctx, uint32_t tile_x, uint32_t tile_y, mcpt_stage_stats *st); /* one iteration, one tile */
+int mcpt_iterate(mcpt_ctx *ctx, uint32_t iterations, mcpt_stage_stats *st);  /* batch iterations over the tile set */
+int mcpt_render(mcpt_ctx *ctx, mcpt_stage_stats *st);                       /* iterate until every pixel has spp */
+int mcpt_stage_run(mcpt_ctx *ctx, int stage, const mcpt_soa_view *in, mcpt_soa_view *out, uint32_t n);
+int mcpt_film_read(mcpt_ctx *ctx, float *Ld_rgb, uint32_t *samples);         /* host copies, 3*W*H / W*H */
+int mcpt_film_read_device(mcpt_ctx *ctx, void *d_Ld_rgb, void *d_samples);  /* device-to-device */
+int mcpt_film_pack_tiles(mcpt_ctx *ctx, void *d_out, uint32_t *npix);       /* tile-set pixels -> packed 16 B/px (rgb f32, samples u32) */
+int mcpt_film_tonemap_rgba8(mcpt_ctx *ctx, float exposure, uint8_t *out);   /* == draw_to_surface */
+int mcpt_sync(mcpt_ctx *ctx);
+int mcpt_device_name(mcpt_ctx *ctx, char *buf, int32_t len);
+
+/* ---- host scene builder (Scene.cu:24-470, EnvironmentLight.cu:329-452, BVH.cu) ---- */
+mcpt_scene *mcpt_scene_new(void);
+void mcpt_scene_free(mcpt_scene *s);
+int mcpt_scene_load_glb(mcpt_scene *s, const char *path, const float *xform16);  /* xform may be NULL */
+int mcpt_scene_add_mesh(mcpt_scene *s, int32_t ntri, const float *v0, const float *v1, const float *v2,
+                        const float *n0, const float *n1, const float *n2, const float *base_rgb);
+int mcpt_scene_set_env_hdr(mcpt_scene *s, const char *path, int32_t mode);
+int mcpt_scene_set_env_color(mcpt_scene *s, const float *rgb, float ls);
+int mcpt_scene_add_dir_light(mcpt_scene *s, const float *dir, const float *rgb, float ls);
+int mcpt_scene_transform(mcpt_scene *s, const float *xform16);   /* bake a transform into all meshes */
+int mcpt_scene_make_proxy(mcpt_scene *s, int32_t config_id, const char *asset_dir); /* SURVEY.md 8d proxies */
+int mcpt_scene_build(mcpt_scene *s, int32_t max_prims_in_node);  /* SAH BVH (BVH.cu:84-333) + env tables */
+int mcpt_scene_get_desc(const mcpt_scene *s, mcpt_scene_desc *out); /* pointers owned by s */
+int mcpt_scene_bvh_depth(const mcpt_scene *s);
+int mcpt_camera_make(const mcpt_camera_params *p, mcpt_camera *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

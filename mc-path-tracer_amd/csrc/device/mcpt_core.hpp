@@ -1,0 +1,504 @@
+// mcpt_core.hpp -- MI355X-native numeric core of the wavefront path tracer.
+//
+// __host__ __device__ so the same arithmetic runs in the gfx950 kernels and in
+// the host setup code (env tables).  Every function states the reference line
+// it implements (paths relative to /root/reference/CUDA-RayTracer/).  Build
+// flags: -ffp-contract=off, no fast-math: each float/double operation is one
+// IEEE-754 rounding, so CPU and GPU agree bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MCPT_HD __host__ __device__ inline
+
+namespace mcpt {
+
+// cuda_math/dMath.h:8-25
+constexpr float K_EPSILON = 1e-6f;
+constexpr float K_HUGE = 1e32f;
+constexpr float PI_F = 3.14159265358979323846f;
+constexpr float TWO_PI_F = 6.28318530717958647692f;
+constexpr float PI_2_F = 1.57079632679489661923f;
+constexpr float PI_4_F = 0.78539816339744830961f;
+constexpr float ONE_PI_F = 0.31830988618379067153f;
+constexpr float ONE_2PI_F = 0.15915494309189533576f;
+constexpr float ONE_4PI_F = 0.07957747154594766788f;
+constexpr float BRDF_EPS = 0.00001f;  // dMaterial.cu:8
+
+MCPT_HD float qnan() { return __builtin_nanf(""); }
+MCPT_HD int sign_bit(float x) { return (int)(__builtin_bit_cast(uint32_t, x) >> 31); }
+MCPT_HD bool isnan_(float x) { return x != x; }
+// IEEE fmax: a NaN operand loses (CUDA fmaxf semantics).
+MCPT_HD float fmx(float a, float b) {
+    if (a != a) return b;
+    if (b != b) return a;
+    return a > b ? a : b;
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic transcendentals (replace CUDA --use_fast_math sin/cos/asin/
+// acos/atan2/pow): cephes single-precision polynomials, one rounding per op.
+// ---------------------------------------------------------------------------
+constexpr float DP1 = 0.78515625f;
+constexpr float DP2 = 2.4187564849853515625e-4f;
+constexpr float DP3 = 3.77489497744594108e-8f;
+constexpr float FOPI = 1.27323954473516f;
+
+MCPT_HD float sin_poly(float x, float z) {
+    float p = -1.9515295891e-4f * z;
+    p = p + 8.3321608736e-3f;
+    p = p * z;
+    p = p - 1.6666654611e-1f;
+    p = p * z;
+    p = p * x;
+    return p + x;
+}
+MCPT_HD float cos_poly(float z) {
+    float p = 2.443315711809948e-5f * z;
+    p = p - 1.388731625493765e-3f;
+    p = p * z;
+    p = p + 4.166664568298827e-2f;
+    p = p * z;
+    p = p * z;
+    float h = 0.5f * z;
+    p = p - h;
+    return p + 1.0f;
+}
+MCPT_HD float dsin(float xx) {
+    float x = xx;
+    int sign = 1;
+    if (x != x) return x;
+    if (x < 0.f) { x = -x; sign = -1; }
+    if (!(x <= 8192.f)) return qnan();
+    int j = (int)(FOPI * x);
+    float y = (float)j;
+    if (j & 1) { j += 1; y += 1.0f; }
+    j &= 7;
+    if (j > 3) { sign = -sign; j -= 4; }
+    x = ((x - y * DP1) - y * DP2) - y * DP3;
+    float z = x * x;
+    float r = (j == 1 || j == 2) ? cos_poly(z) : sin_poly(x, z);
+    return sign < 0 ? -r : r;
+}
+MCPT_HD float dcos(float xx) {
+    float x = xx;
+    if (x != x) return x;
+    if (x < 0.f) x = -x;
+    if (!(x <= 8192.f)) return qnan();
+    int j = (int)(FOPI * x);
+    float y = (float)j;
+    if (j & 1) { j += 1; y += 1.0f; }
+    j &= 7;
+    int sign = 1;
+    if (j > 3) { j -= 4; sign = -sign; }
+    if (j > 1) sign = -sign;
+    x = ((x - y * DP1) - y * DP2) - y * DP3;
+    float z = x * x;
+    float r = (j == 1 || j == 2) ? sin_poly(x, z) : cos_poly(z);
+    return sign < 0 ? -r : r;
+}
+MCPT_HD float dasin(float xx) {
+    float a, x, z;
+    int sign, flag;
+    if (xx != xx) return xx;
+    if (xx > 0.f) { sign = 1; a = xx; } else { sign = -1; a = -xx; }
+    if (a > 1.0f) return qnan();
+    if (a < 1.0e-4f) {
+        z = a;
+    } else {
+        if (a > 0.5f) { z = 0.5f * (1.0f - a); x = __builtin_sqrtf(z); flag = 1; }
+        else { x = a; z = x * x; flag = 0; }
+        float p = 4.2163199048e-2f * z;
+        p = p + 2.4181311049e-2f; p = p * z;
+        p = p + 4.5470025998e-2f; p = p * z;
+        p = p + 7.4953002686e-2f; p = p * z;
+        p = p + 1.6666752422e-1f; p = p * z;
+        p = p * x;
+        z = p + x;
+        if (flag) { z = z + z; z = PI_2_F - z; }
+    }
+    return sign < 0 ? -z : z;
+}
+MCPT_HD float dacos(float x) {
+    if (x != x) return x;
+    if (x < -1.0f || x > 1.0f) return qnan();
+    if (x < -0.5f) return PI_F - 2.0f * dasin(__builtin_sqrtf(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * dasin(__builtin_sqrtf(0.5f * (1.0f - x)));
+    return PI_2_F - dasin(x);
+}
+MCPT_HD float datan(float xx) {
+    float x, y, z;
+    int sign = 1;
+    if (xx != xx) return xx;
+    x = xx;
+    if (xx < 0.f) { sign = -1; x = -xx; }
+    if (x > 2.414213562373095f) { y = PI_2_F; x = -(1.0f / x); }
+    else if (x > 0.4142135623730950f) { y = PI_4_F; x = (x - 1.0f) / (x + 1.0f); }
+    else y = 0.0f;
+    z = x * x;
+    float p = 8.05374449538e-2f * z;
+    p = p - 1.38776856032e-1f; p = p * z;
+    p = p + 1.99777106478e-1f; p = p * z;
+    p = p - 3.33329491539e-1f; p = p * z;
+    p = p * x;
+    p = p + x;
+    y = y + p;
+    return sign < 0 ? -y : y;
+}
+MCPT_HD float datan2(float y, float x) {
+    if (x != x || y != y) return x + y;
+    if (x == 0.f) {
+        if (y > 0.f) return PI_2_F;
+        if (y < 0.f) return -PI_2_F;
+        return sign_bit(x) ? (sign_bit(y) ? -PI_F : PI_F) : y;
+    }
+    if (y == 0.f) return x > 0.f ? y : (sign_bit(y) ? -PI_F : PI_F);
+    float w;
+    if (x < 0.f) w = (y < 0.f) ? -PI_F : PI_F;
+    else w = 0.0f;
+    return w + datan(y / x);
+}
+MCPT_HD float pow5(float x) {  // pow(x, 5.f) in fresnel_schlick (dMaterial.cu:143)
+    float x2 = x * x;
+    float x4 = x2 * x2;
+    return x4 * x;
+}
+
+// ---------------------------------------------------------------------------
+// Keyed RNG around lowerbias32 (cuda_math/Random.cu:5-13)
+// ---------------------------------------------------------------------------
+MCPT_HD uint32_t lowerbias32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0xa812d533u;
+    x ^= x >> 15;
+    x *= 0xb278e4adu;
+    x ^= x >> 17;
+    return x;
+}
+MCPT_HD uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+MCPT_HD uint32_t rng_key(uint64_t seed, uint32_t pixel, uint32_t sample) {
+    uint64_t s = splitmix64((((uint64_t)pixel << 32) | (uint64_t)sample) ^ seed);
+    return (uint32_t)(s ^ (s >> 32));
+}
+// rand_float: rand() * 2^-32 in double, rounded to float (Random.cu:31-35).
+MCPT_HD float rngf(uint32_t key, uint32_t len, uint32_t slot) {
+    uint32_t d = lowerbias32(key + (len * 16u + slot) * 0x9E3779B9u);
+    return (float)((double)d * 0.00000000023283064365386962890625);
+}
+enum : uint32_t {
+    SL_GEN_U = 0, SL_GEN_V = 1,
+    SL_RR = 0, SL_LIGHT = 1, SL_ENV_U = 2, SL_ENV_V = 3,
+    SL_MAT_LOBE = 4, SL_MAT_E0 = 5,
+    SL_CONT_LOBE = 10, SL_CONT_E0 = 11
+};
+struct Rng {
+    uint32_t key, len;
+    MCPT_HD float operator()(uint32_t slot) const { return rngf(key, len, slot); }
+};
+
+// ---------------------------------------------------------------------------
+// Vec3f (cuda_math/Vector.h): one rounding per component per operator.
+// ---------------------------------------------------------------------------
+struct V3 { float x, y, z; };
+MCPT_HD V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+MCPT_HD V3 operator+(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+MCPT_HD V3 operator-(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+MCPT_HD V3 operator*(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+MCPT_HD V3 operator/(V3 a, V3 b) { return V3{a.x / b.x, a.y / b.y, a.z / b.z}; }
+MCPT_HD V3 operator*(V3 v, float s) { return V3{s * v.x, s * v.y, s * v.z}; }
+MCPT_HD V3 operator/(V3 v, float s) { return V3{v.x / s, v.y / s, v.z / s}; }
+MCPT_HD V3 operator-(V3 v) { return V3{-v.x, -v.y, -v.z}; }
+MCPT_HD float dot(V3 a, V3 b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }  // Vector.h:790
+MCPT_HD V3 normalize(V3 v) {                                                      // Vector.h:1077
+    float l = __builtin_sqrtf(dot(v, v));
+    return (l == 0.f) ? v : v / l;
+}
+MCPT_HD V3 cross(V3 a, V3 b) {                                                    // Vector.h:1108
+    return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+MCPT_HD V3 reflect(V3 i, V3 n) { return i - (n * 2.f) * dot(n, i); }               // Vector.h:1103
+MCPT_HD V3 mix(V3 a, V3 b, float t) { return a * (1.f - t) + b * t; }               // Vector.h:1092
+MCPT_HD float luminance(V3 c) {                                                   // Vector.h:1123
+    return (float)(0.299 * (double)c.x + 0.587 * (double)c.y + 0.114 * (double)c.z);
+}
+MCPT_HD V3 ld3(const float* p, int64_t i) { return V3{p[3 * i], p[3 * i + 1], p[3 * i + 2]}; }
+
+// jek::gram_schmidt (Vector.h:1128-1139): component-wise divide quirk kept.
+MCPT_HD V3 gram_schmidt(V3 v, const Rng& r, uint32_t slot0) {
+    float rx = r(slot0 + 0) * 2.f + -1.f;  // rand_float(-1,1): Random.cu:39-42
+    float ry = r(slot0 + 1) * 2.f + -1.f;
+    float rz = r(slot0 + 2) * 2.f + -1.f;
+    V3 x = v3(rx, ry, rz);
+    float x_dot_v = dot(x, v);
+    V3 vn = normalize(v);
+    V3 vn2 = vn * vn;
+    x = x - ((v * x_dot_v) / vn2);
+    return normalize(x);
+}
+// sample_spherical_map / _direction (Vector.h:1141-1160).
+MCPT_HD void spherical_map(V3 d, float& u, float& v) {
+    u = 0.5f + datan2(d.z, d.x) * ONE_2PI_F;
+    v = 0.5f - dasin(d.y) * ONE_PI_F;
+}
+MCPT_HD V3 spherical_direction(float u, float v) {
+    float phi = (float)((double)(2.f * PI_F) * ((double)u - 0.5));  // fp64 island
+    float theta = PI_F * v;
+    float st = dsin(theta);
+    V3 n;
+    n.x = dcos(phi) * st;
+    n.z = dsin(phi) * st;
+    n.y = dcos(theta);
+    return n;
+}
+
+// ---------------------------------------------------------------------------
+// Environment light (EnvironmentLight.cu:10-109, Helpers.cu:15-30).
+// ---------------------------------------------------------------------------
+struct EnvView {
+    int mode;  // 0 Color, 1 HRDI
+    float color[3];
+    float ls;
+    int w, h;
+    const float4* tex;        // RGBA32F, row 0 = top (stbi_loadf, no flip: dTexture.cu:208)
+    const float* marginal_y;  // h
+    const float* conds_y;     // h*w
+    const float* pdf;         // h*w
+};
+
+MCPT_HD int upper_bound(const float* list, int size, float val) {  // Helpers.cu:15-30
+    int middle, left = 0, right = size;
+    while (left < right) {
+        middle = (right - left) / 2 + left;
+        if (val >= list[middle]) left = middle + 1;
+        else right = middle;
+    }
+    if (left < size && list[left] <= val) left++;
+    return left;
+}
+MCPT_HD int wrapi(int i, int n) { int r = i % n; return r < 0 ? r + n : r; }
+MCPT_HD float q8(float a) { return __builtin_floorf(a * 256.f + 0.5f) * (1.0f / 256.f); }
+// Software tex2DLod<float4>: linear filter, wrap, normalized coords, 8-bit
+// fractional weights like the texture unit (dTexture.cu:265-271).  NaN -> 0.
+MCPT_HD V3 tex_bilinear(const float4* tex, int W, int H, float u, float v) {
+    if (!(__builtin_fabsf(u) < 65536.f)) u = 0.f;
+    if (!(__builtin_fabsf(v) < 65536.f)) v = 0.f;
+    float x = u * (float)W - 0.5f;
+    float y = v * (float)H - 0.5f;
+    float fx = __builtin_floorf(x), fy = __builtin_floorf(y);
+    float ax = q8(x - fx), ay = q8(y - fy);
+    int i0 = wrapi((int)fx, W), i1 = wrapi((int)fx + 1, W);
+    int j0 = wrapi((int)fy, H), j1 = wrapi((int)fy + 1, H);
+    float4 t00 = tex[(int64_t)j0 * W + i0], t10 = tex[(int64_t)j0 * W + i1];
+    float4 t01 = tex[(int64_t)j1 * W + i0], t11 = tex[(int64_t)j1 * W + i1];
+    float bx = 1.f - ax, by = 1.f - ay;
+    float w00 = bx * by, w10 = ax * by, w01 = bx * ay, w11 = ax * ay;
+    V3 o;
+    o.x = ((w00 * t00.x + w10 * t10.x) + w01 * t01.x) + w11 * t11.x;
+    o.y = ((w00 * t00.y + w10 * t10.y) + w01 * t01.y) + w11 * t11.y;
+    o.z = ((w00 * t00.z + w10 * t10.z) + w01 * t01.z) + w11 * t11.z;
+    return o;
+}
+MCPT_HD V3 env_L(const EnvView& e, V3 wi) {  // EnvironmentLight.cu:34-47
+    if (e.mode == 0 || e.tex == nullptr) return v3(e.color[0], e.color[1], e.color[2]) * e.ls;
+    float u, v;
+    spherical_map(wi, u, v);
+    return tex_bilinear(e.tex, e.w, e.h, u, v);
+}
+MCPT_HD float env_pdf(const EnvView& e, V3 wi) {  // EnvironmentLight.cu:65-85
+    if (e.mode == 0 || e.tex == nullptr) return ONE_4PI_F;
+    float u, v;
+    spherical_map(wi, u, v);
+    float fx = u * (float)(unsigned)(e.w - 1), fy = v * (float)(unsigned)(e.h - 1);
+    int px = (fx == fx && fx >= 0.f && fx < (float)e.w) ? (int)fx : 0;
+    int py = (fy == fy && fy >= 0.f && fy < (float)e.h) ? (int)fy : 0;
+    float pdf = e.pdf[(int64_t)py * e.w + px];
+    float sin_theta = dsin(PI_F * v);
+    if (sin_theta == 0.f) return 0.f;
+    return pdf * (float)((unsigned)e.w * (unsigned)e.h) / (((2.f * sin_theta) * PI_F) * PI_F);
+}
+MCPT_HD V3 env_dir(const EnvView& e, const Rng& r) {  // EnvironmentLight.cu:10-33
+    if (e.mode == 0 || e.tex == nullptr) {
+        float u = r(SL_ENV_U);
+        float v = r(SL_ENV_V);
+        return spherical_direction(u, v);
+    }
+    float ex = r(SL_ENV_U);
+    float ey = r(SL_ENV_V);
+    int y = (int)((float)upper_bound(e.marginal_y, e.h, ey) - 1.f);
+    if (y < 0) y = 0;  // unreachable (marginal_y[0] == 0); reference reads row -1
+    int x = (int)((float)upper_bound(e.conds_y + (int64_t)y * e.w, e.w, ex) - 1.f);
+    float u = (float)x / (float)e.w;
+    float v = (float)y / (float)e.h;
+    return spherical_direction(u, v);
+}
+
+// ---------------------------------------------------------------------------
+// BRDF (dMaterial.cu), material factors only (dMaterial.cu:10-115).
+// ---------------------------------------------------------------------------
+struct Mat { V3 base, fresnel; float rough, metal; };
+MCPT_HD Mat load_mat(const float* p) {
+    Mat m;
+    m.base = v3(p[0], p[1], p[2]);
+    m.fresnel = v3(p[3], p[4], p[5]);
+    m.rough = fmx(p[6], BRDF_EPS);  // get_roughness (dMaterial.cu:54)
+    m.metal = p[7];
+    return m;
+}
+MCPT_HD float power_heuristic(float fPdf, float gPdf) {  // dMaterial.cu:134-139
+    float f = 1.0f * fPdf, g = 1.0f * gPdf;
+    return (f * f) / (f * f + g * g);
+}
+MCPT_HD V3 fresnel_schlick(V3 f0, V3 v, V3 h) {  // dMaterial.cu:141-144
+    float v_dot_h = fmx(dot(v, h), 0.f);
+    return f0 + (v3(1.f, 1.f, 1.f) - f0) * pow5(1.f - v_dot_h);
+}
+MCPT_HD float ndf_ggx_tr(V3 n, V3 h, float r) {  // dMaterial.cu:150-161
+    float a = r * r;
+    float a2 = a * a;
+    float n_dot_h = fmx(dot(n, h), BRDF_EPS);
+    float n_dot_h_2 = n_dot_h * n_dot_h;
+    float denom = fmx(n_dot_h_2 * (a2 - 1.f) + 1.f, BRDF_EPS);
+    return a2 / ((PI_F * denom) * denom);
+}
+MCPT_HD float g1_schlick_ggx(V3 v, V3 n, float r) {  // dMaterial.cu:205-213
+    float a = r * r;
+    float k = a / 2.f;
+    float n_dot_v = fmx(dot(n, v), BRDF_EPS);
+    return n_dot_v / fmx(n_dot_v * (1.f - k) + k, BRDF_EPS);
+}
+MCPT_HD V3 diff_get_wi(V3 N, const Rng& r, uint32_t s0) {  // dMaterial.cu:232-254
+    float e0 = r(s0 + 0);
+    float e1 = r(s0 + 1);
+    float sinTheta = __builtin_sqrtf(1.f - e0 * e0);
+    float phi = (2.f * PI_F) * e1;
+    float x = sinTheta * dcos(phi);
+    float z = sinTheta * dsin(phi);
+    V3 T = gram_schmidt(N, r, s0 + 2);
+    V3 B = normalize(cross(N, T));
+    return normalize((T * x + N * e0) + B * z);
+}
+MCPT_HD V3 diff_get_f(const Mat& m, V3 n, V3 wi, V3 wo) {  // dMaterial.cu:259-276
+    float n_dot_wi = fmx(dot(n, wi), BRDF_EPS);
+    V3 f0 = mix(m.fresnel, m.base, m.metal);
+    V3 wh = normalize(wo + wi);
+    V3 F = fresnel_schlick(f0, wh, wo);
+    V3 kD = v3(1.f, 1.f, 1.f) - F;
+    kD = kD * (1.f - m.metal);
+    return ((kD * m.base) * n_dot_wi) * ONE_PI_F;
+}
+MCPT_HD V3 spec_get_wi(const Mat& m, V3 N, V3 wo, const Rng& r, uint32_t s0) {  // dMaterial.cu:278-307
+    float rr = m.rough;
+    float a2 = ((rr * rr) * rr) * rr;
+    float e0 = r(s0 + 0);
+    float e1 = r(s0 + 1);
+    float theta = dacos(__builtin_sqrtf((1.f - e0) / (e0 * (a2 - 1.f) + 1.f)));
+    float phi = TWO_PI_F * e1;
+    float st = dsin(theta);
+    V3 h = v3(st * dcos(phi), dcos(theta), st * dsin(phi));
+    V3 T = gram_schmidt(N, r, s0 + 2);
+    V3 B = normalize(cross(N, T));
+    V3 smp = normalize((T * h.x + N * h.y) + B * h.z);
+    return normalize(reflect(-wo, smp));
+}
+MCPT_HD float spec_get_pdf(const Mat& m, V3 n, V3 wi, V3 wo) {  // dMaterial.cu:308-321
+    V3 wh = normalize(wo + wi);
+    float wh_dot_n = fmx(dot(wh, n), BRDF_EPS);
+    float wo_dot_wh = fmx(dot(wo, wh), BRDF_EPS);
+    float D = ndf_ggx_tr(n, wh, m.rough);
+    return (D * wh_dot_n) / fmx(4.f * wo_dot_wh, BRDF_EPS);
+}
+MCPT_HD V3 spec_get_f(const Mat& m, V3 n, V3 wi, V3 wo) {  // dMaterial.cu:322-343
+    V3 f0 = mix(m.fresnel, m.base, m.metal);
+    V3 wh = normalize(wo + wi);
+    float n_dot_wi = fmx(dot(n, wi), BRDF_EPS);
+    float n_dot_wo = fmx(dot(n, wo), BRDF_EPS);
+    float D = ndf_ggx_tr(n, wh, m.rough);
+    float G = g1_schlick_ggx(wi, n, m.rough) * g1_schlick_ggx(wo, n, m.rough);
+    V3 F = fresnel_schlick(f0, wh, wo);
+    V3 L = (F * (D * G)) * n_dot_wi;
+    return L / fmx((4.f * n_dot_wo) * n_dot_wi, BRDF_EPS);
+}
+MCPT_HD float diff_get_pdf() { return ONE_2PI_F; }  // dMaterial.cu:255-258
+MCPT_HD V3 brdf_f(const Mat& m, V3 n, V3 wi, V3 wo) {  // spec_get_f + diff_get_f (wavefront_kernels.cu:326)
+    return spec_get_f(m, n, wi, wo) + diff_get_f(m, n, wi, wo);
+}
+MCPT_HD float brdf_pdf(const Mat& m, V3 n, V3 wi, V3 wo) {  // (diff + spec) * 0.5 (wavefront_kernels.cu:329)
+    return (diff_get_pdf() + spec_get_pdf(m, n, wi, wo)) * 0.5f;
+}
+
+// ---------------------------------------------------------------------------
+// Camera (Camera.cu:18-45, Sample.cu:129-149).
+// ---------------------------------------------------------------------------
+struct CamView {
+    float ivp[16];  // inverse(proj*view), column-major m[c][r]
+    float iv[16];   // inverse(view)
+    float lens_radius, focal;
+};
+MCPT_HD void mat_vec4(const float* m, float v0, float v1, float v2, float v3_, float out[4]) {
+    for (int r = 0; r < 4; r++)  // cuda_math/Matrix.h:196-204
+        out[r] = m[0 * 4 + r] * v0 + m[1 * 4 + r] * v1 + m[2 * 4 + r] * v2 + m[3 * 4 + r] * v3_;
+}
+MCPT_HD void concentric_disk(const Rng& r, float& dx, float& dy) {  // Sample.cu:150-172
+    float ux = r(SL_GEN_U), uy = r(SL_GEN_V);
+    float ox = 2.f * ux - 1.f, oy = 2.f * uy - 1.f;
+    if (ox == 0.f && oy == 0.f) { dx = 0.f; dy = 0.f; return; }
+    float theta, rr;
+    if (__builtin_fabsf(ox) > __builtin_fabsf(oy)) { rr = ox; theta = PI_4_F * (oy / ox); }
+    else { rr = oy; theta = PI_2_F - PI_4_F * (ox / oy); }
+    dx = rr * dcos(theta);
+    dy = rr * dsin(theta);
+}
+MCPT_HD void gen_ray(const CamView& c, int W, int H, int xi, int yi, const Rng& r, V3& o, V3& d) {
+    float x = (float)xi, y = (float)yi;
+    float px = (float)(2.f * (((double)x + 0.5) / (double)(float)W) - 1.f);  // fp64 island :21-22
+    float py = (float)(1.f - 2.f * (((double)y + 0.5) / (double)(float)H));
+    float an[4], af[4];
+    mat_vec4(c.ivp, px, py, -1.f, 1.f, an);
+    mat_vec4(c.ivp, px, py, 1.f, 1.f, af);
+    V3 pNear = v3(an[0], an[1], an[2]) / an[3];
+    V3 pFar = v3(af[0], af[1], af[2]) / af[3];
+    o = pNear;
+    d = normalize(pFar - pNear);
+    if (c.lens_radius > 0.f) {
+        V3 pFocal = o + d * c.focal;
+        float lx, ly;
+        concentric_disk(r, lx, ly);
+        lx = lx * c.lens_radius;
+        ly = ly * c.lens_radius;
+        float al[4];
+        mat_vec4(c.iv, lx, ly, 0.f, 1.f, al);
+        V3 pLens = v3(al[0], al[1], al[2]) / al[3];
+        o = pLens;
+        d = normalize(pFocal - o);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Triangle / box tests (Triangle.cu:9-65, Bounds3f.h:121-153).
+// ---------------------------------------------------------------------------
+// Moller-Trumbore with TEST_CULL and the fp64 det island.  Returns 1 when the
+// line hits the front face; t/u/v are the reference's float values.
+MCPT_HD bool tri_test(V3 o, V3 d, V3 p0, V3 e1, V3 e2, float& t, float& u_out, float& v_out) {
+    V3 pvec = cross(d, e2);
+    float detf = dot(e1, pvec);
+    if (detf < K_EPSILON) return false;  // (double)det < (double)1e-6f, same ordering
+    V3 tvec = o - p0;
+    float u = dot(tvec, pvec);
+    if (u < 0.f || u > detf) return false;
+    V3 qvec = cross(tvec, e1);
+    float v = dot(d, qvec);
+    if (v < 0.f || u + v > detf) return false;
+    float tf = dot(e2, qvec);
+    double inv_det = 1.0 / (double)detf;
+    t = (float)((double)tf * inv_det);
+    u_out = (float)((double)u * inv_det);
+    v_out = (float)((double)v * inv_det);
+    return true;
+}
+
+}  // namespace mcpt

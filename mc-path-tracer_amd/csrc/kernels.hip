@@ -1,0 +1,479 @@
+// kernels.hip -- gfx950 kernels of the wavefront path tracer.
+//
+// One wavefront iteration (= one reference wavefront_pathtrace call,
+// wavefront_kernels.cu:377-442, widened from one 256x256 tile to a tile set):
+//   k_shade   fused wf_logic + wf_generate + wf_mat_mix  (wavefront_kernels.cu:90-251, 295-375)
+//   k_extend  wf_extend: closest-hit BVH traversal      (wavefront_kernels.cu:253-272, Triangle.cu:144-203)
+//   k_anyhit  wf_shadow + the BRDF visibility ray that the reference traces inline in
+//             wf_mat_mix (wavefront_kernels.cu:274-293, 334-336; Triangle.cu:204-243)
+// The material stage evaluates the BRDF-sample terms unconditionally and the
+// visibility bit selects them in the next k_shade; this is exactly the
+// reference's result (f_brdf = Li_brdf = 0, pdf_brdf.x = pdf_light.y = 1 when
+// occluded, wavefront_kernels.cu:311).  Queues are compacted per block with
+// wave64 ballot + mbcnt + an LDS prefix and one atomic per block and queue.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device/mcpt_core.hpp"
+#include "kernels.hpp"
+
+using namespace mcpt;
+
+namespace mcpt_dev {
+
+// ---------------------------------------------------------------------------
+// block-level stream compaction (replaces per-thread atomicAdd pushes,
+// wavefront_kernels.cu:215,221,250,373,374)
+// ---------------------------------------------------------------------------
+template <int NQ>
+__device__ inline void block_push(const bool (&want)[NQ], uint32_t* const (&counters)[NQ], uint32_t (&slot)[NQ],
+                                  uint32_t (&total)[NQ]) {
+    __shared__ uint32_t s_wave[NQ][kBlock / 64];
+    __shared__ uint32_t s_base[NQ];
+    __shared__ uint32_t s_tot[NQ];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t prefix[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+        uint64_t m = __ballot(want[q]);
+        prefix[q] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (lane == 0) s_wave[q][wave] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x < NQ) {
+        const int q = threadIdx.x;
+        uint32_t tot = 0;
+        for (int w = 0; w < kBlock / 64; w++) { uint32_t c = s_wave[q][w]; s_wave[q][w] = tot; tot += c; }
+        s_base[q] = tot ? atomicAdd(counters[q], tot) : 0u;
+        s_tot[q] = tot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+        slot[q] = s_base[q] + s_wave[q][wave] + prefix[q];
+        total[q] = s_tot[q];
+    }
+}
+
+__device__ inline V3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
+__device__ inline float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
+
+__device__ inline V3 light_L(const DevScene& sc, int id, V3 wi) {
+    if (id == 0) return env_L(sc.env, wi);
+    const float* p = sc.dirs + 7 * (id - 1);  // DirectionalLight.cu:34
+    return v3(p[3], p[4], p[5]) * p[6];
+}
+__device__ inline float light_pdf(const DevScene& sc, int id, V3 wi) {
+    if (id == 0) return env_pdf(sc.env, wi);
+    return 1.f;  // DirectionalLight.cu:40-43
+}
+
+// ---------------------------------------------------------------------------
+// k_shade: one thread per pixel of the tile set.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
+    const DevScene& sc = a.scene;
+    const int tile_px = a.tile_w * a.tile_h;
+    const int bpt = (tile_px + kBlock - 1) / kBlock;
+    const int tile = blockIdx.x / bpt;
+    const int li = (blockIdx.x - tile * bpt) * kBlock + threadIdx.x;
+    bool valid = tile < a.ntiles && li < tile_px;
+    uint32_t pid = 0;
+    int x = 0, y = 0;
+    if (valid) {
+        int2 t = a.tiles[tile];
+        x = t.x * a.tile_w + li % a.tile_w;
+        y = t.y * a.tile_h + li / a.tile_w;
+        valid = x < a.W - 1 && y < a.H - 1;  // last column and row never rendered (wavefront_kernels.cu:110)
+        pid = (uint32_t)y * (uint32_t)a.W + (uint32_t)x;
+    }
+    bool want_ext = false, want_l = false, want_b = false;
+    bool new_path = false;
+    uint32_t nflags = 0, fl = F_DEAD;
+    V3 new_o = v3(0, 0, 0), new_d = v3(0, 0, 0);
+    V3 so_l = v3(0, 0, 0), sd_l = v3(0, 0, 0), so_b = v3(0, 0, 0), sd_b = v3(0, 0, 0);
+    if (valid) {
+        fl = a.p.flags[pid];
+        nflags = fl;
+        uint32_t samples = a.p.samples[pid];
+        bool dead = (fl & F_DEAD) != 0;
+        const uint32_t spp = (uint32_t)a.spp;
+        if (!dead && samples < spp) {  // wavefront_kernels.cu:124
+            const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
+            const Rng r{rng_key(a.seed, pid, samples), len};
+            float4 hn = a.p.hit_n[pid];
+            const int mat = __float_as_int(hn.w);
+            const bool found = mat >= 0;
+            float4 b4 = a.p.beta[pid];
+            const V3 B = xyz(b4);
+            float4 ld4 = a.p.Ld[pid];
+            V3 film = xyz(ld4);
+            bool terminate = false;
+            V3 beta_store = B;
+            V3 wo = v3(0, 0, 0);
+            if (len == 1) {  // :129-140
+                if (found) {
+                    film = film + v3(0.f, 0.f, 0.f) * B;
+                } else {
+                    float4 rd = a.p.ray_d[pid];
+                    for (int i = 0; i < sc.nlights; i++) film = film + env_L(sc.env, xyz(rd)) * B;
+                }
+            }
+            if (len > (uint32_t)a.max_depth || !found) terminate = true;  // :142-146
+            if (len <= (uint32_t)a.max_depth && len > 1) {                // :150-197
+                float4 n0 = a.p.nee0[pid], n1 = a.p.nee1[pid];
+                const uint8_t vl = a.p.vis[2 * pid], vb = a.p.vis[2 * pid + 1];
+                V3 acc = v3(0.f, 0.f, 0.f);
+                if ((fl & F_CONDL) && vl) acc = acc + xyz(n0);
+                if (fl & F_HASVIS) {
+                    if (vb) { if (fl & F_CONDB) acc = acc + xyz(n1); }
+                    else acc = acc + v3(0.f, 0.f, 0.f);
+                } else {
+                    acc = acc + v3(0.f, 0.f, 0.f);  // delta light: f_brdf = 0, weights 0.5
+                }
+                film = film + acc * B;
+                if (fl & F_FZERO) {
+                    terminate = true;
+                } else {
+                    beta_store = B * v3(b4.w, n0.w, n1.w);  // paths->beta *= f_sample / pdf_sample (:187)
+                    if (len > (uint32_t)a.rr_depth) {        // :189-196
+                        float q = fmx(0.05f, 1.f - B.y);
+                        if (r(SL_RR) < q) terminate = true;
+                    }
+                }
+            }
+            a.p.Ld[pid] = f4(film, ld4.w);
+            if (terminate) {  // :199-204
+                dead = true;
+                samples++;
+                a.p.samples[pid] = samples;
+                nflags = F_DEAD;
+            } else {
+                // ---- continue: light choice (:207-215) fused with wf_mat_mix (:295-375)
+                float4 hp = a.p.hit_p[pid];
+                const V3 pos = xyz(hp), n = xyz(hn);
+                wo = -xyz(a.p.ray_d[pid]);
+                int l_id = (int)(r(SL_LIGHT) * (float)(sc.nlights - 0) + (float)0);
+                const int light_id = (l_id == sc.nlights) ? 0 : l_id;
+                V3 ldir;
+                if (light_id == 0) ldir = env_dir(sc.env, r);
+                else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
+                so_l = pos + n * 0.01f;
+                sd_l = ldir;
+                const Mat m = load_mat(sc.mats + 8 * mat);
+                const bool delta = light_id > 0;
+                V3 f_l = brdf_f(m, n, ldir, wo);
+                V3 Li_l = light_L(sc, light_id, ldir);
+                float pdfl_x = light_pdf(sc, light_id, ldir);
+                float pdfb_y = !delta ? brdf_pdf(m, n, ldir, wo) : 1.f;
+                float wL = power_heuristic(pdfl_x, pdfb_y);
+                V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
+                uint32_t nf = 0;
+                if (wL > 0.f && pdfl_x > 0.f) nf |= F_CONDL;
+                V3 cB = v3(0.f, 0.f, 0.f);
+                if (!delta) {
+                    V3 wi_b = (r(SL_MAT_LOBE) < 0.5f) ? spec_get_wi(m, n, wo, r, SL_MAT_E0) : diff_get_wi(n, r, SL_MAT_E0);
+                    so_b = pos + wi_b * 0.001f;
+                    sd_b = wi_b;
+                    V3 f_b = brdf_f(m, n, wi_b, wo);
+                    V3 Li_b = light_L(sc, light_id, wi_b);
+                    float pdfb_x = brdf_pdf(m, n, wi_b, wo);
+                    float pdfl_y = light_pdf(sc, light_id, wi_b);
+                    float wB = power_heuristic(pdfb_x, pdfl_y);
+                    cB = ((f_b * Li_b) * wB) / pdfb_x;
+                    if (wB > 0.f && pdfb_x > 0.f) nf |= F_CONDB;
+                    nf |= F_HASVIS;
+                    want_b = true;
+                }
+                V3 wi_s = (r(SL_CONT_LOBE) < 0.5f) ? spec_get_wi(m, n, wo, r, SL_CONT_E0) : diff_get_wi(n, r, SL_CONT_E0);
+                float pdf_s = brdf_pdf(m, n, wi_s, wo);
+                V3 f_s = brdf_f(m, n, wi_s, wo);
+                if ((f_s.x == 0.f && f_s.y == 0.f && f_s.z == 0.f) || pdf_s == 0.f) nf |= F_FZERO;
+                V3 rr = f_s / pdf_s;
+                new_o = pos + n * 0.001f;  // :358
+                new_d = wi_s;
+                a.p.beta[pid] = f4(beta_store, rr.x);
+                a.p.nee0[pid] = f4(cL, rr.y);
+                a.p.nee1[pid] = f4(cB, rr.z);
+                nflags = nf | ((len + 1) << F_LEN_SHIFT);  // extend increments len (:270)
+                want_ext = true;
+                want_l = true;
+            }
+        }
+        if (dead && samples < spp) {  // :219-222 + wf_generate (:225-251)
+            const Rng r0{rng_key(a.seed, pid, samples), 0u};
+            gen_ray(a.cam, a.W, a.H, x, y, r0, new_o, new_d);
+            a.p.beta[pid] = make_float4(1.f, 1.f, 1.f, 0.f);
+            nflags = 1u << F_LEN_SHIFT;
+            want_ext = true;
+            new_path = true;
+        }
+        if (want_ext || nflags != fl) a.p.flags[pid] = nflags;
+        if (want_ext) {
+            a.p.ray_o[pid] = f4(new_o, 0.f);
+            a.p.ray_d[pid] = f4(new_d, 0.f);
+        }
+        if (want_l) {
+            a.p.sray_o[2 * pid] = f4(so_l, 0.f);
+            a.p.sray_d[2 * pid] = f4(sd_l, 0.f);
+        }
+        if (want_b) {
+            a.p.sray_o[2 * pid + 1] = f4(so_b, 0.f);
+            a.p.sray_d[2 * pid + 1] = f4(sd_b, 0.f);
+        }
+    }
+    (void)new_path;
+    // ---- compaction: ext queue and any-hit queue (light + vis rays)
+    bool want[3] = {want_ext, want_l, want_b};
+    uint32_t* ctr[3] = {&a.cnt->ext, &a.cnt->any, &a.cnt->any};
+    uint32_t slot[3], total[3];
+    block_push<3>(want, ctr, slot, total);
+    if (want_ext) a.ext_q[slot[0]] = pid;
+    if (want_l) a.any_q[slot[1]] = 2 * pid;
+    if (want_b) a.any_q[slot[2]] = 2 * pid + 1;
+    if (threadIdx.x == 0 && total[2]) atomicAdd(&a.cnt->vis, total[2]);  // BRDF visibility rays
+}
+
+// ---------------------------------------------------------------------------
+// BVH traversal.  Child-pair nodes (both child boxes in the parent, 64 B) with
+// the reference's slab arithmetic per box (Bounds3f.h:121-153); an extra
+// conservative cull rejects boxes entirely behind the origin or beyond the
+// current best t by more than 2^-8 relative (results unchanged unless a
+// triangle's Moller-Trumbore t error exceeds that margin).  Ties on t go to
+// the lower triangle index, so the traversal order is free (near-first here).
+// Stack: kLdsStack entries per lane in LDS ([entry][lane], conflict-free),
+// deeper entries in private scratch.
+// ---------------------------------------------------------------------------
+__device__ inline bool slab(const float* mn, const float* mx, V3 o, V3 inv, int nx, int ny, int nz, float& t0, float& t1) {
+    float bx0 = nx ? mx[0] : mn[0], bx1 = nx ? mn[0] : mx[0];
+    float by0 = ny ? mx[1] : mn[1], by1 = ny ? mn[1] : mx[1];
+    float bz0 = nz ? mx[2] : mn[2], bz1 = nz ? mn[2] : mx[2];
+    float tmin = (bx0 - o.x) * inv.x;
+    float tmax = (bx1 - o.x) * inv.x;
+    float tymin = (by0 - o.y) * inv.y;
+    float tymax = (by1 - o.y) * inv.y;
+    if ((tmin > tymax) || (tymin > tmax)) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = (bz0 - o.z) * inv.z;
+    float tzmax = (bz1 - o.z) * inv.z;
+    if ((tmin > tzmax) || (tzmin > tmax)) return false;
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    t0 = tmin;
+    t1 = tmax;
+    return true;
+}
+constexpr float kCullAbs = 1e-5f;
+constexpr float kCullRel = 1.0f / 256.0f;
+
+__device__ inline bool keep_box(float t0, float t1, float cut) { return !(t1 < -kCullAbs) && !(t0 > cut); }
+
+template <bool ANY>
+struct TraceResult { int tri; float t; };
+
+template <bool ANY>
+__device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*stk)[kBlock], int lane_slot, uint32_t* nstat) {
+    TraceResult<ANY> res{-1, K_HUGE};
+    V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;
+    float best = K_HUGE;
+    float cut = best + best * kCullRel;
+    int2 spill[kMaxStack - kLdsStack];
+    int sp = 0;
+    // NaN / zero direction: every triangle test fails (det NaN or 0), so the
+    // reference reports a miss / visible.
+    if (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f)) return res;
+    float t0, t1;
+    if (!slab(sc.root_mn, sc.root_mx, o, inv, nx, ny, nz, t0, t1) || !keep_box(t0, t1, cut)) return res;
+    int ref = sc.root_ref;
+    uint32_t nodes = 0, tests = 0;
+    for (;;) {
+        if (ref >= 0) {
+            const float4* nd = sc.nodes + 4 * ref;
+            float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+            nodes++;
+            float mn0[3] = {q0.x, q0.y, q0.z}, mx0[3] = {q0.w, q1.x, q1.y};
+            float mn1[3] = {q1.z, q1.w, q2.x}, mx1[3] = {q2.y, q2.z, q2.w};
+            float a0, b0, a1, b1;
+            bool h0 = slab(mn0, mx0, o, inv, nx, ny, nz, a0, b0) && keep_box(a0, b0, cut);
+            bool h1 = slab(mn1, mx1, o, inv, nx, ny, nz, a1, b1) && keep_box(a1, b1, cut);
+            int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
+            if (h0 && h1) {
+                bool first0 = !(a1 < a0);
+                int near = first0 ? c0 : c1, far = first0 ? c1 : c0;
+                float far_t = first0 ? a1 : a0;
+                int2 e = make_int2(far, __float_as_int(far_t));
+                if (sp < kLdsStack) stk[sp][lane_slot] = e;
+                else spill[sp - kLdsStack] = e;
+                sp++;
+                ref = near;
+                continue;
+            } else if (h0) {
+                ref = c0;
+                continue;
+            } else if (h1) {
+                ref = c1;
+                continue;
+            }
+        } else {
+            const int off = ref & 0xffffff;
+            const int cnt = ((ref >> 24) & 7) + 1;
+            for (int k = 0; k < cnt; k++) {
+                const int id = off + k;
+                const float4* tp = sc.tri + 3 * id;
+                float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
+                tests++;
+                float t, u, v;
+                if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) && !(t < 0.f)) {
+                    if (ANY) {
+                        if (t < K_HUGE) { res.tri = id; res.t = t; if (nstat) { atomicAdd(nstat, nodes); atomicAdd(nstat + 1, tests); } return res; }
+                    } else if (t < best || (t == best && id < res.tri)) {
+                        best = t;
+                        res.tri = id;
+                        res.t = t;
+                        cut = best + best * kCullRel;
+                    }
+                }
+            }
+        }
+        // pop, skipping entries culled by the improved best
+        bool got = false;
+        while (sp > 0) {
+            sp--;
+            int2 e = (sp < kLdsStack) ? stk[sp][lane_slot] : spill[sp - kLdsStack];
+            if (!ANY && __int_as_float(e.y) > cut) continue;
+            ref = e.x;
+            got = true;
+            break;
+        }
+        if (!got) break;
+    }
+    if (nstat) { atomicAdd(nstat, nodes); atomicAdd(nstat + 1, tests); }
+    return res;
+}
+
+// Persistent trace kernel: each wave pulls 64 rays at a time from a counter.
+template <bool ANY>
+__global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
+    __shared__ int2 stk[kLdsStack][kBlock];
+    const int lane = threadIdx.x & 63;
+    const uint32_t n = a.count_ptr ? *a.count_ptr : a.count;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(a.work, 64u);
+        base = __shfl(base, 0);
+        if (base >= n) break;
+        const uint32_t i = base + lane;
+        if (i < n) {
+            const uint32_t rid = a.queue ? a.queue[i] : i;
+            const float4 o4 = a.ro[rid], d4 = a.rd[rid];
+            const V3 o = xyz(o4), d = xyz(d4);
+            TraceResult<ANY> tr = trace<ANY>(a.scene, o, d, stk, threadIdx.x, a.stats);
+            if (ANY) {
+                a.vis[rid] = (uint8_t)(tr.tri < 0);
+            } else {
+                const uint32_t pid = rid;
+                if (tr.tri >= 0) {
+                    const float4* tp = a.scene.tri + 3 * tr.tri;
+                    float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
+                    float t, u, v;
+                    tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v);
+                    const float4* sp4 = a.scene.tri_sh + 3 * tr.tri;
+                    float4 s0 = sp4[0], s1 = sp4[1], s2 = sp4[2];
+                    V3 n0 = v3(s0.x, s0.y, s0.z), n1 = v3(s0.w, s1.x, s1.y), n2 = v3(s1.z, s1.w, s2.x);
+                    float w = (1.f - u) - v;
+                    V3 nn = normalize((n1 * u + n2 * v) + n0 * w);  // Triangle.cu:76
+                    nn = normalize(nn);                              // identity transform, :82
+                    V3 p = o + d * t;                                // :86
+                    a.hit_p[pid] = make_float4(p.x, p.y, p.z, t);
+                    a.hit_n[pid] = make_float4(nn.x, nn.y, nn.z, s2.y);  // s2.y = material id bits
+                    if (a.hit_tri) a.hit_tri[pid] = tr.tri;
+                } else {
+                    a.hit_p[pid] = make_float4(0.f, 0.f, 0.f, K_HUGE);
+                    a.hit_n[pid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+                    if (a.hit_tri) a.hit_tri[pid] = -1;
+                }
+            }
+        }
+    }
+}
+
+__global__ void k_clear(ClearArgs a) {  // g_clear_dfilm (wavefront_kernels.cu:55-66)
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    a.flags[i] = F_DEAD;
+    a.samples[i] = 0;
+    a.Ld[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__global__ void k_tonemap(TonemapArgs a) {  // draw_to_surface (wavefront_kernels.cu:6-40)
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    float4 L = a.Ld[i];
+    float s = (float)a.samples[i];
+    V3 c = v3(L.x / s, L.y / s, L.z / s);
+    c = c * a.exposure;
+    c = v3(c.x / (c.x + 1.0f), c.y / (c.y + 1.0f), c.z / (c.z + 1.0f));
+    float cc[3] = {255 * c.x, 255 * c.y, 255 * c.z};
+    uchar4 o;
+    unsigned char b[3];
+    for (int k = 0; k < 3; k++) {
+        float v = cc[k];
+        b[k] = (v == v && v >= 0.f && v < 4294967296.f) ? (unsigned char)(unsigned int)v : (unsigned char)0;
+    }
+    o.x = b[0]; o.y = b[1]; o.z = b[2]; o.w = 255;
+    a.out[i] = o;
+}
+
+__global__ void k_accumulate(CounterBlock* c) {  // fold per-iteration counts into 64-bit totals
+    c->tot_ext += c->ext;
+    c->tot_any += c->any;
+    c->tot_vis += c->vis;
+    c->vis = 0;
+    c->last_ext = c->ext;
+    c->ext = 0;
+    c->any = 0;
+    c->work_ext = 0;
+    c->work_any = 0;
+}
+
+__global__ void k_pack(PackArgs a) {  // tile-set pixels -> packed 16 B/px (for the RCCL gather)
+    const int tile_px = a.tile_w * a.tile_h;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint32_t)(a.ntiles * tile_px)) return;
+    const int tile = i / tile_px, li = i % tile_px;
+    int2 t = a.tiles[tile];
+    int x = t.x * a.tile_w + li % a.tile_w, y = t.y * a.tile_h + li / a.tile_w;
+    float4 o = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+    if (x < a.W && y < a.H) {
+        uint32_t pid = (uint32_t)y * a.W + x;
+        float4 L = a.Ld[pid];
+        o = make_float4(L.x, L.y, L.z, __uint_as_float(a.samples[pid]));
+    }
+    a.out[i] = o;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s) {
+    hipLaunchKernelGGL(k_shade, dim3(nblocks), dim3(kBlock), 0, s, a);
+}
+void launch_trace(const TraceArgs& a, bool any, int nblocks, hipStream_t s) {
+    if (any) hipLaunchKernelGGL(k_trace<true>, dim3(nblocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_trace<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
+}
+void launch_clear(const ClearArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_clear, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+}
+void launch_tonemap(const TonemapArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_tonemap, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+}
+void launch_accumulate(CounterBlock* c, hipStream_t s) { hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(1), 0, s, c); }
+void launch_pack(const PackArgs& a, hipStream_t s) {
+    uint32_t n = (uint32_t)(a.ntiles * a.tile_w * a.tile_h);
+    hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, s, a);
+}
+
+}  // namespace mcpt_dev

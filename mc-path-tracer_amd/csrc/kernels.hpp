@@ -1,0 +1,99 @@
+// kernels.hpp -- device data layout shared by kernels.hip and runtime.hip.
+//
+// HBM layout (P = W*H paths, one per pixel as in the reference, path_id ==
+// pixel_id, wavefront_kernels.cu:108,114).  The reference's Paths is an
+// array-of-structs with 128-B Isect and 32-B dRay per path (Wavefront.cuh:8-26);
+// here every field is a separate 16-B-aligned stream so a wave64 access is one
+// coalesced 1 KiB dwordx4 transaction:
+//   ray_o/ray_d   float4 [P]    extension ray (xyz, pad)
+//   hit_p         float4 [P]    isect.position, t
+//   hit_n         float4 [P]    isect.normal, material id (int bits, -1 = miss)
+//   sray_o/sray_d float4 [2P]   any-hit rays: [2p] light sample, [2p+1] BRDF visibility
+//   beta          float4 [P]    throughput, (f_sample/pdf_sample).x
+//   nee0 / nee1   float4 [P]    precomputed light / BRDF MIS terms, ratio .y / .z
+//   flags         u32    [P]    dead, len, MIS condition bits
+//   vis           u8     [2P]   any-hit results
+//   samples       u32    [P]    film sample count (dFilm.samples)
+//   Ld            float4 [P]    film radiance (dFilm.Ld)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device/mcpt_core.hpp"
+
+namespace mcpt_dev {
+
+constexpr int kBlock = 256;
+constexpr int kLdsStack = 16;  // traversal stack entries per lane kept in LDS
+constexpr int kMaxStack = 64;  // total (reference: int nodesToVisit[64], Triangle.cu:161)
+
+enum : uint32_t {
+    F_DEAD = 1u,
+    F_LEN_SHIFT = 1,        // bits 1..8
+    F_CONDL = 1u << 9,      // light-sample MIS term valid (w > 0 && pdf > 0)
+    F_CONDB = 1u << 10,     // BRDF-sample MIS term valid when visible
+    F_FZERO = 1u << 11,     // f_sample == 0 || pdf_sample == 0
+    F_HASVIS = 1u << 12     // non-delta light: a BRDF visibility ray was traced
+};
+
+struct DevScene {
+    const float4* nodes;    // child-pair BVH nodes, 4 x float4 each
+    const float4* tri;      // 3 x float4: (v0.xyz, e1.x) (e1.yz, e2.xy) (e2.z, -, -, -)
+    const float4* tri_sh;   // 3 x float4: (n0.xyz, n1.x) (n1.yz, n2.xy) (n2.z, mat, -, -)
+    float root_mn[3], root_mx[3];
+    int root_ref;           // >= 0 pair node, < 0 leaf (0x80000000 | (count-1)<<24 | offset)
+    int nlights;            // 1 + ndir (Scene.cu:370-388)
+    const float* mats;      // 8 floats per material
+    const float* dirs;      // 7 floats per directional light
+    mcpt::EnvView env;
+};
+
+struct DevPaths {
+    float4 *ray_o, *ray_d, *hit_p, *hit_n, *sray_o, *sray_d, *beta, *nee0, *nee1, *Ld;
+    uint32_t *flags, *samples;
+    uint8_t* vis;
+};
+
+struct CounterBlock {
+    uint32_t ext, any, vis, work_ext, work_any, last_ext, pad0, pad1;
+    unsigned long long tot_ext, tot_any, tot_vis, pad2;
+    uint32_t stats[4];      // optional traversal counters: nodes, triangle tests
+};
+
+struct ShadeArgs {
+    DevScene scene;
+    mcpt::CamView cam;
+    DevPaths p;
+    const int2* tiles;
+    int ntiles, tile_w, tile_h, W, H;
+    int spp, max_depth, rr_depth;
+    uint64_t seed;
+    uint32_t *ext_q, *any_q;
+    CounterBlock* cnt;
+};
+
+struct TraceArgs {
+    DevScene scene;
+    const float4 *ro, *rd;
+    const uint32_t* queue;      // nullptr => identity
+    const uint32_t* count_ptr;  // device count (nullptr => use count)
+    uint32_t count;
+    uint32_t* work;             // per-launch work counter (zeroed before launch)
+    float4 *hit_p, *hit_n;      // closest-hit outputs
+    int32_t* hit_tri;           // optional
+    uint8_t* vis;               // any-hit output
+    uint32_t* stats;            // optional: [nodes, tests]
+};
+
+struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n; };
+struct TonemapArgs { const float4* Ld; const uint32_t* samples; uchar4* out; float exposure; uint32_t n; };
+struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* out; };
+
+void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s);
+void launch_trace(const TraceArgs& a, bool any, int nblocks, hipStream_t s);
+void launch_clear(const ClearArgs& a, hipStream_t s);
+void launch_tonemap(const TonemapArgs& a, hipStream_t s);
+void launch_accumulate(CounterBlock* c, hipStream_t s);
+void launch_pack(const PackArgs& a, hipStream_t s);
+
+}  // namespace mcpt_dev

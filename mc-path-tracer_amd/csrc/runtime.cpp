@@ -1,0 +1,624 @@
+// runtime.cpp -- device context behind the mcpt_* C ABI (include/mcpt.h).
+//
+// Replaces the reference's orchestration: PathTracer (PathTracer.cpp:112-187),
+// Film device state (Film.cu:121-276), Scene::transfer_data_to_device
+// (Scene.cu:363-470) and wavefront_pathtrace (wavefront_kernels.cu:377-442).
+// Differences by design: one stream, no host sync or managed-memory counter
+// readback between stages (counts stay on the device and the trace kernels are
+// persistent), a whole tile set per iteration instead of one 256x256 tile, and
+// error codes instead of exit(99).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+#include "mcpt.h"
+
+using namespace mcpt_dev;
+
+namespace mcpt_host {
+void set_global_error(const std::string& e);
+const char* global_error();
+}  // namespace mcpt_host
+
+struct mcpt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    mcpt_config cfg{};
+    char devname[256] = {0};
+    int num_cu = 0;
+    // scene
+    std::vector<void*> scene_bufs;
+    DevScene scene{};
+    bool has_scene = false;
+    int pair_depth = 0;
+    // camera
+    mcpt::CamView cam{};
+    bool has_cam = false;
+    // film + paths
+    uint32_t W = 0, H = 0, tile_w = 256, tile_h = 256;
+    size_t P = 0;
+    std::vector<void*> film_bufs;
+    DevPaths p{};
+    uint32_t *ext_q = nullptr, *any_q = nullptr;
+    CounterBlock* cnt = nullptr;
+    CounterBlock* cnt_host = nullptr;  // pinned
+    int2* tiles = nullptr;
+    std::vector<int2> tiles_h;
+    uint32_t tiles_cap = 0;
+    std::vector<hipEvent_t> events;
+    int trace_blocks[2] = {0, 0};
+    // stage_run scratch
+    std::vector<void*> tmp_bufs;
+};
+
+static int set_err(mcpt_ctx* c, int rc, const std::string& msg) {
+    if (c) c->err = msg;
+    mcpt_host::set_global_error(msg);
+    return rc;
+}
+#define HIPCHK(c, x)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess)                                                                 \
+            return set_err((c), MCPT_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_));  \
+    } while (0)
+
+static void free_list(std::vector<void*>& v) {
+    for (void* q : v)
+        if (q) (void)hipFree(q);
+    v.clear();
+}
+template <class T>
+static int dalloc(mcpt_ctx* c, std::vector<void*>& list, T** out, size_t count) {
+    void* q = nullptr;
+    size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) return set_err(c, MCPT_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    list.push_back(q);
+    *out = (T*)q;
+    return MCPT_OK;
+}
+template <class T>
+static int dupload(mcpt_ctx* c, std::vector<void*>& list, T** out, const T* src, size_t count) {
+    int rc = dalloc(c, list, out, count);
+    if (rc) return rc;
+    if (count) HIPCHK(c, hipMemcpy(*out, src, count * sizeof(T), hipMemcpyHostToDevice));
+    return MCPT_OK;
+}
+
+extern "C" {
+
+const char* mcpt_last_error(const mcpt_ctx* c) { return c ? c->err.c_str() : mcpt_host::global_error(); }
+
+int mcpt_create(int device, const mcpt_config* cfg, mcpt_ctx** out) {
+    if (!out) return set_err(nullptr, MCPT_E_INVALID, "out is null");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return set_err(nullptr, MCPT_E_NODEVICE, "no HIP device visible (the backend has no CPU fallback)");
+    if (device < 0 || device >= n) return set_err(nullptr, MCPT_E_INVALID, "device index out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+        return set_err(nullptr, MCPT_E_HIP, "hipGetDeviceProperties failed");
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_err(nullptr, MCPT_E_NODEVICE, std::string("device is ") + prop.gcnArchName + ", code objects are gfx950 only");
+    mcpt_ctx* c = new mcpt_ctx();
+    c->device = device;
+    c->num_cu = prop.multiProcessorCount;
+    snprintf(c->devname, sizeof(c->devname), "%s (%s, %d CUs)", prop.name, prop.gcnArchName, prop.multiProcessorCount);
+    if (cfg) c->cfg = *cfg;
+    else { c->cfg.seed = 0x5EED2026ull; c->cfg.spp = 16; c->cfg.max_depth = 5; c->cfg.rr_depth = 3; c->cfg.tile_w = 256; c->cfg.tile_h = 256; }
+    if (c->cfg.max_depth < 1 || c->cfg.max_depth > 200 || c->cfg.spp < 0) { delete c; return set_err(nullptr, MCPT_E_INVALID, "bad config"); }
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return set_err(nullptr, MCPT_E_HIP, "stream creation failed");
+    }
+    if (hipMalloc(&c->cnt, sizeof(CounterBlock)) != hipSuccess || hipHostMalloc(&c->cnt_host, sizeof(CounterBlock)) != hipSuccess) {
+        delete c;
+        return set_err(nullptr, MCPT_E_NOMEM, "counter allocation failed");
+    }
+    (void)hipMemset(c->cnt, 0, sizeof(CounterBlock));
+    for (int k = 0; k < 2; k++) {
+        int per_cu = 0;
+        // persistent grid: what the occupancy query admits per CU (a plain launch
+        // needs no co-residency here: surplus blocks simply find the queue empty)
+        (void)per_cu;
+        c->trace_blocks[k] = c->num_cu * 8;
+    }
+    *out = c;
+    return MCPT_OK;
+}
+
+void mcpt_destroy(mcpt_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_list(c->scene_bufs);
+    free_list(c->film_bufs);
+    free_list(c->tmp_bufs);
+    if (c->cnt) (void)hipFree(c->cnt);
+    if (c->cnt_host) (void)hipHostFree(c->cnt_host);
+    if (c->tiles) (void)hipFree(c->tiles);
+    for (auto e : c->events) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int mcpt_device_name(mcpt_ctx* c, char* buf, int32_t len) {
+    if (!c || !buf || len <= 0) return MCPT_E_INVALID;
+    snprintf(buf, (size_t)len, "%s", c->devname);
+    return MCPT_OK;
+}
+
+// Scene upload: LinearBVHNode (BVH.h:63-72) -> child-pair nodes, dTriangle
+// (Triangle.h:11-23, 288 B) -> 48-B intersection + 48-B shading records.
+int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) {
+    if (!c || !d) return set_err(c, MCPT_E_INVALID, "null argument");
+    if (d->ntri < 0 || d->nnodes < 0 || d->nmat < 0 || d->ndir < 0) return set_err(c, MCPT_E_INVALID, "negative sizes");
+    if (d->ntri >= (1 << 24)) return set_err(c, MCPT_E_INVALID, "more than 2^24 triangles");
+    if (d->ntri > 0 && d->nnodes == 0) return set_err(c, MCPT_E_INVALID, "triangles without BVH");
+    for (int32_t i = 0; i < d->ntri; i++)
+        if (d->mat[i] < 0 || d->mat[i] >= d->nmat) return set_err(c, MCPT_E_INVALID, "material id out of range");
+    if (d->env_mode == 1 && (!d->env_tex || !d->env_marginal_y || !d->env_conds_y || !d->env_pdf || d->env_w < 2 || d->env_h < 2))
+        return set_err(c, MCPT_E_INVALID, "HRDI env light without tables");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    free_list(c->scene_bufs);
+    c->has_scene = false;
+    const int N = d->nnodes;
+    // pair-node numbering of interior nodes + validation
+    std::vector<int> pair_of(N, -1);
+    int npair = 0;
+    for (int i = 0; i < N; i++) {
+        if (d->nprims[i] == 0) {
+            if (i + 1 >= N || d->offset[i] <= i || d->offset[i] >= N) return set_err(c, MCPT_E_INVALID, "bad BVH child offset");
+            pair_of[i] = npair++;
+        } else {
+            if (d->nprims[i] < 0 || d->nprims[i] > 8) return set_err(c, MCPT_E_INVALID, "leaf with more than 8 primitives");
+            if (d->offset[i] < 0 || d->offset[i] + d->nprims[i] > d->ntri) return set_err(c, MCPT_E_INVALID, "bad leaf range");
+        }
+    }
+    auto ref_of = [&](int j) -> int {
+        if (d->nprims[j] == 0) return pair_of[j];
+        return (int)(0x80000000u | ((uint32_t)(d->nprims[j] - 1) << 24) | (uint32_t)d->offset[j]);
+    };
+    std::vector<float4> pn((size_t)npair * 4);
+    for (int i = 0; i < N; i++) {
+        if (d->nprims[i] != 0) continue;
+        int c0 = i + 1, c1 = d->offset[i];
+        const float *a0 = d->bmin + 3 * c0, *b0 = d->bmax + 3 * c0, *a1 = d->bmin + 3 * c1, *b1 = d->bmax + 3 * c1;
+        float4* q = &pn[(size_t)pair_of[i] * 4];
+        q[0] = make_float4(a0[0], a0[1], a0[2], b0[0]);
+        q[1] = make_float4(b0[1], b0[2], a1[0], a1[1]);
+        q[2] = make_float4(a1[2], b1[0], b1[1], b1[2]);
+        int r0 = ref_of(c0), r1 = ref_of(c1);
+        float fr0, fr1, fax;
+        int ax = d->axis[i];
+        memcpy(&fr0, &r0, 4);
+        memcpy(&fr1, &r1, 4);
+        memcpy(&fax, &ax, 4);
+        q[3] = make_float4(fr0, fr1, fax, 0.f);
+    }
+    // depth of the tree = bound on stack pushes
+    int depth = 0;
+    if (N > 0) {
+        std::vector<std::pair<int, int>> st{{0, 0}};
+        while (!st.empty()) {
+            auto [n, dd] = st.back();
+            st.pop_back();
+            depth = std::max(depth, dd);
+            if (d->nprims[n] == 0) { st.push_back({n + 1, dd + 1}); st.push_back({d->offset[n], dd + 1}); }
+        }
+    }
+    if (depth > kMaxStack) return set_err(c, MCPT_E_INVALID, "BVH deeper than the 64-entry traversal stack");
+    c->pair_depth = depth;
+    std::vector<float4> tri((size_t)d->ntri * 3), sh((size_t)d->ntri * 3);
+    for (int32_t i = 0; i < d->ntri; i++) {
+        mcpt::V3 p0 = mcpt::ld3(d->v0, i), p1 = mcpt::ld3(d->v1, i), p2 = mcpt::ld3(d->v2, i);
+        mcpt::V3 e1 = p1 - p0, e2 = p2 - p0;  // Triangle.cu:13-14
+        tri[3 * i + 0] = make_float4(p0.x, p0.y, p0.z, e1.x);
+        tri[3 * i + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+        tri[3 * i + 2] = make_float4(e2.z, 0.f, 0.f, 0.f);
+        mcpt::V3 n0 = mcpt::ld3(d->n0, i), n1 = mcpt::ld3(d->n1, i), n2 = mcpt::ld3(d->n2, i);
+        float fm;
+        int mm = d->mat[i];
+        memcpy(&fm, &mm, 4);
+        sh[3 * i + 0] = make_float4(n0.x, n0.y, n0.z, n1.x);
+        sh[3 * i + 1] = make_float4(n1.y, n1.z, n2.x, n2.y);
+        sh[3 * i + 2] = make_float4(n2.z, fm, 0.f, 0.f);
+    }
+    DevScene s{};
+    float4 *dn, *dt, *dsh;
+    float *dm, *dd;
+    int rc;
+    if ((rc = dupload(c, c->scene_bufs, &dn, pn.data(), pn.size()))) return rc;
+    if ((rc = dupload(c, c->scene_bufs, &dt, tri.data(), tri.size()))) return rc;
+    if ((rc = dupload(c, c->scene_bufs, &dsh, sh.data(), sh.size()))) return rc;
+    if ((rc = dupload(c, c->scene_bufs, &dm, d->mat_params, (size_t)d->nmat * 8))) return rc;
+    if ((rc = dupload(c, c->scene_bufs, &dd, d->dir_params, (size_t)d->ndir * 7))) return rc;
+    s.nodes = dn; s.tri = dt; s.tri_sh = dsh; s.mats = dm; s.dirs = dd;
+    s.nlights = 1 + d->ndir;
+    if (N > 0) {
+        for (int k = 0; k < 3; k++) { s.root_mn[k] = d->bmin[k]; s.root_mx[k] = d->bmax[k]; }
+        s.root_ref = ref_of(0);
+    } else {
+        // empty scene: a root box that no ray can enter
+        for (int k = 0; k < 3; k++) { s.root_mn[k] = 1.f; s.root_mx[k] = -1.f; }
+        s.root_ref = 0;
+    }
+    s.env.mode = d->env_mode;
+    for (int k = 0; k < 3; k++) s.env.color[k] = d->env_color[k];
+    s.env.ls = d->env_ls;
+    s.env.w = d->env_w;
+    s.env.h = d->env_h;
+    s.env.tex = nullptr;
+    if (d->env_mode == 1) {
+        float4* tx;
+        float *my, *cy, *pd;
+        size_t WH = (size_t)d->env_w * d->env_h;
+        if ((rc = dupload(c, c->scene_bufs, &tx, reinterpret_cast<const float4*>(d->env_tex), WH))) return rc;
+        if ((rc = dupload(c, c->scene_bufs, &my, d->env_marginal_y, (size_t)d->env_h))) return rc;
+        if ((rc = dupload(c, c->scene_bufs, &cy, d->env_conds_y, WH))) return rc;
+        if ((rc = dupload(c, c->scene_bufs, &pd, d->env_pdf, WH))) return rc;
+        s.env.tex = tx; s.env.marginal_y = my; s.env.conds_y = cy; s.env.pdf = pd;
+    }
+    c->scene = s;
+    c->has_scene = true;
+    return MCPT_OK;
+}
+
+int mcpt_camera_set(mcpt_ctx* c, const mcpt_camera* cam) {
+    if (!c || !cam) return set_err(c, MCPT_E_INVALID, "null argument");
+    memcpy(c->cam.ivp, cam->inv_view_proj, sizeof(c->cam.ivp));
+    memcpy(c->cam.iv, cam->inv_view, sizeof(c->cam.iv));
+    c->cam.lens_radius = cam->lens_radius;
+    c->cam.focal = cam->focal;
+    c->has_cam = true;
+    return MCPT_OK;
+}
+
+static int set_tiles_internal(mcpt_ctx* c, const std::vector<int2>& t) {
+    if (t.size() > c->tiles_cap) {
+        if (c->tiles) HIPCHK(c, hipFree(c->tiles));
+        c->tiles = nullptr;
+        HIPCHK(c, hipMalloc(&c->tiles, std::max<size_t>(t.size(), 1) * sizeof(int2)));
+        c->tiles_cap = (uint32_t)t.size();
+    }
+    if (!t.empty()) HIPCHK(c, hipMemcpyAsync(c->tiles, t.data(), t.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->tiles_h = t;
+    return MCPT_OK;
+}
+static std::vector<int2> all_tiles(const mcpt_ctx* c) {
+    std::vector<int2> t;
+    uint32_t nx = (c->W + c->tile_w - 1) / c->tile_w, ny = (c->H + c->tile_h - 1) / c->tile_h;
+    for (uint32_t y = 0; y < ny; y++)
+        for (uint32_t x = 0; x < nx; x++) t.push_back(make_int2((int)x, (int)y));
+    return t;
+}
+
+int mcpt_film_clear(mcpt_ctx* c) {
+    if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
+    HIPCHK(c, hipSetDevice(c->device));
+    ClearArgs a{c->p.flags, c->p.samples, c->p.Ld, (uint32_t)c->P};
+    launch_clear(a, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemsetAsync(c->cnt, 0, sizeof(CounterBlock), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MCPT_OK;
+}
+
+int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t th) {
+    if (!c || w == 0 || h == 0 || tw == 0 || th == 0) return set_err(c, MCPT_E_INVALID, "bad film size");
+    if ((uint64_t)w * h >= (1ull << 31)) return set_err(c, MCPT_E_INVALID, "film too large");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    free_list(c->film_bufs);
+    c->P = 0;
+    c->W = w; c->H = h; c->tile_w = tw; c->tile_h = th;
+    size_t P = (size_t)w * h;
+    DevPaths p{};
+    int rc;
+    if ((rc = dalloc(c, c->film_bufs, &p.ray_o, P)) || (rc = dalloc(c, c->film_bufs, &p.ray_d, P)) ||
+        (rc = dalloc(c, c->film_bufs, &p.hit_p, P)) || (rc = dalloc(c, c->film_bufs, &p.hit_n, P)) ||
+        (rc = dalloc(c, c->film_bufs, &p.sray_o, 2 * P)) || (rc = dalloc(c, c->film_bufs, &p.sray_d, 2 * P)) ||
+        (rc = dalloc(c, c->film_bufs, &p.beta, P)) || (rc = dalloc(c, c->film_bufs, &p.nee0, P)) ||
+        (rc = dalloc(c, c->film_bufs, &p.nee1, P)) || (rc = dalloc(c, c->film_bufs, &p.Ld, P)) ||
+        (rc = dalloc(c, c->film_bufs, &p.flags, P)) || (rc = dalloc(c, c->film_bufs, &p.samples, P)) ||
+        (rc = dalloc(c, c->film_bufs, &p.vis, 2 * P)) || (rc = dalloc(c, c->film_bufs, &c->ext_q, P)) ||
+        (rc = dalloc(c, c->film_bufs, &c->any_q, 2 * P)))
+        return rc;
+    HIPCHK(c, hipMemset(p.hit_n, 0xff, P * sizeof(float4)));
+    HIPCHK(c, hipMemset(p.vis, 0, 2 * P));
+    c->p = p;
+    c->P = P;
+    int rc2 = set_tiles_internal(c, all_tiles(c));
+    if (rc2) return rc2;
+    return mcpt_film_clear(c);
+}
+
+int mcpt_set_tiles(mcpt_ctx* c, const uint32_t* xy, uint32_t n) {
+    if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!xy) return set_tiles_internal(c, all_tiles(c));
+    std::vector<int2> t;
+    uint32_t nx = (c->W + c->tile_w - 1) / c->tile_w, ny = (c->H + c->tile_h - 1) / c->tile_h;
+    for (uint32_t i = 0; i < n; i++) {
+        if (xy[2 * i] >= nx || xy[2 * i + 1] >= ny) return set_err(c, MCPT_E_INVALID, "tile out of range");
+        t.push_back(make_int2((int)xy[2 * i], (int)xy[2 * i + 1]));
+    }
+    return set_tiles_internal(c, t);
+}
+
+static hipEvent_t ev(mcpt_ctx* c, size_t i) {
+    while (c->events.size() <= i) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->events.push_back(e);
+    }
+    return c->events[i];
+}
+
+static int check_ready(mcpt_ctx* c) {
+    if (!c) return MCPT_E_INVALID;
+    if (!c->has_scene) return set_err(c, MCPT_E_INVALID, "no scene uploaded");
+    if (!c->has_cam) return set_err(c, MCPT_E_INVALID, "no camera set");
+    if (!c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
+    return MCPT_OK;
+}
+
+// One wavefront iteration over the current tile set: shade -> extend -> any-hit.
+static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
+    ShadeArgs sa;
+    sa.scene = c->scene;
+    sa.cam = c->cam;
+    sa.p = c->p;
+    sa.tiles = c->tiles;
+    sa.ntiles = (int)c->tiles_h.size();
+    sa.tile_w = (int)c->tile_w;
+    sa.tile_h = (int)c->tile_h;
+    sa.W = (int)c->W;
+    sa.H = (int)c->H;
+    sa.spp = c->cfg.spp;
+    sa.max_depth = c->cfg.max_depth;
+    sa.rr_depth = c->cfg.rr_depth;
+    sa.seed = c->cfg.seed;
+    sa.ext_q = c->ext_q;
+    sa.any_q = c->any_q;
+    sa.cnt = c->cnt;
+    int bpt = (int)((c->tile_w * c->tile_h + kBlock - 1) / kBlock);
+    if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 0), c->stream));
+    if (sa.ntiles > 0) launch_shade(sa, sa.ntiles * bpt, c->stream);
+    if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 1), c->stream));
+    TraceArgs ta{};
+    ta.scene = c->scene;
+    ta.ro = c->p.ray_o;
+    ta.rd = c->p.ray_d;
+    ta.queue = c->ext_q;
+    ta.count_ptr = &c->cnt->ext;
+    ta.work = &c->cnt->work_ext;
+    ta.hit_p = c->p.hit_p;
+    ta.hit_n = c->p.hit_n;
+    launch_trace(ta, false, c->trace_blocks[0], c->stream);
+    if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
+    TraceArgs tb{};
+    tb.scene = c->scene;
+    tb.ro = c->p.sray_o;
+    tb.rd = c->p.sray_d;
+    tb.queue = c->any_q;
+    tb.count_ptr = &c->cnt->any;
+    tb.work = &c->cnt->work_any;
+    tb.vis = c->p.vis;
+    launch_trace(tb, true, c->trace_blocks[1], c->stream);
+    if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 3), c->stream));
+    launch_accumulate(c->cnt, c->stream);
+    HIPCHK(c, hipGetLastError());
+    return MCPT_OK;
+}
+
+static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st) {
+    int rc = check_ready(c);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(c->cnt_host, c->cnt, sizeof(CounterBlock), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    CounterBlock before = *c->cnt_host;
+    for (uint32_t i = 0; i < n; i++) {
+        // events for at most the first 4096 iterations of a call
+        bool timing = i < 4096;
+        if ((rc = enqueue_iteration(c, (size_t)4 * i, timing))) return rc;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->cnt_host, c->cnt, sizeof(CounterBlock), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const CounterBlock& after = *c->cnt_host;
+    if (st) {
+        memset(st, 0, sizeof(*st));
+        st->extend_rays = after.tot_ext - before.tot_ext;
+        st->vis_rays = after.tot_vis - before.tot_vis;
+        st->shadow_rays = (after.tot_any - before.tot_any) - st->vis_rays;
+        st->iterations = n;
+        st->live_paths = after.last_ext;
+        uint32_t tn = std::min<uint32_t>(n, 4096);
+        for (uint32_t i = 0; i < tn; i++) {
+            float a = 0, b = 0, d = 0;
+            HIPCHK(c, hipEventElapsedTime(&a, c->events[4 * i + 0], c->events[4 * i + 1]));
+            HIPCHK(c, hipEventElapsedTime(&b, c->events[4 * i + 1], c->events[4 * i + 2]));
+            HIPCHK(c, hipEventElapsedTime(&d, c->events[4 * i + 2], c->events[4 * i + 3]));
+            st->ms_shade += a;
+            st->ms_extend += b;
+            st->ms_shadow += d;
+        }
+        st->ms_total = st->ms_shade + st->ms_extend + st->ms_shadow;
+    }
+    return MCPT_OK;
+}
+
+int mcpt_iterate(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st) { return run_iterations(c, n, st); }
+
+int mcpt_wavefront_step(mcpt_ctx* c, uint32_t tx, uint32_t ty, mcpt_stage_stats* st) {
+    int rc = check_ready(c);
+    if (rc) return rc;
+    uint32_t nx = (c->W + c->tile_w - 1) / c->tile_w, ny = (c->H + c->tile_h - 1) / c->tile_h;
+    if (tx >= nx || ty >= ny) return set_err(c, MCPT_E_INVALID, "tile out of range");
+    std::vector<int2> saved = c->tiles_h;
+    if ((rc = set_tiles_internal(c, {make_int2((int)tx, (int)ty)}))) return rc;
+    rc = run_iterations(c, 1, st);
+    int rc2 = set_tiles_internal(c, saved);
+    return rc ? rc : rc2;
+}
+
+int mcpt_render(mcpt_ctx* c, mcpt_stage_stats* st) {
+    int rc = check_ready(c);
+    if (rc) return rc;
+    mcpt_stage_stats acc{}, one{};
+    const uint64_t cap = (uint64_t)(c->cfg.spp + 1) * (uint64_t)(c->cfg.max_depth + 2) + 16;
+    uint64_t done = 0;
+    for (;;) {
+        if ((rc = run_iterations(c, 32, &one))) return rc;
+        acc.extend_rays += one.extend_rays;
+        acc.shadow_rays += one.shadow_rays;
+        acc.vis_rays += one.vis_rays;
+        acc.iterations += one.iterations;
+        acc.ms_shade += one.ms_shade;
+        acc.ms_extend += one.ms_extend;
+        acc.ms_shadow += one.ms_shadow;
+        acc.ms_total += one.ms_total;
+        acc.live_paths = one.live_paths;
+        done += 32;
+        if (one.live_paths == 0 || done > cap) break;
+    }
+    if (st) *st = acc;
+    if (acc.live_paths != 0) return set_err(c, MCPT_E_INVALID, "render did not converge within the iteration cap");
+    return MCPT_OK;
+}
+
+int mcpt_sync(mcpt_ctx* c) {
+    if (!c) return MCPT_E_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MCPT_OK;
+}
+
+int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_view* out, uint32_t n) {
+    if (!c || !in || !out) return set_err(c, MCPT_E_INVALID, "null argument");
+    if (!c->has_scene) return set_err(c, MCPT_E_INVALID, "no scene uploaded");
+    if (stage != MCPT_STAGE_EXTEND && stage != MCPT_STAGE_SHADOW)
+        return set_err(c, MCPT_E_INVALID, "stage not separately exposed: logic/generate/material are fused into k_shade");
+    if (n == 0) return MCPT_OK;
+    if (!in->ray_o || !in->ray_d) return set_err(c, MCPT_E_INVALID, "null rays");
+    if (stage == MCPT_STAGE_EXTEND && (!out->hit_pos_t || !out->hit_nrm_mat)) return set_err(c, MCPT_E_INVALID, "null outputs");
+    if (stage == MCPT_STAGE_SHADOW && !out->visible) return set_err(c, MCPT_E_INVALID, "null outputs");
+    HIPCHK(c, hipSetDevice(c->device));
+    free_list(c->tmp_bufs);
+    std::vector<float4> ro(n), rd(n);
+    for (uint32_t i = 0; i < n; i++) {
+        ro[i] = make_float4(in->ray_o[3 * i], in->ray_o[3 * i + 1], in->ray_o[3 * i + 2], 0.f);
+        rd[i] = make_float4(in->ray_d[3 * i], in->ray_d[3 * i + 1], in->ray_d[3 * i + 2], 0.f);
+    }
+    float4 *dro, *drd, *hp = nullptr, *hn = nullptr;
+    int32_t* ht = nullptr;
+    uint8_t* vis = nullptr;
+    uint32_t* work;
+    int rc;
+    if ((rc = dupload(c, c->tmp_bufs, &dro, ro.data(), n)) || (rc = dupload(c, c->tmp_bufs, &drd, rd.data(), n)) ||
+        (rc = dalloc(c, c->tmp_bufs, &work, 4)))
+        return rc;
+    HIPCHK(c, hipMemset(work, 0, 16));
+    TraceArgs ta{};
+    ta.scene = c->scene;
+    ta.ro = dro;
+    ta.rd = drd;
+    ta.count = n;
+    ta.work = work;
+    if (stage == MCPT_STAGE_EXTEND) {
+        if ((rc = dalloc(c, c->tmp_bufs, &hp, n)) || (rc = dalloc(c, c->tmp_bufs, &hn, n)) || (rc = dalloc(c, c->tmp_bufs, &ht, n)))
+            return rc;
+        ta.hit_p = hp;
+        ta.hit_n = hn;
+        ta.hit_tri = ht;
+    } else {
+        if ((rc = dalloc(c, c->tmp_bufs, &vis, n))) return rc;
+        ta.vis = vis;
+    }
+    launch_trace(ta, stage == MCPT_STAGE_SHADOW, c->trace_blocks[0], c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (stage == MCPT_STAGE_EXTEND) {
+        std::vector<float4> a(n), b(n);
+        HIPCHK(c, hipMemcpy(a.data(), hp, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(b.data(), hn, n * sizeof(float4), hipMemcpyDeviceToHost));
+        std::vector<int32_t> t(n);
+        HIPCHK(c, hipMemcpy(t.data(), ht, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; i++) {
+            out->hit_pos_t[4 * i + 0] = a[i].x; out->hit_pos_t[4 * i + 1] = a[i].y;
+            out->hit_pos_t[4 * i + 2] = a[i].z; out->hit_pos_t[4 * i + 3] = a[i].w;
+            int m;
+            memcpy(&m, &b[i].w, 4);
+            out->hit_nrm_mat[4 * i + 0] = b[i].x; out->hit_nrm_mat[4 * i + 1] = b[i].y;
+            out->hit_nrm_mat[4 * i + 2] = b[i].z; out->hit_nrm_mat[4 * i + 3] = (float)m;
+            if (out->hit_tri) out->hit_tri[i] = t[i];
+        }
+    } else {
+        HIPCHK(c, hipMemcpy(out->visible, vis, n, hipMemcpyDeviceToHost));
+    }
+    free_list(c->tmp_bufs);
+    return MCPT_OK;
+}
+
+int mcpt_film_read(mcpt_ctx* c, float* Ld, uint32_t* samples) {
+    if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (Ld) {
+        std::vector<float4> tmp(c->P);
+        HIPCHK(c, hipMemcpy(tmp.data(), c->p.Ld, c->P * sizeof(float4), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < c->P; i++) { Ld[3 * i] = tmp[i].x; Ld[3 * i + 1] = tmp[i].y; Ld[3 * i + 2] = tmp[i].z; }
+    }
+    if (samples) HIPCHK(c, hipMemcpy(samples, c->p.samples, c->P * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return MCPT_OK;
+}
+
+int mcpt_film_read_device(mcpt_ctx* c, void* dLd, void* dsamples) {
+    if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (dLd) HIPCHK(c, hipMemcpyAsync(dLd, c->p.Ld, c->P * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+    if (dsamples) HIPCHK(c, hipMemcpyAsync(dsamples, c->p.samples, c->P * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MCPT_OK;
+}
+
+int mcpt_film_pack_tiles(mcpt_ctx* c, void* d_out, uint32_t* npix) {
+    if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
+    uint32_t n = (uint32_t)(c->tiles_h.size() * c->tile_w * c->tile_h);
+    if (npix) *npix = n;
+    if (!d_out) return MCPT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    PackArgs a{c->p.Ld, c->p.samples, c->tiles, (int)c->tiles_h.size(), (int)c->tile_w, (int)c->tile_h, (int)c->W, (int)c->H, (float4*)d_out};
+    if (n) launch_pack(a, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MCPT_OK;
+}
+
+int mcpt_film_tonemap_rgba8(mcpt_ctx* c, float exposure, uint8_t* out) {
+    if (!c || !c->P || !out) return set_err(c, MCPT_E_INVALID, "bad argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    uchar4* d = nullptr;
+    HIPCHK(c, hipMalloc(&d, c->P * sizeof(uchar4)));
+    TonemapArgs a{c->p.Ld, c->p.samples, d, exposure, (uint32_t)c->P};
+    launch_tonemap(a, c->stream);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, d, c->P * sizeof(uchar4), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return set_err(c, MCPT_E_HIP, std::string("tonemap: ") + hipGetErrorString(e));
+    return MCPT_OK;
+}
+
+}  // extern "C"

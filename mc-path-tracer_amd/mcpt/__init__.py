@@ -1,0 +1,411 @@
+"""mcpt -- Python view of the MI355X wavefront path-tracing backend (ctypes over include/mcpt.h).
+
+The product is the C ABI in ``libmcpt.so`` (HIP kernels for gfx950 + host C++).  This module
+is the thin Python mirror of the reference's host objects, used by tests/ and bench.py:
+
+* :class:`Scene`      -- ``Scene::load`` / ``set_environment_light`` / ``add_light``
+                         (CUDA-RayTracer/Scene.h:40-58) plus the BVH build (BVH.cu).
+* :class:`PathTracer` -- ``PathTracer::render_image`` (PathTracer.cpp:112-130) and the
+                         ``wavefront_pathtrace`` / ``clear_dfilm`` entry points
+                         (wavefront_kernels.cuh:18-31), on one device.
+* :func:`make_camera` -- ``Camera::update`` matrices (Camera.cu:194-224).
+
+There is no CPU fallback: constructing a :class:`PathTracer` without a gfx950 device raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "libmcpt.so")
+ASSET_DIR = os.path.join(REPO_DIR, "assets")
+
+MCPT_OK = 0
+STAGE_LOGIC, STAGE_GENERATE, STAGE_MATERIAL, STAGE_EXTEND, STAGE_SHADOW = range(5)
+
+_f = C.POINTER(C.c_float)
+_i = C.POINTER(C.c_int32)
+_u = C.POINTER(C.c_uint32)
+
+
+class Config(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("spp", C.c_int32), ("max_depth", C.c_int32), ("rr_depth", C.c_int32),
+                ("tile_w", C.c_int32), ("tile_h", C.c_int32), ("flags", C.c_int32)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("ntri", C.c_int32), ("v0", _f), ("v1", _f), ("v2", _f), ("n0", _f), ("n1", _f), ("n2", _f),
+                ("mat", _i), ("nnodes", C.c_int32), ("bmin", _f), ("bmax", _f), ("offset", _i), ("nprims", _i),
+                ("axis", _i), ("nmat", C.c_int32), ("mat_params", _f), ("ndir", C.c_int32), ("dir_params", _f),
+                ("env_mode", C.c_int32), ("env_color", C.c_float * 3), ("env_ls", C.c_float),
+                ("env_w", C.c_int32), ("env_h", C.c_int32), ("env_tex", _f), ("env_marginal_y", _f),
+                ("env_conds_y", _f), ("env_pdf", _f)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("inv_view_proj", C.c_float * 16), ("inv_view", C.c_float * 16), ("lens_radius", C.c_float),
+                ("focal", C.c_float)]
+
+
+class CameraParams(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("yaw_deg", C.c_float), ("pitch_deg", C.c_float),
+                ("fovy_rad", C.c_float), ("aspect", C.c_float), ("znear", C.c_float), ("zfar", C.c_float),
+                ("lens_radius", C.c_float), ("focal", C.c_float)]
+
+
+class StageStats(C.Structure):
+    _fields_ = [("extend_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("vis_rays", C.c_uint64),
+                ("iterations", C.c_uint64), ("live_paths", C.c_uint64), ("ms_total", C.c_float),
+                ("ms_shade", C.c_float), ("ms_extend", C.c_float), ("ms_shadow", C.c_float)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+    @property
+    def rays(self) -> int:
+        return int(self.extend_rays + self.shadow_rays + self.vis_rays)
+
+
+class SoaView(C.Structure):
+    _fields_ = [("ray_o", _f), ("ray_d", _f), ("hit_pos_t", _f), ("hit_nrm_mat", _f), ("hit_tri", _i),
+                ("visible", C.POINTER(C.c_uint8))]
+
+
+# Every symbol declared in include/mcpt.h with its ctypes signature.
+ABI = {
+    "mcpt_create": (C.c_int, [C.c_int, C.POINTER(Config), C.POINTER(C.c_void_p)]),
+    "mcpt_destroy": (None, [C.c_void_p]),
+    "mcpt_last_error": (C.c_char_p, [C.c_void_p]),
+    "mcpt_scene_upload": (C.c_int, [C.c_void_p, C.POINTER(SceneDesc)]),
+    "mcpt_camera_set": (C.c_int, [C.c_void_p, C.POINTER(Camera)]),
+    "mcpt_film_resize": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "mcpt_film_clear": (C.c_int, [C.c_void_p]),
+    "mcpt_set_tiles": (C.c_int, [C.c_void_p, _u, C.c_uint32]),
+    "mcpt_wavefront_step": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(StageStats)]),
+    "mcpt_iterate": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(StageStats)]),
+    "mcpt_render": (C.c_int, [C.c_void_p, C.POINTER(StageStats)]),
+    "mcpt_stage_run": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(SoaView), C.POINTER(SoaView), C.c_uint32]),
+    "mcpt_film_read": (C.c_int, [C.c_void_p, _f, _u]),
+    "mcpt_film_read_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mcpt_film_pack_tiles": (C.c_int, [C.c_void_p, C.c_void_p, _u]),
+    "mcpt_film_tonemap_rgba8": (C.c_int, [C.c_void_p, C.c_float, C.POINTER(C.c_uint8)]),
+    "mcpt_sync": (C.c_int, [C.c_void_p]),
+    "mcpt_device_name": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
+    "mcpt_scene_new": (C.c_void_p, []),
+    "mcpt_scene_free": (None, [C.c_void_p]),
+    "mcpt_scene_load_glb": (C.c_int, [C.c_void_p, C.c_char_p, _f]),
+    "mcpt_scene_add_mesh": (C.c_int, [C.c_void_p, C.c_int32, _f, _f, _f, _f, _f, _f, _f]),
+    "mcpt_scene_set_env_hdr": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
+    "mcpt_scene_set_env_color": (C.c_int, [C.c_void_p, _f, C.c_float]),
+    "mcpt_scene_add_dir_light": (C.c_int, [C.c_void_p, _f, _f, C.c_float]),
+    "mcpt_scene_transform": (C.c_int, [C.c_void_p, _f]),
+    "mcpt_scene_make_proxy": (C.c_int, [C.c_void_p, C.c_int32, C.c_char_p]),
+    "mcpt_scene_build": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mcpt_scene_get_desc": (C.c_int, [C.c_void_p, C.POINTER(SceneDesc)]),
+    "mcpt_scene_bvh_depth": (C.c_int, [C.c_void_p]),
+    "mcpt_camera_make": (C.c_int, [C.POINTER(CameraParams), C.POINTER(Camera)]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libmcpt.so (in-tree build).  Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() (make) first")
+        l = C.CDLL(LIB_PATH)
+        for name, (res, args) in ABI.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+class McptError(RuntimeError):
+    pass
+
+
+def _check(rc: int, ctx=None):
+    if rc != MCPT_OK:
+        msg = lib().mcpt_last_error(ctx)
+        raise McptError(f"mcpt error {rc}: {msg.decode() if msg else ''}")
+
+
+def fptr(a: np.ndarray):
+    return a.ctypes.data_as(_f)
+
+
+def default_config(spp=16, max_depth=5, rr_depth=3, seed=0x5EED2026, tile=256) -> Config:
+    return Config(seed, spp, max_depth, rr_depth, tile, tile, 0)
+
+
+def make_camera(position, yaw_deg=-90.0, pitch_deg=0.0, fovy_deg=45.0, aspect=1.0, znear=0.01, zfar=1e4,
+                lens_radius=1e-4, focal=35.0) -> Camera:
+    """PerspectiveCamera + Camera::update (Camera.cu:194-224) -> dCamera matrices."""
+    p = CameraParams((C.c_float * 3)(*position), yaw_deg, pitch_deg, np.float32(np.radians(np.float32(fovy_deg))),
+                     aspect, znear, zfar, lens_radius, focal)
+    cam = Camera()
+    _check(lib().mcpt_camera_make(C.byref(p), C.byref(cam)))
+    return cam
+
+
+def _arr(ptr, n, dtype):
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype)
+    ct = {np.float32: C.c_float, np.int32: C.c_int32}[dtype]
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(n,)).copy()
+
+
+class Scene:
+    """Host scene builder (Scene.cu) -- owns flat BVH-ordered arrays after build()."""
+
+    def __init__(self):
+        self.h = lib().mcpt_scene_new()
+        if not self.h:
+            raise McptError("mcpt_scene_new failed")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().mcpt_scene_free(self.h)
+            self.h = None
+
+    def _ck(self, rc):
+        _check(rc)
+        return self
+
+    def load_glb(self, path, xform=None):
+        xf = None if xform is None else fptr(np.ascontiguousarray(xform, np.float32).reshape(16))
+        return self._ck(lib().mcpt_scene_load_glb(self.h, str(path).encode(), xf))
+
+    def add_mesh(self, v0, v1, v2, n0, n1, n2, base_rgb=(1.0, 1.0, 1.0)):
+        arrs = [np.ascontiguousarray(a, np.float32).reshape(-1, 3) for a in (v0, v1, v2, n0, n1, n2)]
+        bc = np.asarray(base_rgb, np.float32)
+        return self._ck(lib().mcpt_scene_add_mesh(self.h, len(arrs[0]), *[fptr(a) for a in arrs], fptr(bc)))
+
+    def set_env_hdr(self, path, mode=1):
+        return self._ck(lib().mcpt_scene_set_env_hdr(self.h, str(path).encode(), mode))
+
+    def set_env_color(self, rgb, ls=1.0):
+        return self._ck(lib().mcpt_scene_set_env_color(self.h, fptr(np.asarray(rgb, np.float32)), ls))
+
+    def add_dir_light(self, direction, rgb, ls=1.0):
+        return self._ck(lib().mcpt_scene_add_dir_light(self.h, fptr(np.asarray(direction, np.float32)),
+                                                       fptr(np.asarray(rgb, np.float32)), ls))
+
+    def transform(self, xform):
+        return self._ck(lib().mcpt_scene_transform(self.h, fptr(np.ascontiguousarray(xform, np.float32).reshape(16))))
+
+    def make_proxy(self, config_id, asset_dir=ASSET_DIR):
+        return self._ck(lib().mcpt_scene_make_proxy(self.h, config_id, str(asset_dir).encode()))
+
+    def build(self, max_prims=8):
+        return self._ck(lib().mcpt_scene_build(self.h, max_prims))
+
+    def desc(self) -> SceneDesc:
+        d = SceneDesc()
+        _check(lib().mcpt_scene_get_desc(self.h, C.byref(d)))
+        d._owner = self  # keep arrays alive
+        return d
+
+    @property
+    def bvh_depth(self) -> int:
+        return lib().mcpt_scene_bvh_depth(self.h)
+
+    def arrays(self) -> dict:
+        """Copies of the built arrays as numpy (for oracles, tests and fixtures)."""
+        d = self.desc()
+        T, N = d.ntri, d.nnodes
+        out = {k: _arr(getattr(d, k), 3 * T, np.float32).reshape(T, 3) for k in ("v0", "v1", "v2", "n0", "n1", "n2")}
+        out["mat"] = _arr(d.mat, T, np.int32)
+        out["bmin"] = _arr(d.bmin, 3 * N, np.float32).reshape(N, 3)
+        out["bmax"] = _arr(d.bmax, 3 * N, np.float32).reshape(N, 3)
+        for k in ("offset", "nprims", "axis"):
+            out[k] = _arr(getattr(d, k), N, np.int32)
+        out["mat_params"] = _arr(d.mat_params, 8 * d.nmat, np.float32).reshape(d.nmat, 8)
+        out["dir_params"] = _arr(d.dir_params, 7 * d.ndir, np.float32).reshape(d.ndir, 7)
+        out["env_mode"] = d.env_mode
+        out["env_color"] = np.array(list(d.env_color), np.float32)
+        out["env_ls"] = np.float32(d.env_ls)
+        W, H = d.env_w, d.env_h
+        out["env_tex"] = _arr(d.env_tex, 4 * W * H, np.float32).reshape(H, W, 4)
+        out["env_marginal_y"] = _arr(d.env_marginal_y, H, np.float32)
+        out["env_conds_y"] = _arr(d.env_conds_y, W * H, np.float32).reshape(H, W)
+        out["env_pdf"] = _arr(d.env_pdf, W * H, np.float32).reshape(H, W)
+        return out
+
+
+def desc_from_arrays(a: dict) -> SceneDesc:
+    """SceneDesc pointing at numpy arrays in ``a`` (kept alive on the returned object)."""
+    keep = {}
+
+    def f(k):
+        arr = np.ascontiguousarray(a[k], np.float32)
+        keep[k] = arr
+        return arr.ctypes.data_as(_f) if arr.size else None
+
+    def i(k):
+        arr = np.ascontiguousarray(a[k], np.int32)
+        keep[k] = arr
+        return arr.ctypes.data_as(_i) if arr.size else None
+
+    d = SceneDesc()
+    d.ntri = len(a["mat"])
+    d.v0, d.v1, d.v2, d.n0, d.n1, d.n2 = (f(k) for k in ("v0", "v1", "v2", "n0", "n1", "n2"))
+    d.mat = i("mat")
+    d.nnodes = len(a["nprims"])
+    d.bmin, d.bmax = f("bmin"), f("bmax")
+    d.offset, d.nprims, d.axis = i("offset"), i("nprims"), i("axis")
+    d.nmat = len(a["mat_params"])
+    d.mat_params = f("mat_params")
+    d.ndir = len(a["dir_params"])
+    d.dir_params = f("dir_params")
+    d.env_mode = int(a["env_mode"])
+    for k in range(3):
+        d.env_color[k] = float(a["env_color"][k])
+    d.env_ls = float(a["env_ls"])
+    tex = np.asarray(a["env_tex"])
+    d.env_h, d.env_w = (tex.shape[0], tex.shape[1]) if tex.size else (0, 0)
+    d.env_tex, d.env_marginal_y, d.env_conds_y, d.env_pdf = (f(k) for k in ("env_tex", "env_marginal_y", "env_conds_y", "env_pdf"))
+    d._keep = keep
+    return d
+
+
+class PathTracer:
+    """Device context (one GPU): the reference's PathTracer + Film device state."""
+
+    def __init__(self, device=0, config: Config | None = None):
+        self.cfg = config or default_config()
+        h = C.c_void_p()
+        _check(lib().mcpt_create(device, C.byref(self.cfg), C.byref(h)))
+        self.h = h
+        self.W = self.H = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mcpt_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def _ck(self, rc):
+        _check(rc, self.h)
+
+    @property
+    def device_name(self) -> str:
+        buf = C.create_string_buffer(256)
+        self._ck(lib().mcpt_device_name(self.h, buf, 256))
+        return buf.value.decode()
+
+    def upload_scene(self, scene):
+        d = scene.desc() if isinstance(scene, Scene) else scene
+        self._ck(lib().mcpt_scene_upload(self.h, C.byref(d)))
+
+    def set_camera(self, cam: Camera):
+        self._ck(lib().mcpt_camera_set(self.h, C.byref(cam)))
+
+    def resize(self, W, H, tile_w=256, tile_h=256):
+        self._ck(lib().mcpt_film_resize(self.h, W, H, tile_w, tile_h))
+        self.W, self.H, self.tile_w, self.tile_h = W, H, tile_w, tile_h
+
+    def clear(self):
+        self._ck(lib().mcpt_film_clear(self.h))
+
+    def set_tiles(self, tiles=None):
+        if tiles is None:
+            self._ck(lib().mcpt_set_tiles(self.h, None, 0))
+        else:
+            t = np.ascontiguousarray(tiles, np.uint32).reshape(-1, 2)
+            self._ck(lib().mcpt_set_tiles(self.h, t.ctypes.data_as(_u), len(t)))
+
+    def step(self, tile_x, tile_y) -> StageStats:
+        st = StageStats()
+        self._ck(lib().mcpt_wavefront_step(self.h, tile_x, tile_y, C.byref(st)))
+        return st
+
+    def iterate(self, n) -> StageStats:
+        st = StageStats()
+        self._ck(lib().mcpt_iterate(self.h, n, C.byref(st)))
+        return st
+
+    def render(self) -> StageStats:
+        st = StageStats()
+        self._ck(lib().mcpt_render(self.h, C.byref(st)))
+        return st
+
+    def film(self):
+        P = self.W * self.H
+        Ld = np.zeros(3 * P, np.float32)
+        s = np.zeros(P, np.uint32)
+        self._ck(lib().mcpt_film_read(self.h, fptr(Ld), s.ctypes.data_as(_u)))
+        return Ld.reshape(self.H, self.W, 3), s.reshape(self.H, self.W)
+
+    def tonemap(self, exposure=1.0):
+        out = np.zeros(self.W * self.H * 4, np.uint8)
+        self._ck(lib().mcpt_film_tonemap_rgba8(self.h, exposure, out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out.reshape(self.H, self.W, 4)
+
+    def trace_closest(self, ro, rd):
+        ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
+        rd = np.ascontiguousarray(rd, np.float32).reshape(-1, 3)
+        n = len(ro)
+        pos_t = np.zeros((n, 4), np.float32)
+        nrm = np.zeros((n, 4), np.float32)
+        tri = np.zeros(n, np.int32)
+        vin = SoaView(fptr(ro), fptr(rd), None, None, None, None)
+        vout = SoaView(None, None, fptr(pos_t), fptr(nrm), tri.ctypes.data_as(_i), None)
+        self._ck(lib().mcpt_stage_run(self.h, STAGE_EXTEND, C.byref(vin), C.byref(vout), n))
+        return pos_t, nrm, tri
+
+    def trace_any(self, ro, rd):
+        ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
+        rd = np.ascontiguousarray(rd, np.float32).reshape(-1, 3)
+        n = len(ro)
+        vis = np.zeros(n, np.uint8)
+        vin = SoaView(fptr(ro), fptr(rd), None, None, None, None)
+        vout = SoaView(None, None, None, None, None, vis.ctypes.data_as(C.POINTER(C.c_uint8)))
+        self._ck(lib().mcpt_stage_run(self.h, STAGE_SHADOW, C.byref(vin), C.byref(vout), n))
+        return vis
+
+
+@dataclass(frozen=True)
+class RenderConfig:
+    """BASELINE.json configs."""
+    cid: int
+    width: int
+    height: int
+    spp: int
+    max_depth: int
+    position: tuple
+    yaw: float = -90.0
+    pitch: float = 0.0
+    fovy: float = 45.0
+
+
+CONFIGS = {
+    1: RenderConfig(1, 256, 256, 16, 3, (0.0, 0.0, 4.0)),
+    2: RenderConfig(2, 1920, 1080, 256, 5, (0.0, 0.0, 3.5)),
+    3: RenderConfig(3, 1920, 1080, 256, 5, (0.0, 1.5, 4.5), pitch=-10.0),
+    4: RenderConfig(4, 3840, 2160, 1024, 8, (0.0, 0.0, 2.5)),
+    5: RenderConfig(5, 4096, 4096, 4096, 12, (0.0, 1.2, 3.0), pitch=-5.0),
+}
+
+
+def build_config_scene(cid: int, asset_dir=ASSET_DIR) -> Scene:
+    s = Scene()
+    s.make_proxy(cid, asset_dir)
+    s.build(8)
+    return s
+
+
+def config_camera(rc: RenderConfig, width=None, height=None) -> Camera:
+    w, h = width or rc.width, height or rc.height
+    return make_camera(rc.position, rc.yaw, rc.pitch, rc.fovy, aspect=np.float32(w) / np.float32(h))

@@ -1,0 +1,116 @@
+/*
+ * mcpt_oracle.h -- CPU restatement of the MC-Path-Tracer wavefront hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (mc-path-tracer_amd/) may
+ * include, link or call this.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py load liboracle.so, and only as the checker.
+ *
+ * Parity status: PARTIALLY PINNED.  The reference (CUDA 11.8 / MSVC / OpenGL)
+ * cannot be compiled or run in this image, and it ships
+ * no tests or golden vectors.  The restatement is pinned by:
+ *   - the reference's only self-check, sum(env pdf) ~= 1
+ *     (light_initialization_kernels.cu:113-133),
+ *   - the README BRDF formulas (README.md:74-124) as known-answer tests,
+ *   - independent re-derivations in tests/ (numpy lowerbias32/splitmix64,
+ *     glibc transcendentals within a stated ULP bound, brute-force ray casts).
+ * Third-party arithmetic the reference delegates (CUDA texture filtering,
+ * stb_image, glm, CUDA fast-math transcendentals) is restated and UNPINNED.
+ *
+ * Every function cites the reference file:line it restates, relative to
+ * /root/reference/CUDA-RayTracer/ (cuda_math/ for the math core).
+ */
+#ifndef MCPT_ORACLE_H
+#define MCPT_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Scene arrays (already BVH-ordered).  Triangles are in world space: the
+ * reference bakes node transforms into vertices (Scene.cu:224) and keeps an
+ * identity dTransform, so Triangle.cu:69/82/86 transforms are exact no-ops. */
+typedef struct or_scene {
+    int32_t ntri;
+    const float *v0, *v1, *v2;      /* 3*ntri positions                   */
+    const float *n0, *n1, *n2;      /* 3*ntri vertex normals              */
+    const int32_t *mat;             /* ntri material id                   */
+    int32_t nnodes;                 /* LinearBVHNode (BVH.h:63-72)        */
+    const float *bmin, *bmax;       /* 3*nnodes                           */
+    const int32_t *offset;          /* primitivesOffset / secondChildOffset */
+    const int32_t *nprims;          /* 0 => interior                      */
+    const int32_t *axis;
+    int32_t nmat;
+    const float *mat_params;        /* nmat*8: base rgb, fresnel rgb, roughness, metallic */
+    int32_t ndir;                   /* directional lights after the env light */
+    const float *dir_params;        /* ndir*7: dir xyz, color rgb, ls     */
+    int32_t env_mode;               /* 0 = Color, 1 = HRDI (EnvironmentLight.h:11-15) */
+    float env_color[3];
+    float env_ls;
+    int32_t env_w, env_h;
+    const float *env_tex;           /* env_h*env_w*4 RGBA32F, row 0 = top */
+    const float *env_marginal_y;    /* env_h                              */
+    const float *env_conds_y;       /* env_h*env_w                        */
+    const float *env_pdf;           /* env_h*env_w                        */
+} or_scene;
+
+typedef struct or_camera {
+    float inv_view_proj[16];        /* column-major m[c][r] = m[c*4+r] (Matrix.h:12-95) */
+    float inv_view[16];
+    float lens_radius;
+    float focal;
+} or_camera;
+
+typedef struct or_config {
+    uint64_t seed;
+    int32_t spp;          /* gates processing and new samples (wavefront_kernels.cu:124,219) */
+    int32_t max_depth;    /* 'path_length > 5' (wavefront_kernels.cu:142,148) */
+    int32_t rr_depth;     /* 'path_length > 3' (wavefront_kernels.cu:189)      */
+    int32_t tile_w, tile_h;
+    int32_t nthreads;
+    int32_t traversal;    /* 0 = reference stack traversal, 1 = brute force   */
+    int32_t row_begin, row_end;  /* restrict to rows [begin,end); 0,0 = all */
+} or_config;
+
+/* counters[0]=extension rays, [1]=shadow rays, [2]=BRDF visibility rays,
+ * [3]=wavefront iterations (summed over tiles), [4]=BVH nodes visited,
+ * [5]=triangle tests. */
+int or_render(const or_scene *sc, const or_camera *cam, const or_config *cfg,
+              int32_t W, int32_t H, float *Ld, uint32_t *samples, uint64_t *counters);
+
+/* Batch ray casts (Triangle.cu:144-203 / 204-243).  hit_f4 per ray:
+ * pos.xyz, t ; nrm_f4: normal.xyz, (float)mat (mat=-1 on miss); tri: index or -1 */
+void or_trace_closest(const or_scene *sc, int32_t n, const float *ro, const float *rd,
+                      int32_t traversal, float *pos_t, float *nrm_mat, int32_t *tri);
+void or_trace_any(const or_scene *sc, int32_t n, const float *ro, const float *rd,
+                  int32_t traversal, uint8_t *visible);
+
+/* Env tables (light_initialization_kernels.cu:3-112). out_pdf_denom may be NULL. */
+void or_env_build(int32_t W, int32_t H, const float *tex, float *marginal_y,
+                  float *marginal_p, float *conds_y, float *pdf, float *out_pdf_denom);
+
+/* Known-answer hooks. */
+float or_sinf(float x);
+float or_cosf(float x);
+float or_asinf(float x);
+float or_acosf(float x);
+float or_atan2f(float y, float x);
+uint32_t or_lowerbias32(uint32_t x);
+uint64_t or_splitmix64(uint64_t z);
+float or_rand(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t len, uint32_t slot);
+void or_env_fetch(const or_scene *sc, float u, float v, float *rgb);
+float or_env_pdf(const or_scene *sc, float dx, float dy, float dz);
+void or_env_dir(const or_scene *sc, float ex, float ey, float *wi);
+/* BRDF hooks: params = base rgb, fresnel rgb, roughness, metallic.
+ * out: f_spec rgb, f_diff rgb, pdf_spec, pdf_diff. */
+void or_brdf_eval(const float *params, const float *n, const float *wi, const float *wo, float *out);
+float or_power_heuristic(float f, float g);
+int32_t or_upper_bound(const float *list, int32_t size, float val);
+void or_gen_ray(const or_camera *cam, int32_t W, int32_t H, int32_t x, int32_t y,
+                uint64_t seed, uint32_t pixel, uint32_t sample, float *o, float *d);
+const char *or_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,178 @@
+"""ctypes binding of liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this.  The
+oracle is the CPU restatement of the reference hot path (see mcpt_oracle.h for its pinning
+status).  Scenes are passed as the numpy dict produced by ``mcpt.Scene.arrays()`` (plain
+arrays, no product objects).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+ORACLE_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
+_f = C.POINTER(C.c_float)
+_i = C.POINTER(C.c_int32)
+_u = C.POINTER(C.c_uint32)
+
+
+class OrScene(C.Structure):
+    _fields_ = [("ntri", C.c_int32), ("v0", _f), ("v1", _f), ("v2", _f), ("n0", _f), ("n1", _f), ("n2", _f),
+                ("mat", _i), ("nnodes", C.c_int32), ("bmin", _f), ("bmax", _f), ("offset", _i), ("nprims", _i),
+                ("axis", _i), ("nmat", C.c_int32), ("mat_params", _f), ("ndir", C.c_int32), ("dir_params", _f),
+                ("env_mode", C.c_int32), ("env_color", C.c_float * 3), ("env_ls", C.c_float),
+                ("env_w", C.c_int32), ("env_h", C.c_int32), ("env_tex", _f), ("env_marginal_y", _f),
+                ("env_conds_y", _f), ("env_pdf", _f)]
+
+
+class OrCamera(C.Structure):
+    _fields_ = [("inv_view_proj", C.c_float * 16), ("inv_view", C.c_float * 16), ("lens_radius", C.c_float),
+                ("focal", C.c_float)]
+
+
+class OrConfig(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("spp", C.c_int32), ("max_depth", C.c_int32), ("rr_depth", C.c_int32),
+                ("tile_w", C.c_int32), ("tile_h", C.c_int32), ("nthreads", C.c_int32), ("traversal", C.c_int32),
+                ("row_begin", C.c_int32), ("row_end", C.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: build the oracle (make -C oracle)")
+        l = C.CDLL(LIB_PATH)
+        sig = {
+            "or_render": (C.c_int, [C.POINTER(OrScene), C.POINTER(OrCamera), C.POINTER(OrConfig), C.c_int32, C.c_int32,
+                                    _f, _u, C.POINTER(C.c_uint64)]),
+            "or_trace_closest": (None, [C.POINTER(OrScene), C.c_int32, _f, _f, C.c_int32, _f, _f, _i]),
+            "or_trace_any": (None, [C.POINTER(OrScene), C.c_int32, _f, _f, C.c_int32, C.POINTER(C.c_uint8)]),
+            "or_env_build": (None, [C.c_int32, C.c_int32, _f, _f, _f, _f, _f, _f]),
+            "or_sinf": (C.c_float, [C.c_float]), "or_cosf": (C.c_float, [C.c_float]),
+            "or_asinf": (C.c_float, [C.c_float]), "or_acosf": (C.c_float, [C.c_float]),
+            "or_atan2f": (C.c_float, [C.c_float, C.c_float]),
+            "or_lowerbias32": (C.c_uint32, [C.c_uint32]), "or_splitmix64": (C.c_uint64, [C.c_uint64]),
+            "or_rand": (C.c_float, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+            "or_env_fetch": (None, [C.POINTER(OrScene), C.c_float, C.c_float, _f]),
+            "or_env_pdf": (C.c_float, [C.POINTER(OrScene), C.c_float, C.c_float, C.c_float]),
+            "or_env_dir": (None, [C.POINTER(OrScene), C.c_float, C.c_float, _f]),
+            "or_brdf_eval": (None, [_f, _f, _f, _f, _f]),
+            "or_power_heuristic": (C.c_float, [C.c_float, C.c_float]),
+            "or_upper_bound": (C.c_int32, [_f, C.c_int32, C.c_float]),
+            "or_gen_ray": (None, [C.POINTER(OrCamera), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_uint64,
+                                  C.c_uint32, C.c_uint32, _f, _f]),
+            "or_version": (C.c_char_p, []),
+        }
+        for n, (r, a) in sig.items():
+            fn = getattr(l, n)
+            fn.restype = r
+            fn.argtypes = a
+        _lib = l
+    return _lib
+
+
+def fptr(a):
+    return a.ctypes.data_as(_f)
+
+
+def scene_struct(a: dict) -> OrScene:
+    keep = {}
+
+    def f(k):
+        arr = np.ascontiguousarray(a[k], np.float32)
+        keep[k] = arr
+        return arr.ctypes.data_as(_f) if arr.size else None
+
+    def i(k):
+        arr = np.ascontiguousarray(a[k], np.int32)
+        keep[k] = arr
+        return arr.ctypes.data_as(_i) if arr.size else None
+
+    s = OrScene()
+    s.ntri = len(a["mat"])
+    s.v0, s.v1, s.v2, s.n0, s.n1, s.n2 = (f(k) for k in ("v0", "v1", "v2", "n0", "n1", "n2"))
+    s.mat = i("mat")
+    s.nnodes = len(a["nprims"])
+    s.bmin, s.bmax = f("bmin"), f("bmax")
+    s.offset, s.nprims, s.axis = i("offset"), i("nprims"), i("axis")
+    s.nmat = len(a["mat_params"])
+    s.mat_params = f("mat_params")
+    s.ndir = len(a["dir_params"])
+    s.dir_params = f("dir_params")
+    s.env_mode = int(a["env_mode"])
+    for k in range(3):
+        s.env_color[k] = float(a["env_color"][k])
+    s.env_ls = float(a["env_ls"])
+    tex = np.asarray(a["env_tex"])
+    s.env_h, s.env_w = (tex.shape[0], tex.shape[1]) if tex.size else (0, 0)
+    s.env_tex, s.env_marginal_y, s.env_conds_y, s.env_pdf = (f(k) for k in ("env_tex", "env_marginal_y", "env_conds_y", "env_pdf"))
+    s._keep = keep
+    return s
+
+
+def camera_struct(cam) -> OrCamera:
+    c = OrCamera()
+    for k in range(16):
+        c.inv_view_proj[k] = cam.inv_view_proj[k]
+        c.inv_view[k] = cam.inv_view[k]
+    c.lens_radius = cam.lens_radius
+    c.focal = cam.focal
+    return c
+
+
+def render(arrays: dict, cam, W, H, spp, max_depth=5, rr_depth=3, seed=0x5EED2026, nthreads=None, traversal=0,
+           tile=256, rows=None):
+    """Full CPU re-execution of the reference wavefront loop.  Returns (Ld[H,W,3], samples[H,W], counters)."""
+    s = scene_struct(arrays)
+    c = camera_struct(cam)
+    nthreads = nthreads or min(8, os.cpu_count() or 1)
+    rb, re = rows if rows else (0, 0)
+    cfg = OrConfig(seed, spp, max_depth, rr_depth, tile, tile, nthreads, traversal, rb, re)
+    Ld = np.zeros(3 * W * H, np.float32)
+    samples = np.zeros(W * H, np.uint32)
+    cnt = (C.c_uint64 * 6)()
+    rc = lib().or_render(C.byref(s), C.byref(c), C.byref(cfg), W, H, fptr(Ld), samples.ctypes.data_as(_u), cnt)
+    if rc != 0:
+        raise RuntimeError(f"or_render failed: {rc}")
+    keys = ("extend_rays", "shadow_rays", "vis_rays", "iterations", "nodes", "tri_tests")
+    return Ld.reshape(H, W, 3), samples.reshape(H, W), dict(zip(keys, list(cnt)))
+
+
+def trace_closest(arrays, ro, rd, traversal=0):
+    s = scene_struct(arrays)
+    ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
+    rd = np.ascontiguousarray(rd, np.float32).reshape(-1, 3)
+    n = len(ro)
+    pos_t = np.zeros((n, 4), np.float32)
+    nrm = np.zeros((n, 4), np.float32)
+    tri = np.zeros(n, np.int32)
+    lib().or_trace_closest(C.byref(s), n, fptr(ro), fptr(rd), traversal, fptr(pos_t), fptr(nrm), tri.ctypes.data_as(_i))
+    return pos_t, nrm, tri
+
+
+def trace_any(arrays, ro, rd, traversal=0):
+    s = scene_struct(arrays)
+    ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
+    rd = np.ascontiguousarray(rd, np.float32).reshape(-1, 3)
+    n = len(ro)
+    vis = np.zeros(n, np.uint8)
+    lib().or_trace_any(C.byref(s), n, fptr(ro), fptr(rd), traversal, vis.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return vis
+
+
+def env_build(tex: np.ndarray):
+    tex = np.ascontiguousarray(tex, np.float32)
+    H, W = tex.shape[:2]
+    my = np.zeros(H, np.float32)
+    mp = np.zeros(H, np.float32)
+    cy = np.zeros((H, W), np.float32)
+    pdf = np.zeros((H, W), np.float32)
+    den = np.zeros(1, np.float32)
+    lib().or_env_build(W, H, fptr(tex), fptr(my), fptr(mp), fptr(cy), fptr(pdf), fptr(den))
+    return {"marginal_y": my, "marginal_p": mp, "conds_y": cy, "pdf": pdf, "denom": float(den[0])}
