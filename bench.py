@@ -1,0 +1,211 @@
+"""bench.py -- Mray/s (extend+shade) of the MI355X wavefront path tracer on BASELINE config 2.
+
+Workload (BASELINE.json configs[1]): 1920x1080, 256 spp, depth 5, MIS on, env importance sampling,
+Cornell-box + 5 spheres proxy for the missing scene_show_off_spheres.glb lit by
+night_free_Env.hdr.  A *step* is one wavefront iteration (the reference's wavefront_pathtrace,
+wavefront_kernels.cu:377-442: logic+generate+material -> extend -> shadow) over every pixel the
+rank owns; paths are in steady state after the warmup.  value = (extension + shadow + BRDF
+visibility rays of all ranks) / (max over ranks of the timed wall time).
+
+Multi-GPU: one process per GPU (torch.distributed.run), weak scaling: the frame is 1920 x 1080*N
+and 256x256 tiles are dealt to ranks by (tx + ty) mod N, so every rank owns ~1 frame of 1080p
+pixels.  No collective runs inside the timed region (tiles are independent); the RCCL gather of
+the film is a separate, untimed step (mcpt/parallel.py).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mc-path-tracer_amd"))
+
+HBM_PEAK = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# SURVEY.md 8(d) algorithmic bytes per unit of work
+B_EXT_STATE = 65      # extend: queue 4 + ray 24 + len 4 read, len/found/pos/n/mat 33 written
+B_ANY_STATE = 33      # shadow: queue 4 + ray 24 + light id 4 read, visible 1 written
+B_NODE = 32           # per BVH node box visited (a child-pair fetch visits 2)
+B_TRI = 36            # per ray/triangle test
+B_HIT = 40            # per closest hit: 3 normals + material id
+B_SHADE = 195 + 172   # logic + material per path-bounce
+B_GEN = 49            # generate per new sample
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the frame in the CPU sample (0 = auto)")
+    ap.add_argument("--gather", action="store_true", help="RCCL-gather the film after timing (N>1)")
+    return ap.parse_args()
+
+
+def tiles_for(rank, world, W, H, tile):
+    nx, ny = (W + tile - 1) // tile, (H + tile - 1) // tile
+    return [(tx, ty) for ty in range(ny) for tx in range(nx) if (tx + ty) % world == rank]
+
+
+def pmc_traffic(kernel_prefix):
+    """Per-launch HBM bytes for a kernel from the committed rocprofv3 PMC summary, if present."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        for k, v in d.get("kernels", {}).items():
+            if k.startswith(kernel_prefix):
+                return v.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def cpu_baseline(scene_arrays, cam, W, H, spp_rows, max_depth):
+    """Oracle (scalar C port of the reference kernels) on the host cores, bounded band of rows at 1 spp."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_py  # checker/baseline only
+
+    threads = min(16, os.cpu_count() or 1)
+    r0 = max(0, H // 2 - spp_rows // 2)
+    t = time.perf_counter()
+    _, _, cnt = oracle_py.render(scene_arrays, cam, W, H, spp=1, max_depth=max_depth, nthreads=threads,
+                                 rows=(r0, r0 + spp_rows))
+    dt = time.perf_counter() - t
+    rays = cnt["extend_rays"] + cnt["shadow_rays"] + cnt["vis_rays"]
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ (scalar C restatement, -O2, literal reference traversal), rows {r0}-{r0 + spp_rows} "
+                      f"of the {W}x{H} frame at 1 spp: {rays} rays in {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import numpy as np
+
+    import mcpt
+
+    rc = mcpt.CONFIGS[args.config]
+    W, H = rc.width, rc.height * world
+    scene = mcpt.build_config_scene(args.config)
+    cam = mcpt.config_camera(rc, W, H)
+    pt = mcpt.PathTracer(local, mcpt.default_config(spp=rc.spp, max_depth=rc.max_depth))
+    pt.upload_scene(scene)
+    pt.set_camera(cam)
+    pt.resize(W, H)
+    my_tiles = tiles_for(rank, world, W, H, 256)
+    pt.set_tiles(my_tiles)
+
+    pt.iterate(args.warmup)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = pt.iterate(args.steps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+
+    rays = st.rays
+    if dist:
+        v = torch.tensor([dt, float(rays)], dtype=torch.float64, device="cuda")
+        mx = v.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        dt_all, rays_all = float(mx[0]), float(v[1])
+    else:
+        dt_all, rays_all = dt, float(rays)
+
+    if args.gather and dist:
+        from mcpt import parallel
+
+        parallel.gather_film(pt, rank, world)
+
+    if rank != 0:
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    K = args.steps
+    # dominant kernel by summed HIP-event time over the timed region (same stream as the kernels)
+    kern = {"k_trace<closest>": st.ms_extend, "k_trace<any>": st.ms_shadow, "k_shade": st.ms_shade}
+    dom = max(kern, key=kern.get)
+    if dom == "k_trace<closest>":
+        byts = (B_EXT_STATE * st.extend_rays + 2 * B_NODE * st.ext_nodes + B_TRI * st.ext_tests + B_HIT * st.ext_hits)
+        prefix = "void mcpt_dev::k_trace<false>"
+    elif dom == "k_trace<any>":
+        byts = (B_ANY_STATE * (st.shadow_rays + st.vis_rays) + 2 * B_NODE * st.any_nodes + B_TRI * st.any_tests)
+        prefix = "void mcpt_dev::k_trace<true>"
+    else:
+        byts = B_SHADE * st.shadow_rays + B_GEN * (st.extend_rays - st.shadow_rays)
+        prefix = "mcpt_dev::k_shade"
+    per_launch = byts / K
+    avg_ms = kern[dom] / K
+    achieved = per_launch / (avg_ms * 1e-3)
+    traffic = pmc_traffic(prefix)
+    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
+            "algorithmic_bytes_per_launch": int(per_launch),
+            "state_only_frac": round(((B_EXT_STATE * st.extend_rays) / K if dom == "k_trace<closest>" else per_launch)
+                                     / (avg_ms * 1e-3) / HBM_PEAK, 4),
+            "per_ray": {"pair_nodes": round(st.ext_nodes / max(1, st.extend_rays), 2),
+                        "tri_tests": round(st.ext_tests / max(1, st.extend_rays), 2)}}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        rows = args.cpu_rows or max(8, min(H, int(36 * (min(16, os.cpu_count() or 1)))))
+        cpu = cpu_baseline(scene.arrays(), cam, W, H, rows, rc.max_depth)
+    value = rays_all / dt_all / 1e6
+    out = {
+        "metric": "Mray/s (extend+shade) at 1080p x256spp depth5; fraction of HBM roofline",
+        "value": round(value, 2),
+        "unit": "Mray/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt_all * 1e3 / K, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": "BASELINE config 2: Cornell-box + 5 spheres proxy (scene_show_off_spheres.glb missing), "
+                        f"night_free_Env.hdr env IS, {rc.width}x{rc.height} per GPU, {rc.spp} spp, depth {rc.max_depth}, MIS",
+            "frame": [W, H],
+            "tiles": "256x256, rank = (tx+ty) mod N",
+            "step": "one wavefront iteration (shade+extend+shadow) over the rank's pixels, steady state",
+            "rays_per_step": int(rays_all / K),
+            "parallelism": f"tiles{world}",
+            "device": pt.device_name,
+        },
+        "stage_ms_per_step": {k: round(v / K, 4) for k, v in kern.items()},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    pt.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

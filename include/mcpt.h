@@ -96,6 +96,10 @@ typedef struct mcpt_stage_stats {
     uint64_t live_paths;    /* paths still in flight after the call */
     float ms_total;         /* device time of logic+generate+material+extend+shadow */
     float ms_shade, ms_extend, ms_shadow;
+    uint64_t ext_nodes;     /* closest-hit: child-pair nodes fetched (2 boxes each) */
+    uint64_t ext_tests;     /* closest-hit: ray/triangle tests */
+    uint64_t ext_hits;      /* closest-hit: rays that found a surface */
+    uint64_t any_nodes, any_tests, any_hits;   /* any-hit (shadow + visibility) */
 } mcpt_stage_stats;
 
 enum { MCPT_STAGE_LOGIC = 0, MCPT_STAGE_GENERATE = 1, MCPT_STAGE_MATERIAL = 2,

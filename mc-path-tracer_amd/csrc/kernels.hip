@@ -273,7 +273,8 @@ template <bool ANY>
 struct TraceResult { int tri; float t; };
 
 template <bool ANY>
-__device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*stk)[kBlock], int lane_slot, uint32_t* nstat) {
+__device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*stk)[kBlock], int lane_slot,
+                                         uint32_t& nodes, uint32_t& tests) {
     TraceResult<ANY> res{-1, K_HUGE};
     V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
     const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;
@@ -287,7 +288,6 @@ __device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*
     float t0, t1;
     if (!slab(sc.root_mn, sc.root_mx, o, inv, nx, ny, nz, t0, t1) || !keep_box(t0, t1, cut)) return res;
     int ref = sc.root_ref;
-    uint32_t nodes = 0, tests = 0;
     for (;;) {
         if (ref >= 0) {
             const float4* nd = sc.nodes + 4 * ref;
@@ -327,7 +327,7 @@ __device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*
                 float t, u, v;
                 if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) && !(t < 0.f)) {
                     if (ANY) {
-                        if (t < K_HUGE) { res.tri = id; res.t = t; if (nstat) { atomicAdd(nstat, nodes); atomicAdd(nstat + 1, tests); } return res; }
+                        if (t < K_HUGE) { res.tri = id; res.t = t; return res; }
                     } else if (t < best || (t == best && id < res.tri)) {
                         best = t;
                         res.tri = id;
@@ -349,7 +349,6 @@ __device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*
         }
         if (!got) break;
     }
-    if (nstat) { atomicAdd(nstat, nodes); atomicAdd(nstat + 1, tests); }
     return res;
 }
 
@@ -359,6 +358,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
     __shared__ int2 stk[kLdsStack][kBlock];
     const int lane = threadIdx.x & 63;
     const uint32_t n = a.count_ptr ? *a.count_ptr : a.count;
+    uint32_t nodes = 0, tests = 0, hits = 0;
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(a.work, 64u);
@@ -369,7 +369,8 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
             const uint32_t rid = a.queue ? a.queue[i] : i;
             const float4 o4 = a.ro[rid], d4 = a.rd[rid];
             const V3 o = xyz(o4), d = xyz(d4);
-            TraceResult<ANY> tr = trace<ANY>(a.scene, o, d, stk, threadIdx.x, a.stats);
+            TraceResult<ANY> tr = trace<ANY>(a.scene, o, d, stk, threadIdx.x, nodes, tests);
+            hits += tr.tri >= 0;
             if (ANY) {
                 a.vis[rid] = (uint8_t)(tr.tri < 0);
             } else {
@@ -395,6 +396,18 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
                     if (a.hit_tri) a.hit_tri[pid] = -1;
                 }
             }
+        }
+    }
+    if (a.stats) {  // traversal work counters: wave-reduce, one atomic per wave
+        for (int off = 32; off > 0; off >>= 1) {
+            nodes += __shfl_xor(nodes, off);
+            tests += __shfl_xor(tests, off);
+            hits += __shfl_xor(hits, off);
+        }
+        if (lane == 0) {
+            atomicAdd(a.stats + 0, nodes);
+            atomicAdd(a.stats + 1, tests);
+            atomicAdd(a.stats + 2, hits);
         }
     }
 }
@@ -431,6 +444,7 @@ __global__ void k_accumulate(CounterBlock* c) {  // fold per-iteration counts in
     c->tot_any += c->any;
     c->tot_vis += c->vis;
     c->vis = 0;
+    for (int k = 0; k < 6; k++) { c->tot_stats[k] += c->it_stats[k]; c->it_stats[k] = 0; }
     c->last_ext = c->ext;
     c->ext = 0;
     c->any = 0;

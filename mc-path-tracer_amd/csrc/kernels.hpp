@@ -56,8 +56,9 @@ struct DevPaths {
 
 struct CounterBlock {
     uint32_t ext, any, vis, work_ext, work_any, last_ext, pad0, pad1;
+    uint32_t it_stats[6];   // this iteration: closest {pair nodes, tri tests, hits}, any-hit {same}
     unsigned long long tot_ext, tot_any, tot_vis, pad2;
-    uint32_t stats[4];      // optional traversal counters: nodes, triangle tests
+    unsigned long long tot_stats[6];
 };
 
 struct ShadeArgs {
@@ -82,7 +83,7 @@ struct TraceArgs {
     float4 *hit_p, *hit_n;      // closest-hit outputs
     int32_t* hit_tri;           // optional
     uint8_t* vis;               // any-hit output
-    uint32_t* stats;            // optional: [nodes, tests]
+    uint32_t* stats;            // optional: [pair nodes, triangle tests, hits]
 };
 
 struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n; };

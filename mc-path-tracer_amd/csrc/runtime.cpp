@@ -405,6 +405,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     ta.work = &c->cnt->work_ext;
     ta.hit_p = c->p.hit_p;
     ta.hit_n = c->p.hit_n;
+    ta.stats = &c->cnt->it_stats[0];
     launch_trace(ta, false, c->trace_blocks[0], c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
     TraceArgs tb{};
@@ -415,6 +416,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     tb.count_ptr = &c->cnt->any;
     tb.work = &c->cnt->work_any;
     tb.vis = c->p.vis;
+    tb.stats = &c->cnt->it_stats[3];
     launch_trace(tb, true, c->trace_blocks[1], c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 3), c->stream));
     launch_accumulate(c->cnt, c->stream);
@@ -444,6 +446,12 @@ static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st) {
         st->shadow_rays = (after.tot_any - before.tot_any) - st->vis_rays;
         st->iterations = n;
         st->live_paths = after.last_ext;
+        st->ext_nodes = after.tot_stats[0] - before.tot_stats[0];
+        st->ext_tests = after.tot_stats[1] - before.tot_stats[1];
+        st->ext_hits = after.tot_stats[2] - before.tot_stats[2];
+        st->any_nodes = after.tot_stats[3] - before.tot_stats[3];
+        st->any_tests = after.tot_stats[4] - before.tot_stats[4];
+        st->any_hits = after.tot_stats[5] - before.tot_stats[5];
         uint32_t tn = std::min<uint32_t>(n, 4096);
         for (uint32_t i = 0; i < tn; i++) {
             float a = 0, b = 0, d = 0;
@@ -490,6 +498,8 @@ int mcpt_render(mcpt_ctx* c, mcpt_stage_stats* st) {
         acc.ms_shadow += one.ms_shadow;
         acc.ms_total += one.ms_total;
         acc.live_paths = one.live_paths;
+        acc.ext_nodes += one.ext_nodes; acc.ext_tests += one.ext_tests; acc.ext_hits += one.ext_hits;
+        acc.any_nodes += one.any_nodes; acc.any_tests += one.any_tests; acc.any_hits += one.any_hits;
         done += 32;
         if (one.live_paths == 0 || done > cap) break;
     }

@@ -62,7 +62,9 @@ class CameraParams(C.Structure):
 class StageStats(C.Structure):
     _fields_ = [("extend_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("vis_rays", C.c_uint64),
                 ("iterations", C.c_uint64), ("live_paths", C.c_uint64), ("ms_total", C.c_float),
-                ("ms_shade", C.c_float), ("ms_extend", C.c_float), ("ms_shadow", C.c_float)]
+                ("ms_shade", C.c_float), ("ms_extend", C.c_float), ("ms_shadow", C.c_float),
+                ("ext_nodes", C.c_uint64), ("ext_tests", C.c_uint64), ("ext_hits", C.c_uint64),
+                ("any_nodes", C.c_uint64), ("any_tests", C.c_uint64), ("any_hits", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
