@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the frame in the CPU sample (0 = auto)")
+    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the full-frame CPU-oracle sample")
     ap.add_argument("--gather", action="store_true", help="RCCL-gather the film after timing (N>1)")
     return ap.parse_args()
 
@@ -67,21 +67,20 @@ def pmc_traffic(kernel_prefix):
     return None
 
 
-def cpu_baseline(scene_arrays, cam, W, H, spp_rows, max_depth):
-    """Oracle (scalar C port of the reference kernels) on the host cores, bounded band of rows at 1 spp."""
+def cpu_baseline(scene_arrays, cam, W, H, spp, max_depth):
+    """Oracle (scalar C port of the reference kernels) on the host cores: the full frame at a few spp."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_py  # checker/baseline only
 
     threads = min(16, os.cpu_count() or 1)
-    r0 = max(0, H // 2 - spp_rows // 2)
     t = time.perf_counter()
-    _, _, cnt = oracle_py.render(scene_arrays, cam, W, H, spp=1, max_depth=max_depth, nthreads=threads,
-                                 rows=(r0, r0 + spp_rows))
+    _, _, cnt = oracle_py.render(scene_arrays, cam, W, H, spp=spp, max_depth=max_depth, nthreads=threads)
     dt = time.perf_counter() - t
     rays = cnt["extend_rays"] + cnt["shadow_rays"] + cnt["vis_rays"]
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ (scalar C restatement, -O2, literal reference traversal), rows {r0}-{r0 + spp_rows} "
-                      f"of the {W}x{H} frame at 1 spp: {rays} rays in {dt:.1f} s"}
+            "sample": f"oracle/ (scalar C restatement of the reference kernels, -O2, literal stack traversal, "
+                      f"{threads} std threads over 256x256 tiles): the full {W}x{H} frame at {spp} spp, "
+                      f"{rays} rays in {dt:.1f} s"}
 
 
 def main():
@@ -89,7 +88,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
+    if world == 1 and os.environ.get("MCPT_BENCH_NO_TORCH") == "1":
+        torch = None
+    else:
+        import torch
 
     dist = None
     if world > 1:
@@ -115,10 +117,12 @@ def main():
     pt.iterate(args.warmup)
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    if torch:
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
-    st = pt.iterate(args.steps)
-    torch.cuda.synchronize()
+    st = pt.iterate(args.steps)  # returns after its stream has drained
+    if torch:
+        torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
@@ -170,8 +174,7 @@ def main():
                         "tri_tests": round(st.ext_tests / max(1, st.extend_rays), 2)}}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        rows = args.cpu_rows or max(8, min(H, int(36 * (min(16, os.cpu_count() or 1)))))
-        cpu = cpu_baseline(scene.arrays(), cam, W, H, rows, rc.max_depth)
+        cpu = cpu_baseline(scene.arrays(), cam, W, H, args.cpu_spp, rc.max_depth)
     value = rays_all / dt_all / 1e6
     out = {
         "metric": "Mray/s (extend+shade) at 1080p x256spp depth5; fraction of HBM roofline",

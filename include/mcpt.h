@@ -113,6 +113,7 @@ typedef struct mcpt_soa_view {
     float *hit_nrm_mat;     /* EXTEND out: 4*n normal.xyz, (float)material (-1 miss) */
     int32_t *hit_tri;       /* EXTEND out: n triangle index or -1 */
     uint8_t *visible;       /* SHADOW out: n */
+    uint32_t *steps;        /* optional out: per-ray child-pair node fetches + triangle tests */
 } mcpt_soa_view;
 
 typedef struct mcpt_ctx mcpt_ctx;     /* device context: one per GPU, not thread-safe */
@@ -137,6 +138,10 @@ int mcpt_film_pack_tiles(mcpt_ctx *ctx, void *d_out, uint32_t *npix);       /* t
 int mcpt_film_tonemap_rgba8(mcpt_ctx *ctx, float exposure, uint8_t *out);   /* == draw_to_surface */
 int mcpt_sync(mcpt_ctx *ctx);
 int mcpt_device_name(mcpt_ctx *ctx, char *buf, int32_t len);
+/* diagnostics: rays of the current extension (which=0) or any-hit (which=1) queue, and the
+ * device time of the last mcpt_stage_run kernel. */
+int mcpt_debug_queue_rays(mcpt_ctx *ctx, int which, float *ray_o, float *ray_d, uint32_t *n_inout);
+float mcpt_debug_last_stage_ms(const mcpt_ctx *ctx);
 
 /* ---- host scene builder (Scene.cu:24-470, EnvironmentLight.cu:329-452, BVH.cu) ---- */
 mcpt_scene *mcpt_scene_new(void);

@@ -224,14 +224,16 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
     }
     (void)new_path;
     // ---- compaction: ext queue and any-hit queue (light + vis rays)
+    const int shard = blockIdx.x % kShards;
+    uint32_t* sc_ctr = a.cnt->shard[shard];
     bool want[3] = {want_ext, want_l, want_b};
-    uint32_t* ctr[3] = {&a.cnt->ext, &a.cnt->any, &a.cnt->any};
+    uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
     uint32_t slot[3], total[3];
     block_push<3>(want, ctr, slot, total);
-    if (want_ext) a.ext_q[slot[0]] = pid;
-    if (want_l) a.any_q[slot[1]] = 2 * pid;
-    if (want_b) a.any_q[slot[2]] = 2 * pid + 1;
-    if (threadIdx.x == 0 && total[2]) atomicAdd(&a.cnt->vis, total[2]);  // BRDF visibility rays
+    if (want_ext) a.ext_q[shard * a.ext_cap + slot[0]] = pid;
+    if (want_l) a.any_q[shard * a.any_cap + slot[1]] = 2 * pid;
+    if (want_b) a.any_q[shard * a.any_cap + slot[2]] = 2 * pid + 1;
+    if (threadIdx.x == 0 && total[2]) atomicAdd(sc_ctr + C_VIS, total[2]);  // BRDF visibility rays
 }
 
 // ---------------------------------------------------------------------------
@@ -244,157 +246,167 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
 // Stack: kLdsStack entries per lane in LDS ([entry][lane], conflict-free),
 // deeper entries in private scratch.
 // ---------------------------------------------------------------------------
-__device__ inline bool slab(const float* mn, const float* mx, V3 o, V3 inv, int nx, int ny, int nz, float& t0, float& t1) {
-    float bx0 = nx ? mx[0] : mn[0], bx1 = nx ? mn[0] : mx[0];
-    float by0 = ny ? mx[1] : mn[1], by1 = ny ? mn[1] : mx[1];
-    float bz0 = nz ? mx[2] : mn[2], bz1 = nz ? mn[2] : mx[2];
+// Reference slab test (Bounds3f.h:121-153) written branch-free: the same six
+// products and the same comparison sequence, evaluated unconditionally so the
+// whole node is fetched up front (the early-out form let the compiler sink the
+// z loads behind the x/y test: two dependent round trips per node).  NaN slabs
+// compare false and pass, exactly as in the reference.
+__device__ inline bool slab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, V3 o, V3 inv,
+                            int nx, int ny, int nz, float& t0, float& t1) {
+    float bx0 = nx ? mxx : mnx, bx1 = nx ? mnx : mxx;
+    float by0 = ny ? mxy : mny, by1 = ny ? mny : mxy;
+    float bz0 = nz ? mxz : mnz, bz1 = nz ? mnz : mxz;
     float tmin = (bx0 - o.x) * inv.x;
     float tmax = (bx1 - o.x) * inv.x;
     float tymin = (by0 - o.y) * inv.y;
     float tymax = (by1 - o.y) * inv.y;
-    if ((tmin > tymax) || (tymin > tmax)) return false;
-    if (tymin > tmin) tmin = tymin;
-    if (tymax < tmax) tmax = tymax;
     float tzmin = (bz0 - o.z) * inv.z;
     float tzmax = (bz1 - o.z) * inv.z;
-    if ((tmin > tzmax) || (tzmin > tmax)) return false;
-    if (tzmin > tmin) tmin = tzmin;
-    if (tzmax < tmax) tmax = tzmax;
-    t0 = tmin;
-    t1 = tmax;
-    return true;
+    bool miss = (tmin > tymax) || (tymin > tmax);
+    float a = (tymin > tmin) ? tymin : tmin;
+    float b = (tymax < tmax) ? tymax : tmax;
+    miss = miss || (a > tzmax) || (tzmin > b);
+    t0 = (tzmin > a) ? tzmin : a;
+    t1 = (tzmax < b) ? tzmax : b;
+    return !miss;
 }
 constexpr float kCullAbs = 1e-5f;
 constexpr float kCullRel = 1.0f / 256.0f;
+constexpr int kEnd = -1;  // not a valid leaf: offset + count <= ntri < 2^24
 
 __device__ inline bool keep_box(float t0, float t1, float cut) { return !(t1 < -kCullAbs) && !(t0 > cut); }
 
 template <bool ANY>
 struct TraceResult { int tri; float t; };
 
+// Child-pair BVH traversal, while-while structure (Aila & Laine 2009): lanes
+// descend interior nodes together, then test leaves together.  Culling beyond
+// the reference (which visits every box the infinite line crosses) is
+// conservative: a box is skipped only when it lies entirely behind the origin or
+// starts more than 2^-8 * t_best past the current best hit.  Ties on t go to the
+// lower triangle index so the visit order is free (near child first here).
 template <bool ANY>
-__device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*stk)[kBlock], int lane_slot,
+__device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*stk)[kTraceBlock], int lane_slot,
                                          uint32_t& nodes, uint32_t& tests) {
     TraceResult<ANY> res{-1, K_HUGE};
-    V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    // NaN / zero direction: every triangle test fails (det NaN or 0), so the
+    // reference reports a miss / visible (SURVEY.md Appendix A.9).
+    if (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f)) return res;
+    const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
     const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;
     float best = K_HUGE;
     float cut = best + best * kCullRel;
     int2 spill[kMaxStack - kLdsStack];
     int sp = 0;
-    // NaN / zero direction: every triangle test fails (det NaN or 0), so the
-    // reference reports a miss / visible (SURVEY.md Appendix A.9).
-    if (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f)) return res;
     float t0, t1;
-    if (!slab(sc.root_mn, sc.root_mx, o, inv, nx, ny, nz, t0, t1) || !keep_box(t0, t1, cut)) return res;
+    if (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1], sc.root_mx[2], o, inv, nx, ny,
+              nz, t0, t1) || !keep_box(t0, t1, cut))
+        return res;
     int ref = sc.root_ref;
-    for (;;) {
-        if (ref >= 0) {
-            const float4* nd = sc.nodes + 4 * ref;
-            float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-            nodes++;
-            float mn0[3] = {q0.x, q0.y, q0.z}, mx0[3] = {q0.w, q1.x, q1.y};
-            float mn1[3] = {q1.z, q1.w, q2.x}, mx1[3] = {q2.y, q2.z, q2.w};
-            float a0, b0, a1, b1;
-            bool h0 = slab(mn0, mx0, o, inv, nx, ny, nz, a0, b0) && keep_box(a0, b0, cut);
-            bool h1 = slab(mn1, mx1, o, inv, nx, ny, nz, a1, b1) && keep_box(a1, b1, cut);
-            int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
-            if (h0 && h1) {
-                bool first0 = !(a1 < a0);
-                int near = first0 ? c0 : c1, far = first0 ? c1 : c0;
-                float far_t = first0 ? a1 : a0;
-                int2 e = make_int2(far, __float_as_int(far_t));
-                if (sp < kLdsStack) stk[sp][lane_slot] = e;
-                else spill[sp - kLdsStack] = e;
-                sp++;
-                ref = near;
-                continue;
-            } else if (h0) {
-                ref = c0;
-                continue;
-            } else if (h1) {
-                ref = c1;
-                continue;
-            }
-        } else {
-            const int off = ref & 0xffffff;
-            const int cnt = ((ref >> 24) & 7) + 1;
-            for (int k = 0; k < cnt; k++) {
-                const int id = off + k;
-                const float4* tp = sc.tri + 3 * id;
-                float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-                tests++;
-                float t, u, v;
-                if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) && !(t < 0.f)) {
-                    if (ANY) {
-                        if (t < K_HUGE) { res.tri = id; res.t = t; return res; }
-                    } else if (t < best || (t == best && id < res.tri)) {
-                        best = t;
-                        res.tri = id;
-                        res.t = t;
-                        cut = best + best * kCullRel;
-                    }
-                }
-            }
-        }
-        // pop, skipping entries culled by the improved best
-        bool got = false;
+    auto pop = [&]() -> int {
         while (sp > 0) {
             sp--;
             int2 e = (sp < kLdsStack) ? stk[sp][lane_slot] : spill[sp - kLdsStack];
             if (!ANY && __int_as_float(e.y) > cut) continue;
-            ref = e.x;
-            got = true;
-            break;
+            return e.x;
         }
-        if (!got) break;
+        return kEnd;
+    };
+    while (ref != kEnd) {
+        // ---- interior nodes
+        while (ref >= 0) {
+            const float4* nd = sc.nodes + 4 * ref;
+            const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+            nodes++;
+            float a0, b0, a1, b1;
+            bool h0 = slab(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, o, inv, nx, ny, nz, a0, b0) && keep_box(a0, b0, cut);
+            bool h1 = slab(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, o, inv, nx, ny, nz, a1, b1) && keep_box(a1, b1, cut);
+            const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
+            if (h0 && h1) {
+                const bool first0 = !(a1 < a0);
+                const int2 e = make_int2(first0 ? c1 : c0, __float_as_int(first0 ? a1 : a0));
+                if (sp < kLdsStack) stk[sp][lane_slot] = e;
+                else spill[sp - kLdsStack] = e;
+                sp++;
+                ref = first0 ? c0 : c1;
+            } else if (h0 | h1) {
+                ref = h0 ? c0 : c1;
+            } else {
+                ref = pop();
+            }
+        }
+        if (ref == kEnd) break;
+        // ---- leaf
+        const int off = ref & 0xffffff;
+        const int cnt = ((ref >> 24) & 7) + 1;
+        for (int k = 0; k < cnt; k++) {
+            const int id = off + k;
+            const float4* tp = sc.tri + 3 * id;
+            const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
+            tests++;
+            float t, u, v;
+            if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) && !(t < 0.f)) {
+                if (ANY) {
+                    if (t < K_HUGE) { res.tri = id; res.t = t; return res; }
+                } else if (t < best || (t == best && id < res.tri)) {
+                    best = t;
+                    res.tri = id;
+                    res.t = t;
+                    cut = best + best * kCullRel;
+                }
+            }
+        }
+        ref = pop();
     }
     return res;
 }
 
-// Persistent trace kernel: each wave pulls 64 rays at a time from a counter.
+// Trace kernel: one wave per block, one ray per lane; the grid covers the largest
+// possible queue and lanes beyond the device-side count exit at once.  (A
+// persistent variant pulling 64 rays per atomic serialised on the single work
+// counter: ~32K dequeues per launch at <= ~88 per microsecond.)
 template <bool ANY>
-__global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
-    __shared__ int2 stk[kLdsStack][kBlock];
+__global__ __launch_bounds__(kTraceBlock) void k_trace(TraceArgs a) {
+    __shared__ int2 stk[kLdsStack][kTraceBlock];
     const int lane = threadIdx.x & 63;
-    const uint32_t n = a.count_ptr ? *a.count_ptr : a.count;
+    const uint32_t wave_base = blockIdx.x * kTraceBlock;
+    const int shard = (int)(wave_base / a.shard_cap);
+    const uint32_t k = wave_base - (uint32_t)shard * a.shard_cap + threadIdx.x;  // slot within the shard
+    const uint32_t n = a.count_ptr ? a.count_ptr[shard * C_WORDS] : a.count;
     uint32_t nodes = 0, tests = 0, hits = 0;
-    for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(a.work, 64u);
-        base = __shfl(base, 0);
-        if (base >= n) break;
-        const uint32_t i = base + lane;
-        if (i < n) {
-            const uint32_t rid = a.queue ? a.queue[i] : i;
-            const float4 o4 = a.ro[rid], d4 = a.rd[rid];
-            const V3 o = xyz(o4), d = xyz(d4);
-            TraceResult<ANY> tr = trace<ANY>(a.scene, o, d, stk, threadIdx.x, nodes, tests);
-            hits += tr.tri >= 0;
-            if (ANY) {
-                a.vis[rid] = (uint8_t)(tr.tri < 0);
+    if (k - threadIdx.x >= n) return;  // whole wave past the shard's count
+    const uint32_t i = shard * a.shard_cap + k;
+    if (k < n) {
+        const uint32_t rid = a.queue ? a.queue[i] : i;
+        const float4 o4 = a.ro[rid], d4 = a.rd[rid];
+        const V3 o = xyz(o4), d = xyz(d4);
+        const uint32_t n0 = nodes + tests;
+        TraceResult<ANY> tr = trace<ANY>(a.scene, o, d, stk, threadIdx.x, nodes, tests);
+        hits += tr.tri >= 0;
+        if (a.ray_steps) a.ray_steps[i] = nodes + tests - n0;
+        if (ANY) {
+            a.vis[rid] = (uint8_t)(tr.tri < 0);
+        } else {
+            const uint32_t pid = rid;
+            if (tr.tri >= 0) {
+                const float4* tp = a.scene.tri + 3 * tr.tri;
+                float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
+                float t, u, v;
+                tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v);
+                const float4* sp4 = a.scene.tri_sh + 3 * tr.tri;
+                float4 s0 = sp4[0], s1 = sp4[1], s2 = sp4[2];
+                V3 n0 = v3(s0.x, s0.y, s0.z), n1 = v3(s0.w, s1.x, s1.y), n2 = v3(s1.z, s1.w, s2.x);
+                float w = (1.f - u) - v;
+                V3 nn = normalize((n1 * u + n2 * v) + n0 * w);  // Triangle.cu:76
+                nn = normalize(nn);                              // identity transform, :82
+                V3 p = o + d * t;                                // :86
+                a.hit_p[pid] = make_float4(p.x, p.y, p.z, t);
+                a.hit_n[pid] = make_float4(nn.x, nn.y, nn.z, s2.y);  // s2.y = material id bits
+                if (a.hit_tri) a.hit_tri[pid] = tr.tri;
             } else {
-                const uint32_t pid = rid;
-                if (tr.tri >= 0) {
-                    const float4* tp = a.scene.tri + 3 * tr.tri;
-                    float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-                    float t, u, v;
-                    tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v);
-                    const float4* sp4 = a.scene.tri_sh + 3 * tr.tri;
-                    float4 s0 = sp4[0], s1 = sp4[1], s2 = sp4[2];
-                    V3 n0 = v3(s0.x, s0.y, s0.z), n1 = v3(s0.w, s1.x, s1.y), n2 = v3(s1.z, s1.w, s2.x);
-                    float w = (1.f - u) - v;
-                    V3 nn = normalize((n1 * u + n2 * v) + n0 * w);  // Triangle.cu:76
-                    nn = normalize(nn);                              // identity transform, :82
-                    V3 p = o + d * t;                                // :86
-                    a.hit_p[pid] = make_float4(p.x, p.y, p.z, t);
-                    a.hit_n[pid] = make_float4(nn.x, nn.y, nn.z, s2.y);  // s2.y = material id bits
-                    if (a.hit_tri) a.hit_tri[pid] = tr.tri;
-                } else {
-                    a.hit_p[pid] = make_float4(0.f, 0.f, 0.f, K_HUGE);
-                    a.hit_n[pid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-                    if (a.hit_tri) a.hit_tri[pid] = -1;
-                }
+                a.hit_p[pid] = make_float4(0.f, 0.f, 0.f, K_HUGE);
+                a.hit_n[pid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+                if (a.hit_tri) a.hit_tri[pid] = -1;
             }
         }
     }
@@ -405,9 +417,10 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
             hits += __shfl_xor(hits, off);
         }
         if (lane == 0) {
-            atomicAdd(a.stats + 0, nodes);
-            atomicAdd(a.stats + 1, tests);
-            atomicAdd(a.stats + 2, hits);
+            uint32_t* st = a.stats + (blockIdx.x % kShards) * C_WORDS;
+            atomicAdd(st + 0, nodes);
+            atomicAdd(st + 1, tests);
+            atomicAdd(st + 2, hits);
         }
     }
 }
@@ -439,17 +452,25 @@ __global__ void k_tonemap(TonemapArgs a) {  // draw_to_surface (wavefront_kernel
     a.out[i] = o;
 }
 
-__global__ void k_accumulate(CounterBlock* c) {  // fold per-iteration counts into 64-bit totals
-    c->tot_ext += c->ext;
-    c->tot_any += c->any;
-    c->tot_vis += c->vis;
-    c->vis = 0;
-    for (int k = 0; k < 6; k++) { c->tot_stats[k] += c->it_stats[k]; c->it_stats[k] = 0; }
-    c->last_ext = c->ext;
-    c->ext = 0;
-    c->any = 0;
-    c->work_ext = 0;
-    c->work_any = 0;
+__global__ void k_accumulate(CounterBlock* c) {  // fold per-iteration shard counts into 64-bit totals
+    const int t = threadIdx.x;  // one lane per shard
+    uint32_t v[C_STATS + 6];
+#pragma unroll
+    for (int k = 0; k < C_STATS + 6; k++) {
+        v[k] = c->shard[t][k];
+        c->shard[t][k] = 0;
+    }
+    c->last_ext_shard[t] = v[C_EXT];
+#pragma unroll
+    for (int k = 0; k < C_STATS + 6; k++)
+        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    if (t == 0) {
+        c->tot_ext += v[C_EXT];
+        c->tot_any += v[C_ANY];
+        c->tot_vis += v[C_VIS];
+        c->last_ext = v[C_EXT];
+        for (int k = 0; k < 6; k++) c->tot_stats[k] += v[C_STATS + k];
+    }
 }
 
 __global__ void k_pack(PackArgs a) {  // tile-set pixels -> packed 16 B/px (for the RCCL gather)
@@ -474,9 +495,11 @@ __global__ void k_pack(PackArgs a) {  // tile-set pixels -> packed 16 B/px (for 
 void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s) {
     hipLaunchKernelGGL(k_shade, dim3(nblocks), dim3(kBlock), 0, s, a);
 }
-void launch_trace(const TraceArgs& a, bool any, int nblocks, hipStream_t s) {
-    if (any) hipLaunchKernelGGL(k_trace<true>, dim3(nblocks), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL(k_trace<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
+void launch_trace(const TraceArgs& a, bool any, hipStream_t s) {
+    const uint32_t nblocks = (uint32_t)(((uint64_t)a.nshards * a.shard_cap + kTraceBlock - 1) / kTraceBlock);
+    if (nblocks == 0) return;
+    if (any) hipLaunchKernelGGL(k_trace<true>, dim3(nblocks), dim3(kTraceBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_trace<false>, dim3(nblocks), dim3(kTraceBlock), 0, s, a);
 }
 void launch_clear(const ClearArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_clear, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
@@ -484,7 +507,7 @@ void launch_clear(const ClearArgs& a, hipStream_t s) {
 void launch_tonemap(const TonemapArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_tonemap, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
-void launch_accumulate(CounterBlock* c, hipStream_t s) { hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(1), 0, s, c); }
+void launch_accumulate(CounterBlock* c, hipStream_t s) { hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(kShards), 0, s, c); }
 void launch_pack(const PackArgs& a, hipStream_t s) {
     uint32_t n = (uint32_t)(a.ntiles * a.tile_w * a.tile_h);
     hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, s, a);

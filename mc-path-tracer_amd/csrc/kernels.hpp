@@ -24,7 +24,8 @@
 namespace mcpt_dev {
 
 constexpr int kBlock = 256;
-constexpr int kLdsStack = 16;  // traversal stack entries per lane kept in LDS
+constexpr int kTraceBlock = 64;  // one wave per traversal block
+constexpr int kLdsStack = 8;   // traversal stack entries per lane kept in LDS (deeper: scratch)
 constexpr int kMaxStack = 64;  // total (reference: int nodesToVisit[64], Triangle.cu:161)
 
 enum : uint32_t {
@@ -54,9 +55,16 @@ struct DevPaths {
     uint8_t* vis;
 };
 
+// Queue counters and statistics are sharded over kShards cache lines (one
+// shard per k_shade block mod kShards): a single counter word serialises at
+// roughly 90 atomics per microsecond, which is what ~24K pushes and ~100K
+// statistics adds per iteration would otherwise cost.
+constexpr int kShards = 64;
+enum : int { C_EXT = 0, C_ANY = 1, C_VIS = 2, C_STATS = 3, C_WORDS = 32 };  // C_STATS..C_STATS+5
 struct CounterBlock {
-    uint32_t ext, any, vis, work_ext, work_any, last_ext, pad0, pad1;
-    uint32_t it_stats[6];   // this iteration: closest {pair nodes, tri tests, hits}, any-hit {same}
+    uint32_t shard[kShards][C_WORDS];  // [0] ext pushes [1] any-hit pushes [2] vis rays [3..8] traversal stats
+    uint32_t last_ext, pad[31];
+    uint32_t last_ext_shard[kShards];  // per-shard extension pushes of the last iteration
     unsigned long long tot_ext, tot_any, tot_vis, pad2;
     unsigned long long tot_stats[6];
 };
@@ -70,6 +78,7 @@ struct ShadeArgs {
     int spp, max_depth, rr_depth;
     uint64_t seed;
     uint32_t *ext_q, *any_q;
+    uint32_t ext_cap, any_cap;  // per-shard queue capacity
     CounterBlock* cnt;
 };
 
@@ -77,13 +86,15 @@ struct TraceArgs {
     DevScene scene;
     const float4 *ro, *rd;
     const uint32_t* queue;      // nullptr => identity
-    const uint32_t* count_ptr;  // device count (nullptr => use count)
+    const uint32_t* count_ptr;  // device count of shard s at count_ptr[s * C_WORDS] (nullptr => count)
     uint32_t count;
-    uint32_t* work;             // per-launch work counter (zeroed before launch)
+    uint32_t shard_cap;         // queue entries per shard (queue[s * shard_cap + k])
+    int nshards;
     float4 *hit_p, *hit_n;      // closest-hit outputs
     int32_t* hit_tri;           // optional
     uint8_t* vis;               // any-hit output
-    uint32_t* stats;            // optional: [pair nodes, triangle tests, hits]
+    uint32_t* stats;            // optional: shard s counters at stats[s * C_WORDS + 0..2]
+    uint32_t* ray_steps;        // optional per-ray node fetches + triangle tests (diagnostics)
 };
 
 struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n; };
@@ -91,7 +102,7 @@ struct TonemapArgs { const float4* Ld; const uint32_t* samples; uchar4* out; flo
 struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* out; };
 
 void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s);
-void launch_trace(const TraceArgs& a, bool any, int nblocks, hipStream_t s);
+void launch_trace(const TraceArgs& a, bool any, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);
 void launch_accumulate(CounterBlock* c, hipStream_t s);

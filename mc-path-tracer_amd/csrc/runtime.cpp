@@ -46,15 +46,17 @@ struct mcpt_ctx {
     std::vector<void*> film_bufs;
     DevPaths p{};
     uint32_t *ext_q = nullptr, *any_q = nullptr;
+    uint32_t ext_cap = 0, any_cap = 0;  // per-shard capacities
+    size_t queue_alloc = 0;             // entries allocated for ext_q (any_q holds twice)
     CounterBlock* cnt = nullptr;
     CounterBlock* cnt_host = nullptr;  // pinned
     int2* tiles = nullptr;
     std::vector<int2> tiles_h;
     uint32_t tiles_cap = 0;
     std::vector<hipEvent_t> events;
-    int trace_blocks[2] = {0, 0};
     // stage_run scratch
     std::vector<void*> tmp_bufs;
+    float last_stage_ms = 0.f;
 };
 
 static int set_err(mcpt_ctx* c, int rc, const std::string& msg) {
@@ -124,13 +126,6 @@ int mcpt_create(int device, const mcpt_config* cfg, mcpt_ctx** out) {
         return set_err(nullptr, MCPT_E_NOMEM, "counter allocation failed");
     }
     (void)hipMemset(c->cnt, 0, sizeof(CounterBlock));
-    for (int k = 0; k < 2; k++) {
-        int per_cu = 0;
-        // persistent grid: what the occupancy query admits per CU (a plain launch
-        // needs no co-residency here: surplus blocks simply find the queue empty)
-        (void)per_cu;
-        c->trace_blocks[k] = c->num_cu * 8;
-    }
     *out = c;
     return MCPT_OK;
 }
@@ -145,6 +140,8 @@ void mcpt_destroy(mcpt_ctx* c) {
     if (c->cnt) (void)hipFree(c->cnt);
     if (c->cnt_host) (void)hipHostFree(c->cnt_host);
     if (c->tiles) (void)hipFree(c->tiles);
+    if (c->ext_q) (void)hipFree(c->ext_q);
+    if (c->any_q) (void)hipFree(c->any_q);
     for (auto e : c->events) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -284,6 +281,23 @@ int mcpt_camera_set(mcpt_ctx* c, const mcpt_camera* cam) {
 }
 
 static int set_tiles_internal(mcpt_ctx* c, const std::vector<int2>& t) {
+    // per-shard queue capacity: shard = k_shade block mod kShards
+    const uint32_t bpt = (c->tile_w * c->tile_h + kBlock - 1) / kBlock;
+    const uint32_t nblocks = (uint32_t)t.size() * bpt;
+    c->ext_cap = std::max<uint32_t>(1, (nblocks + kShards - 1) / kShards) * kBlock;
+    c->any_cap = 2 * c->ext_cap;
+    const size_t need = (size_t)kShards * c->ext_cap;
+    if (need > c->queue_alloc) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->ext_q) (void)hipFree(c->ext_q);
+        if (c->any_q) (void)hipFree(c->any_q);
+        c->ext_q = c->any_q = nullptr;
+        c->queue_alloc = 0;
+        if (hipMalloc(&c->ext_q, need * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&c->any_q, 2 * need * sizeof(uint32_t)) != hipSuccess)
+            return set_err(c, MCPT_E_NOMEM, "queue allocation failed");
+        c->queue_alloc = need;
+    }
     if (t.size() > c->tiles_cap) {
         if (c->tiles) HIPCHK(c, hipFree(c->tiles));
         c->tiles = nullptr;
@@ -331,9 +345,10 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
         (rc = dalloc(c, c->film_bufs, &p.beta, P)) || (rc = dalloc(c, c->film_bufs, &p.nee0, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.nee1, P)) || (rc = dalloc(c, c->film_bufs, &p.Ld, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.flags, P)) || (rc = dalloc(c, c->film_bufs, &p.samples, P)) ||
-        (rc = dalloc(c, c->film_bufs, &p.vis, 2 * P)) || (rc = dalloc(c, c->film_bufs, &c->ext_q, P)) ||
-        (rc = dalloc(c, c->film_bufs, &c->any_q, 2 * P)))
+        (rc = dalloc(c, c->film_bufs, &p.vis, 2 * P)))
         return rc;
+    c->ext_q = c->any_q = nullptr;
+    c->queue_alloc = 0;
     HIPCHK(c, hipMemset(p.hit_n, 0xff, P * sizeof(float4)));
     HIPCHK(c, hipMemset(p.vis, 0, 2 * P));
     c->p = p;
@@ -391,6 +406,8 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     sa.seed = c->cfg.seed;
     sa.ext_q = c->ext_q;
     sa.any_q = c->any_q;
+    sa.ext_cap = c->ext_cap;
+    sa.any_cap = c->any_cap;
     sa.cnt = c->cnt;
     int bpt = (int)((c->tile_w * c->tile_h + kBlock - 1) / kBlock);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 0), c->stream));
@@ -401,23 +418,25 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     ta.ro = c->p.ray_o;
     ta.rd = c->p.ray_d;
     ta.queue = c->ext_q;
-    ta.count_ptr = &c->cnt->ext;
-    ta.work = &c->cnt->work_ext;
+    ta.count_ptr = &c->cnt->shard[0][C_EXT];
+    ta.shard_cap = c->ext_cap;
+    ta.nshards = kShards;
     ta.hit_p = c->p.hit_p;
     ta.hit_n = c->p.hit_n;
-    ta.stats = &c->cnt->it_stats[0];
-    launch_trace(ta, false, c->trace_blocks[0], c->stream);
+    ta.stats = &c->cnt->shard[0][C_STATS];
+    launch_trace(ta, false, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
     TraceArgs tb{};
     tb.scene = c->scene;
     tb.ro = c->p.sray_o;
     tb.rd = c->p.sray_d;
     tb.queue = c->any_q;
-    tb.count_ptr = &c->cnt->any;
-    tb.work = &c->cnt->work_any;
+    tb.count_ptr = &c->cnt->shard[0][C_ANY];
+    tb.shard_cap = c->any_cap;
+    tb.nshards = kShards;
     tb.vis = c->p.vis;
-    tb.stats = &c->cnt->it_stats[3];
-    launch_trace(tb, true, c->trace_blocks[1], c->stream);
+    tb.stats = &c->cnt->shard[0][C_STATS + 3];
+    launch_trace(tb, true, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 3), c->stream));
     launch_accumulate(c->cnt, c->stream);
     HIPCHK(c, hipGetLastError());
@@ -534,18 +553,16 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
     float4 *dro, *drd, *hp = nullptr, *hn = nullptr;
     int32_t* ht = nullptr;
     uint8_t* vis = nullptr;
-    uint32_t* work;
     int rc;
-    if ((rc = dupload(c, c->tmp_bufs, &dro, ro.data(), n)) || (rc = dupload(c, c->tmp_bufs, &drd, rd.data(), n)) ||
-        (rc = dalloc(c, c->tmp_bufs, &work, 4)))
+    if ((rc = dupload(c, c->tmp_bufs, &dro, ro.data(), n)) || (rc = dupload(c, c->tmp_bufs, &drd, rd.data(), n)))
         return rc;
-    HIPCHK(c, hipMemset(work, 0, 16));
     TraceArgs ta{};
     ta.scene = c->scene;
     ta.ro = dro;
     ta.rd = drd;
     ta.count = n;
-    ta.work = work;
+    ta.shard_cap = (n + kTraceBlock - 1) / kTraceBlock * kTraceBlock;
+    ta.nshards = 1;
     if (stage == MCPT_STAGE_EXTEND) {
         if ((rc = dalloc(c, c->tmp_bufs, &hp, n)) || (rc = dalloc(c, c->tmp_bufs, &hn, n)) || (rc = dalloc(c, c->tmp_bufs, &ht, n)))
             return rc;
@@ -556,9 +573,18 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
         if ((rc = dalloc(c, c->tmp_bufs, &vis, n))) return rc;
         ta.vis = vis;
     }
-    launch_trace(ta, stage == MCPT_STAGE_SHADOW, c->trace_blocks[0], c->stream);
+    uint32_t* steps = nullptr;
+    if (out->steps) {
+        if ((rc = dalloc(c, c->tmp_bufs, &steps, n))) return rc;
+        ta.ray_steps = steps;
+    }
+    HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
+    launch_trace(ta, stage == MCPT_STAGE_SHADOW, c->stream);
+    HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventElapsedTime(&c->last_stage_ms, c->events[0], c->events[1]));
+    if (steps) HIPCHK(c, hipMemcpy(out->steps, steps, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (stage == MCPT_STAGE_EXTEND) {
         std::vector<float4> a(n), b(n);
         HIPCHK(c, hipMemcpy(a.data(), hp, n * sizeof(float4), hipMemcpyDeviceToHost));
@@ -632,3 +658,34 @@ int mcpt_film_tonemap_rgba8(mcpt_ctx* c, float exposure, uint8_t* out) {
 }
 
 }  // extern "C"
+
+extern "C" {
+int mcpt_debug_queue_rays(mcpt_ctx* c, int which, float* ro, float* rd, uint32_t* n_inout) {
+    if (!c || !c->P || !n_inout || (which != 0 && which != 1)) return set_err(c, MCPT_E_INVALID, "bad argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    CounterBlock cb;
+    HIPCHK(c, hipMemcpy(&cb, c->cnt, sizeof(cb), hipMemcpyDeviceToHost));
+    // k_accumulate reset the live counters; the queues still hold the last iteration's entries
+    uint32_t n = which == 0 ? cb.last_ext : 0;
+    if (which == 1) return set_err(c, MCPT_E_INVALID, "any-hit queue length is not retained");
+    if (!ro || !rd) { *n_inout = n; return MCPT_OK; }
+    n = std::min(n, *n_inout);
+    std::vector<uint32_t> all((size_t)kShards * c->ext_cap), q;
+    HIPCHK(c, hipMemcpy(all.data(), c->ext_q, all.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (int sh = 0; sh < kShards; sh++)
+        for (uint32_t k = 0; k < cb.last_ext_shard[sh] && q.size() < n; k++) q.push_back(all[(size_t)sh * c->ext_cap + k]);
+    n = (uint32_t)q.size();
+    std::vector<float4> o(c->P), d(c->P);
+    HIPCHK(c, hipMemcpy(o.data(), c->p.ray_o, c->P * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(d.data(), c->p.ray_d, c->P * sizeof(float4), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; i++) {
+        float4 a = o[q[i]], b = d[q[i]];
+        ro[3 * i] = a.x; ro[3 * i + 1] = a.y; ro[3 * i + 2] = a.z;
+        rd[3 * i] = b.x; rd[3 * i + 1] = b.y; rd[3 * i + 2] = b.z;
+    }
+    *n_inout = n;
+    return MCPT_OK;
+}
+float mcpt_debug_last_stage_ms(const mcpt_ctx* c) { return c ? c->last_stage_ms : -1.f; }
+}

@@ -76,7 +76,7 @@ class StageStats(C.Structure):
 
 class SoaView(C.Structure):
     _fields_ = [("ray_o", _f), ("ray_d", _f), ("hit_pos_t", _f), ("hit_nrm_mat", _f), ("hit_tri", _i),
-                ("visible", C.POINTER(C.c_uint8))]
+                ("visible", C.POINTER(C.c_uint8)), ("steps", _u)]
 
 
 # Every symbol declared in include/mcpt.h with its ctypes signature.
@@ -99,6 +99,8 @@ ABI = {
     "mcpt_film_tonemap_rgba8": (C.c_int, [C.c_void_p, C.c_float, C.POINTER(C.c_uint8)]),
     "mcpt_sync": (C.c_int, [C.c_void_p]),
     "mcpt_device_name": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
+    "mcpt_debug_queue_rays": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _u]),
+    "mcpt_debug_last_stage_ms": (C.c_float, [C.c_void_p]),
     "mcpt_scene_new": (C.c_void_p, []),
     "mcpt_scene_free": (None, [C.c_void_p]),
     "mcpt_scene_load_glb": (C.c_int, [C.c_void_p, C.c_char_p, _f]),
@@ -177,7 +179,10 @@ class Scene:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().mcpt_scene_free(self.h)
+            try:
+                lib().mcpt_scene_free(self.h)
+            except Exception:  # interpreter shutdown
+                pass
             self.h = None
 
     def _ck(self, rc):
@@ -293,7 +298,10 @@ class PathTracer:
 
     def close(self):
         if getattr(self, "h", None):
-            lib().mcpt_destroy(self.h)
+            try:
+                lib().mcpt_destroy(self.h)
+            except Exception:  # interpreter shutdown
+                pass
             self.h = None
 
     __del__ = close
@@ -355,27 +363,44 @@ class PathTracer:
         self._ck(lib().mcpt_film_tonemap_rgba8(self.h, exposure, out.ctypes.data_as(C.POINTER(C.c_uint8))))
         return out.reshape(self.H, self.W, 4)
 
-    def trace_closest(self, ro, rd):
+    def trace_closest(self, ro, rd, steps=False):
         ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
         rd = np.ascontiguousarray(rd, np.float32).reshape(-1, 3)
         n = len(ro)
         pos_t = np.zeros((n, 4), np.float32)
         nrm = np.zeros((n, 4), np.float32)
         tri = np.zeros(n, np.int32)
-        vin = SoaView(fptr(ro), fptr(rd), None, None, None, None)
-        vout = SoaView(None, None, fptr(pos_t), fptr(nrm), tri.ctypes.data_as(_i), None)
+        st = np.zeros(n, np.uint32) if steps else None
+        vin = SoaView(fptr(ro), fptr(rd), None, None, None, None, None)
+        vout = SoaView(None, None, fptr(pos_t), fptr(nrm), tri.ctypes.data_as(_i), None,
+                       st.ctypes.data_as(_u) if steps else None)
         self._ck(lib().mcpt_stage_run(self.h, STAGE_EXTEND, C.byref(vin), C.byref(vout), n))
-        return pos_t, nrm, tri
+        return (pos_t, nrm, tri, st) if steps else (pos_t, nrm, tri)
 
-    def trace_any(self, ro, rd):
+    def trace_any(self, ro, rd, steps=False):
         ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
         rd = np.ascontiguousarray(rd, np.float32).reshape(-1, 3)
         n = len(ro)
         vis = np.zeros(n, np.uint8)
-        vin = SoaView(fptr(ro), fptr(rd), None, None, None, None)
-        vout = SoaView(None, None, None, None, None, vis.ctypes.data_as(C.POINTER(C.c_uint8)))
+        st = np.zeros(n, np.uint32) if steps else None
+        vin = SoaView(fptr(ro), fptr(rd), None, None, None, None, None)
+        vout = SoaView(None, None, None, None, None, vis.ctypes.data_as(C.POINTER(C.c_uint8)),
+                       st.ctypes.data_as(_u) if steps else None)
         self._ck(lib().mcpt_stage_run(self.h, STAGE_SHADOW, C.byref(vin), C.byref(vout), n))
-        return vis
+        return (vis, st) if steps else vis
+
+    @property
+    def last_stage_ms(self) -> float:
+        return lib().mcpt_debug_last_stage_ms(self.h)
+
+    def queue_rays(self):
+        """Rays of the current extension queue (diagnostics)."""
+        n = C.c_uint32(0)
+        self._ck(lib().mcpt_debug_queue_rays(self.h, 0, None, None, C.byref(n)))
+        ro = np.zeros((n.value, 3), np.float32)
+        rd = np.zeros((n.value, 3), np.float32)
+        self._ck(lib().mcpt_debug_queue_rays(self.h, 0, fptr(ro), fptr(rd), C.byref(n)))
+        return ro[: n.value], rd[: n.value]
 
 
 @dataclass(frozen=True)
