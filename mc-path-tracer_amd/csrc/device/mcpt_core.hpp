@@ -9,7 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define MCPT_HD __host__ __device__ inline
+#define MCPT_HD __host__ __device__ inline __attribute__((always_inline))
 
 namespace mcpt {
 

@@ -68,6 +68,48 @@ __device__ inline float light_pdf(const DevScene& sc, int id, V3 wi) {
     return 1.f;  // DirectionalLight.cu:40-43
 }
 
+// Reference slab test (Bounds3f.h:121-153) written branch-free: the same six
+// products and the same comparison sequence, evaluated unconditionally so the
+// whole node is fetched up front (the early-out form let the compiler sink the
+// z loads behind the x/y test: two dependent round trips per node).  NaN slabs
+// compare false and pass, exactly as in the reference.
+__device__ inline bool slab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, V3 o, V3 inv,
+                            int nx, int ny, int nz, float& t0, float& t1) {
+    float bx0 = nx ? mxx : mnx, bx1 = nx ? mnx : mxx;
+    float by0 = ny ? mxy : mny, by1 = ny ? mny : mxy;
+    float bz0 = nz ? mxz : mnz, bz1 = nz ? mnz : mxz;
+    float tmin = (bx0 - o.x) * inv.x;
+    float tmax = (bx1 - o.x) * inv.x;
+    float tymin = (by0 - o.y) * inv.y;
+    float tymax = (by1 - o.y) * inv.y;
+    float tzmin = (bz0 - o.z) * inv.z;
+    float tzmax = (bz1 - o.z) * inv.z;
+    bool miss = (tmin > tymax) || (tymin > tmax);
+    float a = (tymin > tmin) ? tymin : tmin;
+    float b = (tymax < tmax) ? tymax : tmax;
+    miss = miss || (a > tzmax) || (tzmin > b);
+    t0 = (tzmin > a) ? tzmin : a;
+    t1 = (tzmax < b) ? tzmax : b;
+    return !miss;
+}
+constexpr float kCullAbs = 1e-5f;
+constexpr float kCullRel = 1.0f / 256.0f;
+constexpr int kEnd = -1;  // not a valid leaf: offset + count <= ntri < 2^24
+
+__device__ inline bool keep_box(float t0, float t1, float cut) { return !(t1 < -kCullAbs) && !(t0 > cut); }
+
+// The first test trace() makes: a NaN/zero direction or a ray that misses the
+// root box (after the cull) can hit nothing.  k_shade resolves such rays in place
+// instead of queueing them (same result; they are still counted as traced rays).
+__device__ inline bool ray_misses_scene(const DevScene& sc, V3 o, V3 d) {
+    if (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f)) return true;
+    const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    float t0, t1;
+    const float cut = K_HUGE + K_HUGE * kCullRel;
+    return !(slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1], sc.root_mx[2], o, inv,
+                  inv.x < 0.f, inv.y < 0.f, inv.z < 0.f, t0, t1) && keep_box(t0, t1, cut));
+}
+
 // ---------------------------------------------------------------------------
 // k_shade: one thread per pixel of the tile set.
 // ---------------------------------------------------------------------------
@@ -88,7 +130,9 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
         pid = (uint32_t)y * (uint32_t)a.W + (uint32_t)x;
     }
     bool want_ext = false, want_l = false, want_b = false;
-    bool new_path = false;
+    bool new_path = false, trivial_ext = false;
+    uint32_t trivial_any = 0;
+    bool fl_vis_ray = false;
     uint32_t nflags = 0, fl = F_DEAD;
     V3 new_o = v3(0, 0, 0), new_d = v3(0, 0, 0);
     V3 so_l = v3(0, 0, 0), sd_l = v3(0, 0, 0), so_b = v3(0, 0, 0), sd_b = v3(0, 0, 0);
@@ -184,6 +228,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
                     if (wB > 0.f && pdfb_x > 0.f) nf |= F_CONDB;
                     nf |= F_HASVIS;
                     want_b = true;
+                    fl_vis_ray = true;
                 }
                 V3 wi_s = (r(SL_CONT_LOBE) < 0.5f) ? spec_get_wi(m, n, wo, r, SL_CONT_E0) : diff_get_wi(n, r, SL_CONT_E0);
                 float pdf_s = brdf_pdf(m, n, wi_s, wo);
@@ -212,14 +257,32 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
         if (want_ext) {
             a.p.ray_o[pid] = f4(new_o, 0.f);
             a.p.ray_d[pid] = f4(new_d, 0.f);
+            if (ray_misses_scene(sc, new_o, new_d)) {  // resolved here: isect stays "not found"
+                a.p.hit_p[pid] = make_float4(0.f, 0.f, 0.f, K_HUGE);
+                a.p.hit_n[pid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+                want_ext = false;
+                trivial_ext = true;
+            }
         }
         if (want_l) {
-            a.p.sray_o[2 * pid] = f4(so_l, 0.f);
-            a.p.sray_d[2 * pid] = f4(sd_l, 0.f);
+            if (ray_misses_scene(sc, so_l, sd_l)) {
+                a.p.vis[2 * pid] = 1;
+                want_l = false;
+                trivial_any++;
+            } else {
+                a.p.sray_o[2 * pid] = f4(so_l, 0.f);
+                a.p.sray_d[2 * pid] = f4(sd_l, 0.f);
+            }
         }
         if (want_b) {
-            a.p.sray_o[2 * pid + 1] = f4(so_b, 0.f);
-            a.p.sray_d[2 * pid + 1] = f4(sd_b, 0.f);
+            if (ray_misses_scene(sc, so_b, sd_b)) {
+                a.p.vis[2 * pid + 1] = 1;
+                want_b = false;
+                trivial_any++;
+            } else {
+                a.p.sray_o[2 * pid + 1] = f4(so_b, 0.f);
+                a.p.sray_d[2 * pid + 1] = f4(sd_b, 0.f);
+            }
         }
     }
     (void)new_path;
@@ -233,7 +296,19 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
     if (want_ext) a.ext_q[shard * a.ext_cap + slot[0]] = pid;
     if (want_l) a.any_q[shard * a.any_cap + slot[1]] = 2 * pid;
     if (want_b) a.any_q[shard * a.any_cap + slot[2]] = 2 * pid + 1;
-    if (threadIdx.x == 0 && total[2]) atomicAdd(sc_ctr + C_VIS, total[2]);  // BRDF visibility rays
+    // ray statistics: queued + resolved-in-place rays of each kind (per-wave reduce)
+    uint32_t n_ext = want_ext || trivial_ext, n_any = (want_l ? 1u : 0u) + (want_b ? 1u : 0u) + trivial_any;
+    uint32_t n_vis = (fl_vis_ray ? 1u : 0u);
+    for (int off = 32; off > 0; off >>= 1) {
+        n_ext += __shfl_xor(n_ext, off);
+        n_any += __shfl_xor(n_any, off);
+        n_vis += __shfl_xor(n_vis, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
+        if (n_any) atomicAdd(sc_ctr + C_ANY_RAYS, n_any);
+        if (n_vis) atomicAdd(sc_ctr + C_VIS, n_vis);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -246,36 +321,6 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
 // Stack: kLdsStack entries per lane in LDS ([entry][lane], conflict-free),
 // deeper entries in private scratch.
 // ---------------------------------------------------------------------------
-// Reference slab test (Bounds3f.h:121-153) written branch-free: the same six
-// products and the same comparison sequence, evaluated unconditionally so the
-// whole node is fetched up front (the early-out form let the compiler sink the
-// z loads behind the x/y test: two dependent round trips per node).  NaN slabs
-// compare false and pass, exactly as in the reference.
-__device__ inline bool slab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, V3 o, V3 inv,
-                            int nx, int ny, int nz, float& t0, float& t1) {
-    float bx0 = nx ? mxx : mnx, bx1 = nx ? mnx : mxx;
-    float by0 = ny ? mxy : mny, by1 = ny ? mny : mxy;
-    float bz0 = nz ? mxz : mnz, bz1 = nz ? mnz : mxz;
-    float tmin = (bx0 - o.x) * inv.x;
-    float tmax = (bx1 - o.x) * inv.x;
-    float tymin = (by0 - o.y) * inv.y;
-    float tymax = (by1 - o.y) * inv.y;
-    float tzmin = (bz0 - o.z) * inv.z;
-    float tzmax = (bz1 - o.z) * inv.z;
-    bool miss = (tmin > tymax) || (tymin > tmax);
-    float a = (tymin > tmin) ? tymin : tmin;
-    float b = (tymax < tmax) ? tymax : tmax;
-    miss = miss || (a > tzmax) || (tzmin > b);
-    t0 = (tzmin > a) ? tzmin : a;
-    t1 = (tzmax < b) ? tzmax : b;
-    return !miss;
-}
-constexpr float kCullAbs = 1e-5f;
-constexpr float kCullRel = 1.0f / 256.0f;
-constexpr int kEnd = -1;  // not a valid leaf: offset + count <= ntri < 2^24
-
-__device__ inline bool keep_box(float t0, float t1, float cut) { return !(t1 < -kCullAbs) && !(t0 > cut); }
-
 template <bool ANY>
 struct TraceResult { int tri; float t; };
 
@@ -464,11 +509,19 @@ __global__ void k_accumulate(CounterBlock* c) {  // fold per-iteration shard cou
 #pragma unroll
     for (int k = 0; k < C_STATS + 6; k++)
         for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    uint32_t er = c->shard[t][C_EXT_RAYS], ar = c->shard[t][C_ANY_RAYS];
+    c->shard[t][C_EXT_RAYS] = 0;
+    c->shard[t][C_ANY_RAYS] = 0;
+    for (int off = 32; off > 0; off >>= 1) {
+        er += __shfl_xor(er, off);
+        ar += __shfl_xor(ar, off);
+    }
     if (t == 0) {
-        c->tot_ext += v[C_EXT];
-        c->tot_any += v[C_ANY];
+        c->tot_ext += er;
+        c->tot_any += ar;
         c->tot_vis += v[C_VIS];
         c->last_ext = v[C_EXT];
+        c->last_live = er;
         for (int k = 0; k < 6; k++) c->tot_stats[k] += v[C_STATS + k];
     }
 }

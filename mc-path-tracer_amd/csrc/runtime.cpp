@@ -464,7 +464,7 @@ static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st) {
         st->vis_rays = after.tot_vis - before.tot_vis;
         st->shadow_rays = (after.tot_any - before.tot_any) - st->vis_rays;
         st->iterations = n;
-        st->live_paths = after.last_ext;
+        st->live_paths = after.last_live;
         st->ext_nodes = after.tot_stats[0] - before.tot_stats[0];
         st->ext_tests = after.tot_stats[1] - before.tot_stats[1];
         st->ext_hits = after.tot_stats[2] - before.tot_stats[2];

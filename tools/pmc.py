@@ -1,0 +1,63 @@
+"""Summarise rocprofv3 output (gpurun_out/prof_*) into profiles/ (committed evidence).
+
+HBM traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 B: on gfx950 FETCH_SIZE counts
+exactly half the bytes of wide (16 B/lane) coalesced reads (MI355X_MICROARCH.md, HBM section);
+the path-state streams are dwordx4 per lane.  FETCH/WRITE are collected in separate --pmc passes.
+Usage: python tools/pmc.py <round-tag> [gpurun_out]
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+src = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out"
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+dst = os.path.join(REPO, "profiles")
+os.makedirs(dst, exist_ok=True)
+
+
+def find(sub, suffix):
+    d = os.path.join(src, sub)
+    for root, _, files in os.walk(d):
+        for f in files:
+            if f.endswith(suffix):
+                return os.path.join(root, f)
+    return None
+
+
+stats = find("prof_kt", "kernel_stats.csv")
+if stats:
+    shutil.copy(stats, os.path.join(dst, f"kernel_stats_{tag}.csv"))
+pmc = collections.defaultdict(dict)
+for sub, ctr in (("prof_fetch", "FETCH_SIZE"), ("prof_write", "WRITE_SIZE")):
+    f = find(sub, "counter_collection.csv")
+    if not f:
+        continue
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        if r["Counter_Name"] == ctr:
+            acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    for k, v in acc.items():
+        pmc[k][ctr + "_KB_avg"] = sum(v) / len(v)
+        pmc[k]["launches"] = len(v)
+dur = {}
+if stats:
+    for r in csv.DictReader(open(stats)):
+        dur[r["Name"]] = float(r["AverageNs"])
+out = {"round": tag, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on "
+       "'python3 bench.py --no-cpu-baseline --steps 20 --warmup 10'; durations from --kernel-trace --stats",
+       "correction": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE reads half of 16 B/lane streams)",
+       "kernels": {}}
+for k, v in pmc.items():
+    if "FETCH_SIZE_KB_avg" in v and "WRITE_SIZE_KB_avg" in v:
+        b = (2 * v["FETCH_SIZE_KB_avg"] + v["WRITE_SIZE_KB_avg"]) * 1024
+        v["hbm_bytes_per_launch"] = int(b)
+        if k in dur:
+            v["avg_ns"] = dur[k]
+            v["hbm_GBps"] = round(b / dur[k], 1)
+    out["kernels"][k] = v
+json.dump(out, open(os.path.join(dst, f"pmc_{tag}.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))
