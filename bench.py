@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the full-frame CPU-oracle sample")
+    ap.add_argument("--cpu-spp", type=int, default=12, help="spp of the full-frame CPU-oracle sample")
     ap.add_argument("--gather", action="store_true", help="RCCL-gather the film after timing (N>1)")
     return ap.parse_args()
 
