@@ -13,6 +13,9 @@
 // wave64 ballot + mbcnt + an LDS prefix and one atomic per block and queue.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
 
 #include "device/mcpt_core.hpp"
 #include "kernels.hpp"
@@ -110,6 +113,25 @@ __device__ inline bool ray_misses_scene(const DevScene& sc, V3 o, V3 d) {
                   inv.x < 0.f, inv.y < 0.f, inv.z < 0.f, t0, t1) && keep_box(t0, t1, cut));
 }
 
+// Hit record of ray (o, d) on triangle tri, as dTriangle::hit builds it
+// (Triangle.cu:66-92): Moller-Trumbore t/u/v, the interpolated normal
+// normalised twice (identity transform), position o + t d, material id.
+__device__ inline void hit_record(const DevScene& sc, V3 o, V3 d, int tri, V3& pos, V3& nrm, int& mat, float& t_out) {
+    const float4* tp = sc.tri + 3 * tri;
+    const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
+    float t, u, v;
+    tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v);
+    const float4* sp4 = sc.tri_sh + 3 * tri;
+    const float4 s0 = sp4[0], s1 = sp4[1], s2 = sp4[2];
+    const V3 n0 = v3(s0.x, s0.y, s0.z), n1 = v3(s0.w, s1.x, s1.y), n2 = v3(s1.z, s1.w, s2.x);
+    const float w = (1.f - u) - v;
+    nrm = normalize((n1 * u + n2 * v) + n0 * w);  // Triangle.cu:76
+    nrm = normalize(nrm);                          // identity transform, :82
+    pos = o + d * t;                               // :86
+    mat = __float_as_int(s2.y);                    // material id bits
+    t_out = t;
+}
+
 // ---------------------------------------------------------------------------
 // k_shade: one thread per pixel of the tile set.
 // ---------------------------------------------------------------------------
@@ -145,9 +167,8 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
         if (!dead && samples < spp) {  // wavefront_kernels.cu:124
             const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
             const Rng r{rng_key(a.seed, pid, samples), len};
-            float4 hn = a.p.hit_n[pid];
-            const int mat = __float_as_int(hn.w);
-            const bool found = mat >= 0;
+            const int htri = a.p.hit_tri[pid];
+            const bool found = htri >= 0;
             float4 b4 = a.p.beta[pid];
             const V3 B = xyz(b4);
             float4 ld4 = a.p.Ld[pid];
@@ -194,9 +215,12 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
                 nflags = F_DEAD;
             } else {
                 // ---- continue: light choice (:207-215) fused with wf_mat_mix (:295-375)
-                float4 hp = a.p.hit_p[pid];
-                const V3 pos = xyz(hp), n = xyz(hn);
-                wo = -xyz(a.p.ray_d[pid]);
+                const V3 ro = xyz(a.p.ray_o[pid]), rdir = xyz(a.p.ray_d[pid]);
+                V3 pos, n;
+                int mat;
+                float t_hit;
+                hit_record(sc, ro, rdir, htri, pos, n, mat, t_hit);
+                wo = -rdir;
                 int l_id = (int)(r(SL_LIGHT) * (float)(sc.nlights - 0) + (float)0);
                 const int light_id = (l_id == sc.nlights) ? 0 : l_id;
                 V3 ldir;
@@ -258,8 +282,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
             a.p.ray_o[pid] = f4(new_o, 0.f);
             a.p.ray_d[pid] = f4(new_d, 0.f);
             if (ray_misses_scene(sc, new_o, new_d)) {  // resolved here: isect stays "not found"
-                a.p.hit_p[pid] = make_float4(0.f, 0.f, 0.f, K_HUGE);
-                a.p.hit_n[pid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+                a.p.hit_tri[pid] = -1;
                 want_ext = false;
                 trivial_ext = true;
             }
@@ -341,7 +364,9 @@ __device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*
     const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;
     float best = K_HUGE;
     float cut = best + best * kCullRel;
+#ifndef MCPT_X_NOSPILL
     int2 spill[kMaxStack - kLdsStack];
+#endif
     int sp = 0;
     float t0, t1;
     if (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1], sc.root_mx[2], o, inv, nx, ny,
@@ -351,7 +376,11 @@ __device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*
     auto pop = [&]() -> int {
         while (sp > 0) {
             sp--;
+#ifndef MCPT_X_NOSPILL
             int2 e = (sp < kLdsStack) ? stk[sp][lane_slot] : spill[sp - kLdsStack];
+#else
+            int2 e = stk[sp < kLdsStack ? sp : kLdsStack - 1][lane_slot];
+#endif
             if (!ANY && __int_as_float(e.y) > cut) continue;
             return e.x;
         }
@@ -370,8 +399,12 @@ __device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*
             if (h0 && h1) {
                 const bool first0 = !(a1 < a0);
                 const int2 e = make_int2(first0 ? c1 : c0, __float_as_int(first0 ? a1 : a0));
+#ifndef MCPT_X_NOSPILL
                 if (sp < kLdsStack) stk[sp][lane_slot] = e;
                 else spill[sp - kLdsStack] = e;
+#else
+                stk[sp < kLdsStack ? sp : kLdsStack - 1][lane_slot] = e;
+#endif
                 sp++;
                 ref = first0 ? c0 : c1;
             } else if (h0 | h1) {
@@ -406,6 +439,33 @@ __device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*
     return res;
 }
 
+
+// Write one traced ray's result: the visibility byte (any-hit) or the closest
+// triangle index (-1: none).  The hit record (position, normal, material) is
+// rebuilt from the index where it is consumed (hit_record()), which keeps this
+// divergent kernel's finish path short.
+template <bool ANY>
+__device__ inline void store_result(const TraceArgs& a, uint32_t rid, int tri) {
+    if (ANY) a.vis[rid] = (uint8_t)(tri < 0);
+    else a.hit_tri[rid] = tri;
+}
+
+// Traversal work counters: wave-reduce, one atomic per counter per wave.
+__device__ inline void wave_stats(const TraceArgs& a, int lane, uint32_t nodes, uint32_t tests, uint32_t hits) {
+    if (!a.stats) return;
+    for (int off = 32; off > 0; off >>= 1) {
+        nodes += __shfl_xor(nodes, off);
+        tests += __shfl_xor(tests, off);
+        hits += __shfl_xor(hits, off);
+    }
+    if (lane == 0) {
+        uint32_t* st = a.stats + (blockIdx.x % kShards) * C_WORDS;
+        atomicAdd(st + 0, nodes);
+        atomicAdd(st + 1, tests);
+        atomicAdd(st + 2, hits);
+    }
+}
+
 // Trace kernel: one wave per block, one ray per lane; the grid covers the largest
 // possible queue and lanes beyond the device-side count exit at once.  (A
 // persistent variant pulling 64 rays per atomic serialised on the single work
@@ -429,45 +489,186 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(TraceArgs a) {
         TraceResult<ANY> tr = trace<ANY>(a.scene, o, d, stk, threadIdx.x, nodes, tests);
         hits += tr.tri >= 0;
         if (a.ray_steps) a.ray_steps[i] = nodes + tests - n0;
-        if (ANY) {
-            a.vis[rid] = (uint8_t)(tr.tri < 0);
-        } else {
-            const uint32_t pid = rid;
-            if (tr.tri >= 0) {
-                const float4* tp = a.scene.tri + 3 * tr.tri;
-                float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-                float t, u, v;
-                tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v);
-                const float4* sp4 = a.scene.tri_sh + 3 * tr.tri;
-                float4 s0 = sp4[0], s1 = sp4[1], s2 = sp4[2];
-                V3 n0 = v3(s0.x, s0.y, s0.z), n1 = v3(s0.w, s1.x, s1.y), n2 = v3(s1.z, s1.w, s2.x);
-                float w = (1.f - u) - v;
-                V3 nn = normalize((n1 * u + n2 * v) + n0 * w);  // Triangle.cu:76
-                nn = normalize(nn);                              // identity transform, :82
-                V3 p = o + d * t;                                // :86
-                a.hit_p[pid] = make_float4(p.x, p.y, p.z, t);
-                a.hit_n[pid] = make_float4(nn.x, nn.y, nn.z, s2.y);  // s2.y = material id bits
-                if (a.hit_tri) a.hit_tri[pid] = tr.tri;
+        store_result<ANY>(a, rid, tr.tri);
+    }
+    wave_stats(a, lane, nodes, tests, hits);
+}
+
+// Persistent traversal with lane refill, one unit of work per lane per loop
+// trip ("if-if": a node pair test OR one triangle test, then a pop if needed).
+// The grid is sized to the resident wave count; wave w of shard s owns the
+// shard's 64-ray chunks w, w + W, w + 2W, ... (W waves per shard), read as one
+// sequence, and whenever lanes are idle at the top of the loop they take the
+// next rays of that sequence.  With one ray per lane and while-while loops the
+// lanes sat ~83% idle (VALUUtilization 17%, profiles/pmc_r01): every descent ran
+// as long as the wave's longest one and every wave as long as its slowest ray.
+// No atomics: the split is static, balanced by the many chunks each wave owns.
+// A leaf is consumed one triangle per trip by stepping its encoding in place
+// (offset + 1, count - 1).  Per ray the visit order, culling and result are
+// exactly those of trace<ANY>().
+template <bool ANY>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_p(TraceArgs a) {
+    __shared__ int2 stk[kLdsStack][kTraceBlock];
+    const int lane = threadIdx.x;
+    const uint32_t nsh = (uint32_t)a.nshards;
+    const uint32_t wps = gridDim.x / nsh;  // waves per shard (host: gridDim.x % nsh == 0)
+    const uint32_t shard = blockIdx.x % nsh, w_in = blockIdx.x / nsh;
+    const uint32_t n = a.count_ptr ? a.count_ptr[shard * C_WORDS] : a.count;
+    const uint32_t nchunks = (n + 63) >> 6;
+    if (w_in >= nchunks) return;
+    const uint32_t L = ((nchunks - w_in + wps - 1) / wps) << 6;  // this wave's sequence length
+    const uint32_t qbase = shard * a.shard_cap;
+    const DevScene& sc = a.scene;
+
+    uint32_t nodes = 0, tests = 0, hits = 0;
+    uint32_t next = 0;  // wave-uniform position in the sequence
+    bool act = false;
+    uint32_t rid = 0, qi = 0, step0 = 0;
+    V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
+    int nx = 0, ny = 0, nz = 0, ref = kEnd, sp = 0, tri = -1;
+    float best = K_HUGE, cut = K_HUGE;
+#ifndef MCPT_X_NOSPILL
+    int2 spill[kMaxStack - kLdsStack];
+#endif
+    auto pop = [&]() -> int {
+        while (sp > 0) {
+            sp--;
+            int2 e;
+#ifndef MCPT_X_NOSPILL
+            if (sp < kLdsStack) {
+                e = stk[sp][lane];
             } else {
-                a.hit_p[pid] = make_float4(0.f, 0.f, 0.f, K_HUGE);
-                a.hit_n[pid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-                if (a.hit_tri) a.hit_tri[pid] = -1;
+                e = spill[sp - kLdsStack];
+                __asm__ volatile("" : "+v"(e.x), "+v"(e.y));  // keep the LDS load an LDS load (no flat merge)
             }
+#else
+            e = stk[sp < kLdsStack ? sp : kLdsStack - 1][lane];
+#endif
+            if (!ANY && __int_as_float(e.y) > cut) continue;
+            return e.x;
+        }
+        return kEnd;
+    };
+    auto finish = [&]() {
+        hits += tri >= 0;
+        if (a.ray_steps) a.ray_steps[qi] = nodes + tests - step0;
+        store_result<ANY>(a, rid, tri);
+        act = false;
+    };
+    for (;;) {
+        // ---- refill idle lanes from the wave's sequence
+        const uint64_t idle = __ballot(!act);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (next < L && (nidle >= a.refill_min || nidle == 64u)) {
+            if (!act) {
+                const uint32_t q = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                const uint32_t s = next + q;
+                const uint32_t k = (w_in + (s >> 6) * wps) * 64u + (s & 63u);
+                if (s < L && k < n) {
+                    qi = qbase + k;
+                    rid = a.queue ? a.queue[qi] : qi;
+                    const float4 o4 = a.ro[rid], d4 = a.rd[rid];
+                    o = xyz(o4);
+                    d = xyz(d4);
+                    step0 = nodes + tests;
+                    tri = -1;
+                    best = K_HUGE;
+                    cut = best + best * kCullRel;
+                    sp = 0;
+                    act = true;
+                    // NaN / zero direction: a miss / visible
+                    if (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f)) {
+                        finish();
+                    } else {
+                        inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+                        nx = inv.x < 0.f;
+                        ny = inv.y < 0.f;
+                        nz = inv.z < 0.f;
+                        float t0, t1;
+                        if (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1],
+                                  sc.root_mx[2], o, inv, nx, ny, nz, t0, t1) ||
+                            !keep_box(t0, t1, cut))
+                            finish();
+                        else
+                            ref = sc.root_ref;
+                    }
+                }
+            }
+            next += nidle;
+        }
+        if (__ballot(act) == 0) {
+            if (next >= L) break;
+            continue;
+        }
+        if (act) {
+            bool need_pop;
+            if (ref >= 0) {  // ---- interior node: test both child boxes
+                const float4* nd = sc.nodes + 4 * ref;
+                const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+                nodes++;
+                float a0, b0, a1, b1;
+                bool h0 = slab(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, o, inv, nx, ny, nz, a0, b0) && keep_box(a0, b0, cut);
+                bool h1 = slab(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, o, inv, nx, ny, nz, a1, b1) && keep_box(a1, b1, cut);
+                const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
+                need_pop = !(h0 | h1);
+                if (h0 && h1) {
+                    const bool first0 = !(a1 < a0);
+                    const int2 e = make_int2(first0 ? c1 : c0, __float_as_int(first0 ? a1 : a0));
+#ifndef MCPT_X_NOSPILL
+                    if (sp < kLdsStack) stk[sp][lane] = e;
+                    else spill[sp - kLdsStack] = e;
+#else
+                    stk[sp < kLdsStack ? sp : kLdsStack - 1][lane] = e;
+#endif
+                    sp++;
+                    ref = first0 ? c0 : c1;
+                } else {
+                    ref = h0 ? c0 : c1;
+                }
+            } else {  // ---- leaf: one triangle
+                const int id = ref & 0xffffff;
+                const float4* tp = sc.tri + 3 * id;
+                const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
+                tests++;
+                float t, u, v;
+                bool done = false;
+                if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) &&
+                    !(t < 0.f)) {
+                    if (ANY) {
+                        if (t < K_HUGE) { tri = id; done = true; }
+                    } else if (t < best || (t == best && id < tri)) {
+                        best = t;
+                        tri = id;
+                        cut = best + best * kCullRel;
+                    }
+                }
+                need_pop = !done && (ref & 0x07000000) == 0;  // last triangle of the leaf
+                if (done) ref = kEnd;
+                else if (!need_pop) ref += 1 - (1 << 24);      // next triangle: offset + 1, count - 1
+            }
+            if (need_pop) ref = pop();
+            if (ref == kEnd) finish();
         }
     }
-    if (a.stats) {  // traversal work counters: wave-reduce, one atomic per wave
-        for (int off = 32; off > 0; off >>= 1) {
-            nodes += __shfl_xor(nodes, off);
-            tests += __shfl_xor(tests, off);
-            hits += __shfl_xor(hits, off);
-        }
-        if (lane == 0) {
-            uint32_t* st = a.stats + (blockIdx.x % kShards) * C_WORDS;
-            atomicAdd(st + 0, nodes);
-            atomicAdd(st + 1, tests);
-            atomicAdd(st + 2, hits);
-        }
+    wave_stats(a, lane, nodes, tests, hits);
+}
+
+__global__ void k_hit_record(HitRecordArgs a) {  // stage_run(EXTEND) outputs
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const int tri = a.tri[i];
+    if (tri < 0) {
+        a.hit_p[i] = make_float4(0.f, 0.f, 0.f, K_HUGE);
+        a.hit_n[i] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+        return;
     }
+    V3 pos, nrm;
+    int mat;
+    float t;
+    hit_record(a.scene, xyz(a.ro[i]), xyz(a.rd[i]), tri, pos, nrm, mat, t);
+    a.hit_p[i] = make_float4(pos.x, pos.y, pos.z, t);
+    a.hit_n[i] = make_float4(nrm.x, nrm.y, nrm.z, __int_as_float(mat));
 }
 
 __global__ void k_clear(ClearArgs a) {  // g_clear_dfilm (wavefront_kernels.cu:55-66)
@@ -548,7 +749,51 @@ __global__ void k_pack(PackArgs a) {  // tile-set pixels -> packed 16 B/px (for 
 void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s) {
     hipLaunchKernelGGL(k_shade, dim3(nblocks), dim3(kBlock), 0, s, a);
 }
-void launch_trace(const TraceArgs& a, bool any, hipStream_t s) {
+// Trace kernel choice: persistent lane-refill waves (default) or one ray per lane
+// (MCPT_TRACE_KERNEL=ray, kept for A/B measurement).  MCPT_TRACE_WAVES overrides
+// the resident waves per CU the persistent grid is sized for.
+static int trace_mode() {
+    static int mode = [] {
+        const char* e = getenv("MCPT_TRACE_KERNEL");
+        return (e && !strcmp(e, "ray")) ? 0 : 1;
+    }();
+    return mode;
+}
+static uint32_t persistent_waves(bool any) {
+    static uint32_t w[2] = {0, 0};
+    if (!w[any]) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (any) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_p<true>, kTraceBlock, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_p<false>, kTraceBlock, 0);
+        if (const char* e = getenv("MCPT_TRACE_WAVES")) per_cu = atoi(e);
+        if (cus <= 0) cus = 256;
+        if (per_cu <= 0) per_cu = 16;
+        w[any] = (uint32_t)(cus * per_cu);
+    }
+    return w[any];
+}
+static uint32_t refill_min() {
+    static uint32_t m = [] {
+        const char* e = getenv("MCPT_REFILL_MIN");
+        int v = e ? atoi(e) : 16;
+        return (uint32_t)std::min(64, std::max(1, v));
+    }();
+    return m;
+}
+void launch_trace(const TraceArgs& args, bool any, hipStream_t s) {
+    if (args.nshards <= 0 || args.shard_cap == 0) return;
+    TraceArgs a = args;
+    a.refill_min = refill_min();
+    if (trace_mode() == 1) {
+        const uint32_t nsh = (uint32_t)a.nshards;
+        const uint32_t wps = std::max<uint32_t>(1, persistent_waves(any) / nsh);
+        const uint32_t nblocks = wps * nsh;
+        if (any) hipLaunchKernelGGL(k_trace_p<true>, dim3(nblocks), dim3(kTraceBlock), 0, s, a);
+        else hipLaunchKernelGGL(k_trace_p<false>, dim3(nblocks), dim3(kTraceBlock), 0, s, a);
+        return;
+    }
     const uint32_t nblocks = (uint32_t)(((uint64_t)a.nshards * a.shard_cap + kTraceBlock - 1) / kTraceBlock);
     if (nblocks == 0) return;
     if (any) hipLaunchKernelGGL(k_trace<true>, dim3(nblocks), dim3(kTraceBlock), 0, s, a);
@@ -556,6 +801,9 @@ void launch_trace(const TraceArgs& a, bool any, hipStream_t s) {
 }
 void launch_clear(const ClearArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_clear, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+}
+void launch_hit_record(const HitRecordArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_hit_record, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 void launch_tonemap(const TonemapArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_tonemap, dim3((a.n + 255) / 256), dim3(256), 0, s, a);

@@ -25,7 +25,10 @@ namespace mcpt_dev {
 
 constexpr int kBlock = 256;
 constexpr int kTraceBlock = 64;  // one wave per traversal block
-constexpr int kLdsStack = 8;   // traversal stack entries per lane kept in LDS (deeper: scratch)
+#ifndef MCPT_LDS_STACK
+#define MCPT_LDS_STACK 8
+#endif
+constexpr int kLdsStack = MCPT_LDS_STACK;  // traversal stack entries per lane kept in LDS (deeper: scratch)
 constexpr int kMaxStack = 64;  // total (reference: int nodesToVisit[64], Triangle.cu:161)
 
 enum : uint32_t {
@@ -50,7 +53,8 @@ struct DevScene {
 };
 
 struct DevPaths {
-    float4 *ray_o, *ray_d, *hit_p, *hit_n, *sray_o, *sray_d, *beta, *nee0, *nee1, *Ld;
+    float4 *ray_o, *ray_d, *sray_o, *sray_d, *beta, *nee0, *nee1, *Ld;
+    int32_t* hit_tri;  // closest hit of the extension ray (-1: none); k_shade rebuilds the hit record
     uint32_t *flags, *samples;
     uint8_t* vis;
 };
@@ -90,13 +94,14 @@ struct TraceArgs {
     uint32_t count;
     uint32_t shard_cap;         // queue entries per shard (queue[s * shard_cap + k])
     int nshards;
-    float4 *hit_p, *hit_n;      // closest-hit outputs
-    int32_t* hit_tri;           // optional
+    int32_t* hit_tri;           // closest-hit output: triangle index or -1
     uint8_t* vis;               // any-hit output
     uint32_t* stats;            // optional: shard s counters at stats[s * C_WORDS + 0..2]
     uint32_t* ray_steps;        // optional per-ray node fetches + triangle tests (diagnostics)
+    uint32_t refill_min;        // persistent kernel: refill when at least this many lanes are idle (set by launch_trace)
 };
 
+struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; uint32_t n; };
 struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n; };
 struct TonemapArgs { const float4* Ld; const uint32_t* samples; uchar4* out; float exposure; uint32_t n; };
 struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* out; };
@@ -104,6 +109,7 @@ struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; 
 void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s);
 void launch_trace(const TraceArgs& a, bool any, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
+void launch_hit_record(const HitRecordArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);
 void launch_accumulate(CounterBlock* c, hipStream_t s);
 void launch_pack(const PackArgs& a, hipStream_t s);

@@ -340,7 +340,7 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
     DevPaths p{};
     int rc;
     if ((rc = dalloc(c, c->film_bufs, &p.ray_o, P)) || (rc = dalloc(c, c->film_bufs, &p.ray_d, P)) ||
-        (rc = dalloc(c, c->film_bufs, &p.hit_p, P)) || (rc = dalloc(c, c->film_bufs, &p.hit_n, P)) ||
+        (rc = dalloc(c, c->film_bufs, &p.hit_tri, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.sray_o, 2 * P)) || (rc = dalloc(c, c->film_bufs, &p.sray_d, 2 * P)) ||
         (rc = dalloc(c, c->film_bufs, &p.beta, P)) || (rc = dalloc(c, c->film_bufs, &p.nee0, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.nee1, P)) || (rc = dalloc(c, c->film_bufs, &p.Ld, P)) ||
@@ -349,7 +349,7 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
         return rc;
     c->ext_q = c->any_q = nullptr;
     c->queue_alloc = 0;
-    HIPCHK(c, hipMemset(p.hit_n, 0xff, P * sizeof(float4)));
+    HIPCHK(c, hipMemset(p.hit_tri, 0xff, P * sizeof(int32_t)));
     HIPCHK(c, hipMemset(p.vis, 0, 2 * P));
     c->p = p;
     c->P = P;
@@ -421,8 +421,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     ta.count_ptr = &c->cnt->shard[0][C_EXT];
     ta.shard_cap = c->ext_cap;
     ta.nshards = kShards;
-    ta.hit_p = c->p.hit_p;
-    ta.hit_n = c->p.hit_n;
+    ta.hit_tri = c->p.hit_tri;
     ta.stats = &c->cnt->shard[0][C_STATS];
     launch_trace(ta, false, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
@@ -566,8 +565,6 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
     if (stage == MCPT_STAGE_EXTEND) {
         if ((rc = dalloc(c, c->tmp_bufs, &hp, n)) || (rc = dalloc(c, c->tmp_bufs, &hn, n)) || (rc = dalloc(c, c->tmp_bufs, &ht, n)))
             return rc;
-        ta.hit_p = hp;
-        ta.hit_n = hn;
         ta.hit_tri = ht;
     } else {
         if ((rc = dalloc(c, c->tmp_bufs, &vis, n))) return rc;
@@ -581,6 +578,10 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
     HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
     launch_trace(ta, stage == MCPT_STAGE_SHADOW, c->stream);
     HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
+    if (stage == MCPT_STAGE_EXTEND) {
+        HitRecordArgs ha{c->scene, dro, drd, ht, hp, hn, n};
+        launch_hit_record(ha, c->stream);
+    }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipEventElapsedTime(&c->last_stage_ms, c->events[0], c->events[1]));

@@ -23,7 +23,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.dirname(_HERE)
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "libmcpt.so")
+LIB_PATH = os.environ.get("MCPT_LIB") or os.path.join(PKG_DIR, "libmcpt.so")
 ASSET_DIR = os.path.join(REPO_DIR, "assets")
 
 MCPT_OK = 0
