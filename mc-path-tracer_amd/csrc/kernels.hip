@@ -95,7 +95,26 @@ __device__ inline bool slab(float mnx, float mny, float mnz, float mxx, float mx
     t1 = (tzmax < b) ? tzmax : b;
     return !miss;
 }
+// Same decisions as slab() for rays whose inverse direction is finite in all
+// three components (no slab product can be NaN then): per axis the entry t is
+// <= the exit t (monotone rounding), so the reference's pairwise overlap tests
+// reduce to max3(entries) <= min3(exits) (Helly in 1-D), and the returned t0/t1
+// equal the reference's running max/min up to the sign of zero.  Rays with an
+// infinite inverse component take slab().
+__device__ inline bool slab_fast(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, V3 o, V3 inv,
+                                 int nx, int ny, int nz, float& t0, float& t1) {
+    float bx0 = nx ? mxx : mnx, bx1 = nx ? mnx : mxx;
+    float by0 = ny ? mxy : mny, by1 = ny ? mny : mxy;
+    float bz0 = nz ? mxz : mnz, bz1 = nz ? mnz : mxz;
+    const float tmin = (bx0 - o.x) * inv.x, tmax = (bx1 - o.x) * inv.x;
+    const float tymin = (by0 - o.y) * inv.y, tymax = (by1 - o.y) * inv.y;
+    const float tzmin = (bz0 - o.z) * inv.z, tzmax = (bz1 - o.z) * inv.z;
+    t0 = __builtin_fmaxf(__builtin_fmaxf(tmin, tymin), tzmin);
+    t1 = __builtin_fminf(__builtin_fminf(tmax, tymax), tzmax);
+    return t0 <= t1;
+}
 constexpr float kCullAbs = 1e-5f;
+constexpr float K_INF_F = __builtin_huge_valf();
 constexpr float kCullRel = 1.0f / 256.0f;
 constexpr int kEnd = -1;  // not a valid leaf: offset + count <= ntri < 2^24
 
@@ -506,8 +525,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(TraceArgs a) {
 // A leaf is consumed one triangle per trip by stepping its encoding in place
 // (offset + 1, count - 1).  Per ray the visit order, culling and result are
 // exactly those of trace<ANY>().
+#ifdef MCPT_TRACE_WPE
+#define MCPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_TRACE_WPE, MCPT_TRACE_WPE)))
+#else
+#define MCPT_TRACE_ATTR
+#endif
 template <bool ANY>
-__global__ __launch_bounds__(kTraceBlock) void k_trace_p(TraceArgs a) {
+__global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace_p(TraceArgs a) {
     __shared__ int2 stk[kLdsStack][kTraceBlock];
     const int lane = threadIdx.x;
     const uint32_t nsh = (uint32_t)a.nshards;
@@ -525,7 +549,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_p(TraceArgs a) {
     bool act = false;
     uint32_t rid = 0, qi = 0, step0 = 0;
     V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
-    int nx = 0, ny = 0, nz = 0, ref = kEnd, sp = 0, tri = -1;
+    int nx = 0, ny = 0, nz = 0, ref = kEnd, leaf = kEnd, sp = 0, tri = -1;
+    bool fin = true;  // inverse direction finite: slab_fast() is exact
     float best = K_HUGE, cut = K_HUGE;
 #ifndef MCPT_X_NOSPILL
     int2 spill[kMaxStack - kLdsStack];
@@ -576,6 +601,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_p(TraceArgs a) {
                     best = K_HUGE;
                     cut = best + best * kCullRel;
                     sp = 0;
+                    leaf = kEnd;
                     act = true;
                     // NaN / zero direction: a miss / visible
                     if (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f)) {
@@ -585,6 +611,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_p(TraceArgs a) {
                         nx = inv.x < 0.f;
                         ny = inv.y < 0.f;
                         nz = inv.z < 0.f;
+                        fin = __builtin_fabsf(inv.x) < K_INF_F && __builtin_fabsf(inv.y) < K_INF_F &&
+                              __builtin_fabsf(inv.z) < K_INF_F;
                         float t0, t1;
                         if (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1],
                                   sc.root_mx[2], o, inv, nx, ny, nz, t0, t1) ||
@@ -601,15 +629,24 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_p(TraceArgs a) {
             if (next >= L) break;
             continue;
         }
+        // ---- node phase: one child-pair test per lane holding an interior node
         if (act) {
-            bool need_pop;
-            if (ref >= 0) {  // ---- interior node: test both child boxes
+            bool need_pop = false;
+            if (ref >= 0) {
                 const float4* nd = sc.nodes + 4 * ref;
                 const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
                 nodes++;
                 float a0, b0, a1, b1;
-                bool h0 = slab(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, o, inv, nx, ny, nz, a0, b0) && keep_box(a0, b0, cut);
-                bool h1 = slab(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, o, inv, nx, ny, nz, a1, b1) && keep_box(a1, b1, cut);
+                bool h0, h1;
+                if (fin) {
+                    h0 = slab_fast(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, o, inv, nx, ny, nz, a0, b0);
+                    h1 = slab_fast(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, o, inv, nx, ny, nz, a1, b1);
+                } else {
+                    h0 = slab(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, o, inv, nx, ny, nz, a0, b0);
+                    h1 = slab(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, o, inv, nx, ny, nz, a1, b1);
+                }
+                h0 = h0 && keep_box(a0, b0, cut);
+                h1 = h1 && keep_box(a1, b1, cut);
                 const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
                 need_pop = !(h0 | h1);
                 if (h0 && h1) {
@@ -626,8 +663,22 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_p(TraceArgs a) {
                 } else {
                     ref = h0 ? c0 : c1;
                 }
-            } else {  // ---- leaf: one triangle
-                const int id = ref & 0xffffff;
+            }
+            // a reached leaf is parked in the lane's leaf slot and traversal
+            // continues speculatively with the next stack entry
+            if (!need_pop && ref < 0 && ref != kEnd && leaf == kEnd) {
+                leaf = ref;
+                need_pop = true;
+            }
+            if (need_pop) ref = pop();
+        }
+        // ---- triangle phase (wave-uniform): when enough lanes have a parked
+        // leaf, or no lane has node work left, each parked leaf tests one triangle
+        const uint32_t n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
+        const uint32_t n_node = (uint32_t)__popcll(__ballot(act && ref >= 0));
+        if (n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node)) {
+            if (leaf != kEnd) {
+                const int id = leaf & 0xffffff;
                 const float4* tp = sc.tri + 3 * id;
                 const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
                 tests++;
@@ -643,13 +694,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_p(TraceArgs a) {
                         cut = best + best * kCullRel;
                     }
                 }
-                need_pop = !done && (ref & 0x07000000) == 0;  // last triangle of the leaf
-                if (done) ref = kEnd;
-                else if (!need_pop) ref += 1 - (1 << 24);      // next triangle: offset + 1, count - 1
+                if (done) {  // any-hit: occluded, drop the rest of the traversal
+                    leaf = kEnd;
+                    ref = kEnd;
+                } else {
+                    leaf = (leaf & 0x07000000) == 0 ? kEnd : leaf + 1 - (1 << 24);  // offset + 1, count - 1
+                }
             }
-            if (need_pop) ref = pop();
-            if (ref == kEnd) finish();
         }
+        if (act && ref == kEnd && leaf == kEnd) finish();
     }
     wave_stats(a, lane, nodes, tests, hits);
 }
@@ -774,6 +827,11 @@ static uint32_t persistent_waves(bool any) {
     }
     return w[any];
 }
+static uint32_t env_u32(const char* name, int def, int lo, int hi) {
+    const char* e = getenv(name);
+    int v = e ? atoi(e) : def;
+    return (uint32_t)std::min(hi, std::max(lo, v));
+}
 static uint32_t refill_min() {
     static uint32_t m = [] {
         const char* e = getenv("MCPT_REFILL_MIN");
@@ -786,6 +844,8 @@ void launch_trace(const TraceArgs& args, bool any, hipStream_t s) {
     if (args.nshards <= 0 || args.shard_cap == 0) return;
     TraceArgs a = args;
     a.refill_min = refill_min();
+    static const uint32_t tri_min = env_u32("MCPT_TRI_MIN", 16, 0, 64);
+    a.tri_min = tri_min;
     if (trace_mode() == 1) {
         const uint32_t nsh = (uint32_t)a.nshards;
         const uint32_t wps = std::max<uint32_t>(1, persistent_waves(any) / nsh);

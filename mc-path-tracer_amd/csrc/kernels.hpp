@@ -99,6 +99,7 @@ struct TraceArgs {
     uint32_t* stats;            // optional: shard s counters at stats[s * C_WORDS + 0..2]
     uint32_t* ray_steps;        // optional per-ray node fetches + triangle tests (diagnostics)
     uint32_t refill_min;        // persistent kernel: refill when at least this many lanes are idle (set by launch_trace)
+    uint32_t tri_min;           // persistent kernel: run the triangle phase when this many lanes hold a leaf
 };
 
 struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; uint32_t n; };
