@@ -60,7 +60,7 @@ def pmc_traffic(kernel_prefix):
     try:
         d = json.load(open(files[-1]))
         for k, v in d.get("kernels", {}).items():
-            if k.startswith(kernel_prefix):
+            if any(k.startswith(p) for p in kernel_prefix):
                 return v.get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -154,13 +154,13 @@ def main():
     dom = max(kern, key=kern.get)
     if dom == "k_trace<closest>":
         byts = (B_EXT_STATE * st.extend_rays + 2 * B_NODE * st.ext_nodes + B_TRI * st.ext_tests + B_HIT * st.ext_hits)
-        prefix = "void mcpt_dev::k_trace<false>"
+        prefix = ("void mcpt_dev::k_trace_p<false>", "void mcpt_dev::k_trace<false>")
     elif dom == "k_trace<any>":
         byts = (B_ANY_STATE * (st.shadow_rays + st.vis_rays) + 2 * B_NODE * st.any_nodes + B_TRI * st.any_tests)
-        prefix = "void mcpt_dev::k_trace<true>"
+        prefix = ("void mcpt_dev::k_trace_p<true>", "void mcpt_dev::k_trace<true>")
     else:
         byts = B_SHADE * st.shadow_rays + B_GEN * (st.extend_rays - st.shadow_rays)
-        prefix = "mcpt_dev::k_shade"
+        prefix = ("mcpt_dev::k_shade",)
     per_launch = byts / K
     avg_ms = kern[dom] / K
     achieved = per_launch / (avg_ms * 1e-3)
@@ -172,6 +172,17 @@ def main():
                                      / (avg_ms * 1e-3) / HBM_PEAK, 4),
             "per_ray": {"pair_nodes": round(st.ext_nodes / max(1, st.extend_rays), 2),
                         "tri_tests": round(st.ext_tests / max(1, st.extend_rays), 2)}}
+    # SURVEY.md 8(d) whole-pipeline form: all logical bytes of the three stages over their summed time
+    b_ext = B_EXT_STATE * st.extend_rays + 2 * B_NODE * st.ext_nodes + B_TRI * st.ext_tests + B_HIT * st.ext_hits
+    b_any = B_ANY_STATE * (st.shadow_rays + st.vis_rays) + 2 * B_NODE * st.any_nodes + B_TRI * st.any_tests
+    b_shd = B_SHADE * st.shadow_rays + B_GEN * (st.extend_rays - st.shadow_rays)
+    t_pipe = (st.ms_extend + st.ms_shadow + st.ms_shade) * 1e-3
+    roof["pipeline_frac"] = round((b_ext + b_any + b_shd) / t_pipe / HBM_PEAK, 4)
+    hbm_meas = [pmc_traffic(p) for p in (("void mcpt_dev::k_trace_p<false>", "void mcpt_dev::k_trace<false>"),
+                                         ("void mcpt_dev::k_trace_p<true>", "void mcpt_dev::k_trace<true>"),
+                                         ("mcpt_dev::k_shade",))]
+    if all(h is not None for h in hbm_meas):  # measured HBM bytes per iteration (committed PMC summary)
+        roof["pipeline_hbm_frac_measured"] = round(sum(hbm_meas) * K / t_pipe / HBM_PEAK, 4)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(scene.arrays(), cam, W, H, args.cpu_spp, rc.max_depth)
