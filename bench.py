@@ -60,7 +60,7 @@ def pmc_traffic(kernel_prefix):
     try:
         d = json.load(open(files[-1]))
         for k, v in d.get("kernels", {}).items():
-            if any(k.startswith(p) for p in kernel_prefix):
+            if any(k.startswith(p) or k.startswith("void " + p) for p in kernel_prefix):
                 return v.get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -149,38 +149,36 @@ def main():
         return
 
     K = args.steps
-    # dominant kernel by summed HIP-event time over the timed region (same stream as the kernels)
-    kern = {"k_trace<closest>": st.ms_extend, "k_trace<any>": st.ms_shadow, "k_shade": st.ms_shade}
-    dom = max(kern, key=kern.get)
-    if dom == "k_trace<closest>":
-        byts = (B_EXT_STATE * st.extend_rays + 2 * B_NODE * st.ext_nodes + B_TRI * st.ext_tests + B_HIT * st.ext_hits)
-        prefix = ("void mcpt_dev::k_trace_p<false>", "void mcpt_dev::k_trace<false>")
-    elif dom == "k_trace<any>":
-        byts = (B_ANY_STATE * (st.shadow_rays + st.vis_rays) + 2 * B_NODE * st.any_nodes + B_TRI * st.any_tests)
-        prefix = ("void mcpt_dev::k_trace_p<true>", "void mcpt_dev::k_trace<true>")
-    else:
-        byts = B_SHADE * st.shadow_rays + B_GEN * (st.extend_rays - st.shadow_rays)
-        prefix = ("mcpt_dev::k_shade",)
-    per_launch = byts / K
-    avg_ms = kern[dom] / K
-    achieved = per_launch / (avg_ms * 1e-3)
-    traffic = pmc_traffic(prefix)
-    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
-            "algorithmic_bytes_per_launch": int(per_launch),
-            "state_only_frac": round(((B_EXT_STATE * st.extend_rays) / K if dom == "k_trace<closest>" else per_launch)
-                                     / (avg_ms * 1e-3) / HBM_PEAK, 4),
-            "per_ray": {"pair_nodes": round(st.ext_nodes / max(1, st.extend_rays), 2),
-                        "tri_tests": round(st.ext_tests / max(1, st.extend_rays), 2)}}
-    # SURVEY.md 8(d) whole-pipeline form: all logical bytes of the three stages over their summed time
+    # logical bytes per SURVEY.md 8(d): state bytes per ray/path-bounce + BVH bytes per visit
     b_ext = B_EXT_STATE * st.extend_rays + 2 * B_NODE * st.ext_nodes + B_TRI * st.ext_tests + B_HIT * st.ext_hits
     b_any = B_ANY_STATE * (st.shadow_rays + st.vis_rays) + 2 * B_NODE * st.any_nodes + B_TRI * st.any_tests
     b_shd = B_SHADE * st.shadow_rays + B_GEN * (st.extend_rays - st.shadow_rays)
+    # dominant kernel by summed HIP-event time over the timed region (same stream as the kernels);
+    # k_trace traces the extension (closest-hit) and any-hit rays of an iteration in one launch
+    kern = {"k_trace": st.ms_extend + st.ms_shadow, "k_shade": st.ms_shade}
+    names = {"k_trace": ("mcpt_dev::k_trace(",), "k_shade": ("mcpt_dev::k_shade(",)}
+    dom = max(kern, key=kern.get)
+    byts = b_ext + b_any if dom == "k_trace" else b_shd
+    state = (B_EXT_STATE * st.extend_rays + B_ANY_STATE * (st.shadow_rays + st.vis_rays)) if dom == "k_trace" else b_shd
+    per_launch = byts / K
+    avg_ms = kern[dom] / K
+    achieved = per_launch / (avg_ms * 1e-3)
+    traffic = pmc_traffic(names[dom])
+    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
+            "algorithmic_bytes_per_launch": int(per_launch),
+            "note": "logical bytes (SURVEY 8d) count every BVH node/triangle fetch; those are served from L2/MALL, "
+                    "so frac can exceed HBM reality - traffic is the measured HBM bytes per launch; the traversal "
+                    "is VALU-issue bound (DESIGN.md)",
+            "state_only_frac": round(state / K / (avg_ms * 1e-3) / HBM_PEAK, 4),
+            "per_ray": {"ext_pair_nodes": round(st.ext_nodes / max(1, st.extend_rays), 2),
+                        "ext_tri_tests": round(st.ext_tests / max(1, st.extend_rays), 2),
+                        "any_pair_nodes": round(st.any_nodes / max(1, st.shadow_rays + st.vis_rays), 2),
+                        "any_tri_tests": round(st.any_tests / max(1, st.shadow_rays + st.vis_rays), 2)}}
+    # whole-pipeline form: all logical bytes of both kernels over their summed time
     t_pipe = (st.ms_extend + st.ms_shadow + st.ms_shade) * 1e-3
     roof["pipeline_frac"] = round((b_ext + b_any + b_shd) / t_pipe / HBM_PEAK, 4)
-    hbm_meas = [pmc_traffic(p) for p in (("void mcpt_dev::k_trace_p<false>", "void mcpt_dev::k_trace<false>"),
-                                         ("void mcpt_dev::k_trace_p<true>", "void mcpt_dev::k_trace<true>"),
-                                         ("mcpt_dev::k_shade",))]
+    hbm_meas = [pmc_traffic(p) for p in names.values()]
     if all(h is not None for h in hbm_meas):  # measured HBM bytes per iteration (committed PMC summary)
         roof["pipeline_hbm_frac_measured"] = round(sum(hbm_meas) * K / t_pipe / HBM_PEAK, 4)
     cpu = None

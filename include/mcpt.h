@@ -95,7 +95,9 @@ typedef struct mcpt_stage_stats {
     uint64_t iterations;    /* wavefront iterations executed */
     uint64_t live_paths;    /* paths still in flight after the call */
     float ms_total;         /* device time of logic+generate+material+extend+shadow */
-    float ms_shade, ms_extend, ms_shadow;
+    float ms_shade;         /* k_shade: logic + generate + material (fused) */
+    float ms_extend;        /* k_trace: extension AND any-hit rays (one fused persistent launch) */
+    float ms_shadow;        /* 0: the any-hit rays are traced inside the k_trace launch */
     uint64_t ext_nodes;     /* closest-hit: child-pair nodes fetched (2 boxes each) */
     uint64_t ext_tests;     /* closest-hit: ray/triangle tests */
     uint64_t ext_hits;      /* closest-hit: rays that found a surface */

@@ -95,6 +95,13 @@ __device__ inline bool slab(float mnx, float mny, float mnz, float mxx, float mx
     t1 = (tzmax < b) ? tzmax : b;
     return !miss;
 }
+constexpr float kCullAbs = 1e-5f;
+constexpr float kCullRel = 1.0f / 256.0f;
+constexpr float K_INF_F = __builtin_huge_valf();
+constexpr int kEnd = -1;  // not a valid leaf: offset + count <= ntri < 2^24
+
+__device__ inline bool keep_box(float t0, float t1, float cut) { return !(t1 < -kCullAbs) && !(t0 > cut); }
+
 // Same decisions as slab() for rays whose inverse direction is finite in all
 // three components (no slab product can be NaN then): per axis the entry t is
 // <= the exit t (monotone rounding), so the reference's pairwise overlap tests
@@ -113,16 +120,10 @@ __device__ inline bool slab_fast(float mnx, float mny, float mnz, float mxx, flo
     t1 = __builtin_fminf(__builtin_fminf(tmax, tymax), tzmax);
     return t0 <= t1;
 }
-constexpr float kCullAbs = 1e-5f;
-constexpr float K_INF_F = __builtin_huge_valf();
-constexpr float kCullRel = 1.0f / 256.0f;
-constexpr int kEnd = -1;  // not a valid leaf: offset + count <= ntri < 2^24
 
-__device__ inline bool keep_box(float t0, float t1, float cut) { return !(t1 < -kCullAbs) && !(t0 > cut); }
-
-// The first test trace() makes: a NaN/zero direction or a ray that misses the
-// root box (after the cull) can hit nothing.  k_shade resolves such rays in place
-// instead of queueing them (same result; they are still counted as traced rays).
+// The first test the traversal makes: a NaN/zero direction or a ray that misses
+// the root box (after the cull) can hit nothing.  k_shade resolves such rays in
+// place instead of queueing them.
 __device__ inline bool ray_misses_scene(const DevScene& sc, V3 o, V3 d) {
     if (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f)) return true;
     const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
@@ -354,199 +355,72 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// BVH traversal.  Child-pair nodes (both child boxes in the parent, 64 B) with
-// the reference's slab arithmetic per box (Bounds3f.h:121-153); an extra
-// conservative cull rejects boxes entirely behind the origin or beyond the
-// current best t by more than 2^-8 relative (results unchanged unless a
-// triangle's Moller-Trumbore t error exceeds that margin).  Ties on t go to
-// the lower triangle index, so the traversal order is free (near-first here).
-// Stack: kLdsStack entries per lane in LDS ([entry][lane], conflict-free),
-// deeper entries in private scratch.
+// BVH traversal (BVH.cu:115-207 closest hit, Triangle.cu:157-205 any hit).
+// Child-pair nodes (both child boxes in the parent, 64 B) with the reference's
+// slab arithmetic per box (Bounds3f.h:121-153).  Culling beyond the reference
+// (which visits every box the infinite line crosses) is conservative: a box is
+// skipped only when it lies entirely behind the origin or starts more than
+// 2^-8 * t_best past the current best hit, so the result is unchanged unless a
+// triangle's Moller-Trumbore t error exceeded that margin.  Ties on t go to the
+// lower triangle index, so the visit order is free (near child first here).
+//
+// One persistent kernel traces both ray sets of an iteration: set 0 closest hit
+// (extension rays -> hit_tri), set 1 any hit (light and BRDF visibility rays ->
+// vis).  The grid is sized to the resident wave count; wave w of shard s owns
+// the shard's 64-ray chunks w, w + W, w + 2W, ... of set 0 followed by those of
+// set 1 (W waves per shard), read as one sequence, and whenever enough lanes
+// are idle at the top of the loop they take the next rays of that sequence.
+// Each loop trip a lane does one unit of work: one child-pair test, or (in the
+// wave-uniform triangle phase) one triangle of its parked leaf.  Reaching a
+// leaf parks it and traversal continues speculatively from the stack, so node
+// and triangle work are executed by full waves rather than interleaved per
+// lane.  No atomics: the split is static, balanced by the many chunks each
+// wave owns.  Stack: kLdsStack entries per lane in LDS ([entry][lane],
+// conflict-free), deeper entries in private scratch.
 // ---------------------------------------------------------------------------
-template <bool ANY>
-struct TraceResult { int tri; float t; };
-
-// Child-pair BVH traversal, while-while structure (Aila & Laine 2009): lanes
-// descend interior nodes together, then test leaves together.  Culling beyond
-// the reference (which visits every box the infinite line crosses) is
-// conservative: a box is skipped only when it lies entirely behind the origin or
-// starts more than 2^-8 * t_best past the current best hit.  Ties on t go to the
-// lower triangle index so the visit order is free (near child first here).
-template <bool ANY>
-__device__ inline TraceResult<ANY> trace(const DevScene& sc, V3 o, V3 d, int2 (*stk)[kTraceBlock], int lane_slot,
-                                         uint32_t& nodes, uint32_t& tests) {
-    TraceResult<ANY> res{-1, K_HUGE};
-    // NaN / zero direction: every triangle test fails (det NaN or 0), so the
-    // reference reports a miss / visible.
-    if (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f)) return res;
-    const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-    const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;
-    float best = K_HUGE;
-    float cut = best + best * kCullRel;
-#ifndef MCPT_X_NOSPILL
-    int2 spill[kMaxStack - kLdsStack];
-#endif
-    int sp = 0;
-    float t0, t1;
-    if (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1], sc.root_mx[2], o, inv, nx, ny,
-              nz, t0, t1) || !keep_box(t0, t1, cut))
-        return res;
-    int ref = sc.root_ref;
-    auto pop = [&]() -> int {
-        while (sp > 0) {
-            sp--;
-#ifndef MCPT_X_NOSPILL
-            int2 e = (sp < kLdsStack) ? stk[sp][lane_slot] : spill[sp - kLdsStack];
-#else
-            int2 e = stk[sp < kLdsStack ? sp : kLdsStack - 1][lane_slot];
-#endif
-            if (!ANY && __int_as_float(e.y) > cut) continue;
-            return e.x;
-        }
-        return kEnd;
-    };
-    while (ref != kEnd) {
-        // ---- interior nodes
-        while (ref >= 0) {
-            const float4* nd = sc.nodes + 4 * ref;
-            const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-            nodes++;
-            float a0, b0, a1, b1;
-            bool h0 = slab(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, o, inv, nx, ny, nz, a0, b0) && keep_box(a0, b0, cut);
-            bool h1 = slab(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, o, inv, nx, ny, nz, a1, b1) && keep_box(a1, b1, cut);
-            const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
-            if (h0 && h1) {
-                const bool first0 = !(a1 < a0);
-                const int2 e = make_int2(first0 ? c1 : c0, __float_as_int(first0 ? a1 : a0));
-#ifndef MCPT_X_NOSPILL
-                if (sp < kLdsStack) stk[sp][lane_slot] = e;
-                else spill[sp - kLdsStack] = e;
-#else
-                stk[sp < kLdsStack ? sp : kLdsStack - 1][lane_slot] = e;
-#endif
-                sp++;
-                ref = first0 ? c0 : c1;
-            } else if (h0 | h1) {
-                ref = h0 ? c0 : c1;
-            } else {
-                ref = pop();
-            }
-        }
-        if (ref == kEnd) break;
-        // ---- leaf
-        const int off = ref & 0xffffff;
-        const int cnt = ((ref >> 24) & 7) + 1;
-        for (int k = 0; k < cnt; k++) {
-            const int id = off + k;
-            const float4* tp = sc.tri + 3 * id;
-            const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-            tests++;
-            float t, u, v;
-            if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) && !(t < 0.f)) {
-                if (ANY) {
-                    if (t < K_HUGE) { res.tri = id; res.t = t; return res; }
-                } else if (t < best || (t == best && id < res.tri)) {
-                    best = t;
-                    res.tri = id;
-                    res.t = t;
-                    cut = best + best * kCullRel;
-                }
-            }
-        }
-        ref = pop();
-    }
-    return res;
-}
-
-
-// Write one traced ray's result: the visibility byte (any-hit) or the closest
-// triangle index (-1: none).  The hit record (position, normal, material) is
-// rebuilt from the index where it is consumed (hit_record()), which keeps this
-// divergent kernel's finish path short.
-template <bool ANY>
-__device__ inline void store_result(const TraceArgs& a, uint32_t rid, int tri) {
-    if (ANY) a.vis[rid] = (uint8_t)(tri < 0);
-    else a.hit_tri[rid] = tri;
-}
-
 // Traversal work counters: wave-reduce, one atomic per counter per wave.
-__device__ inline void wave_stats(const TraceArgs& a, int lane, uint32_t nodes, uint32_t tests, uint32_t hits) {
-    if (!a.stats) return;
+__device__ inline void wave_stats(uint32_t* stats, int lane, uint32_t nodes, uint32_t tests, uint32_t hits) {
+    if (!stats) return;
     for (int off = 32; off > 0; off >>= 1) {
         nodes += __shfl_xor(nodes, off);
         tests += __shfl_xor(tests, off);
         hits += __shfl_xor(hits, off);
     }
     if (lane == 0) {
-        uint32_t* st = a.stats + (blockIdx.x % kShards) * C_WORDS;
+        uint32_t* st = stats + (blockIdx.x % kShards) * C_WORDS;
         atomicAdd(st + 0, nodes);
         atomicAdd(st + 1, tests);
         atomicAdd(st + 2, hits);
     }
 }
 
-// Trace kernel: one wave per block, one ray per lane; the grid covers the largest
-// possible queue and lanes beyond the device-side count exit at once.  (A
-// persistent variant pulling 64 rays per atomic serialised on the single work
-// counter: ~32K dequeues per launch at <= ~88 per microsecond.)
-template <bool ANY>
-__global__ __launch_bounds__(kTraceBlock) void k_trace(TraceArgs a) {
-    __shared__ int2 stk[kLdsStack][kTraceBlock];
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave_base = blockIdx.x * kTraceBlock;
-    const int shard = (int)(wave_base / a.shard_cap);
-    const uint32_t k = wave_base - (uint32_t)shard * a.shard_cap + threadIdx.x;  // slot within the shard
-    const uint32_t n = a.count_ptr ? a.count_ptr[shard * C_WORDS] : a.count;
-    uint32_t nodes = 0, tests = 0, hits = 0;
-    if (k - threadIdx.x >= n) return;  // whole wave past the shard's count
-    const uint32_t i = shard * a.shard_cap + k;
-    if (k < n) {
-        const uint32_t rid = a.queue ? a.queue[i] : i;
-        const float4 o4 = a.ro[rid], d4 = a.rd[rid];
-        const V3 o = xyz(o4), d = xyz(d4);
-        const uint32_t n0 = nodes + tests;
-        TraceResult<ANY> tr = trace<ANY>(a.scene, o, d, stk, threadIdx.x, nodes, tests);
-        hits += tr.tri >= 0;
-        if (a.ray_steps) a.ray_steps[i] = nodes + tests - n0;
-        store_result<ANY>(a, rid, tr.tri);
-    }
-    wave_stats(a, lane, nodes, tests, hits);
-}
-
-// Persistent traversal with lane refill, one unit of work per lane per loop
-// trip ("if-if": a node pair test OR one triangle test, then a pop if needed).
-// The grid is sized to the resident wave count; wave w of shard s owns the
-// shard's 64-ray chunks w, w + W, w + 2W, ... (W waves per shard), read as one
-// sequence, and whenever lanes are idle at the top of the loop they take the
-// next rays of that sequence.  With one ray per lane and while-while loops the
-// lanes sat ~83% idle (VALUUtilization 17%, profiles/pmc_r01): every descent ran
-// as long as the wave's longest one and every wave as long as its slowest ray.
-// No atomics: the split is static, balanced by the many chunks each wave owns.
-// A leaf is consumed one triangle per trip by stepping its encoding in place
-// (offset + 1, count - 1).  Per ray the visit order, culling and result are
-// exactly those of trace<ANY>().
 #ifdef MCPT_TRACE_WPE
 #define MCPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_TRACE_WPE, MCPT_TRACE_WPE)))
 #else
 #define MCPT_TRACE_ATTR
 #endif
-template <bool ANY>
-__global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace_p(TraceArgs a) {
+__global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs a) {
     __shared__ int2 stk[kLdsStack][kTraceBlock];
     const int lane = threadIdx.x;
     const uint32_t nsh = (uint32_t)a.nshards;
     const uint32_t wps = gridDim.x / nsh;  // waves per shard (host: gridDim.x % nsh == 0)
     const uint32_t shard = blockIdx.x % nsh, w_in = blockIdx.x / nsh;
-    const uint32_t n = a.count_ptr ? a.count_ptr[shard * C_WORDS] : a.count;
-    const uint32_t nchunks = (n + 63) >> 6;
-    if (w_in >= nchunks) return;
-    const uint32_t L = ((nchunks - w_in + wps - 1) / wps) << 6;  // this wave's sequence length
-    const uint32_t qbase = shard * a.shard_cap;
+    uint32_t n[2], L[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const TraceSet& ts = a.set[k];
+        n[k] = ts.count_ptr ? ts.count_ptr[shard * C_WORDS] : ts.count;
+        const uint32_t nchunks = (n[k] + 63) >> 6;
+        L[k] = w_in < nchunks ? ((nchunks - w_in + wps - 1) / wps) << 6 : 0u;  // this wave's share of set k
+    }
+    const uint32_t Ltot = L[0] + L[1];
+    if (Ltot == 0) return;
     const DevScene& sc = a.scene;
 
-    uint32_t nodes = 0, tests = 0, hits = 0;
+    uint32_t nodes[2] = {0, 0}, tests[2] = {0, 0}, hits[2] = {0, 0};
     uint32_t next = 0;  // wave-uniform position in the sequence
     bool act = false;
+    int kind = 0;  // 0 closest, 1 any
     uint32_t rid = 0, qi = 0, step0 = 0;
     V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
     int nx = 0, ny = 0, nz = 0, ref = kEnd, leaf = kEnd, sp = 0, tri = -1;
@@ -555,6 +429,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace_p(TraceAr
 #ifndef MCPT_X_NOSPILL
     int2 spill[kMaxStack - kLdsStack];
 #endif
+    // Pop the next entry still in front of the current cut (any-hit rays keep
+    // cut = K_HUGE * (1 + 2^-8), so for them every entry is taken).
     auto pop = [&]() -> int {
         while (sp > 0) {
             sp--;
@@ -569,34 +445,40 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace_p(TraceAr
 #else
             e = stk[sp < kLdsStack ? sp : kLdsStack - 1][lane];
 #endif
-            if (!ANY && __int_as_float(e.y) > cut) continue;
+            if (__int_as_float(e.y) > cut) continue;
             return e.x;
         }
         return kEnd;
     };
     auto finish = [&]() {
-        hits += tri >= 0;
-        if (a.ray_steps) a.ray_steps[qi] = nodes + tests - step0;
-        store_result<ANY>(a, rid, tri);
+        hits[kind] += tri >= 0;
+        uint32_t* rs = a.set[kind].ray_steps;
+        if (rs) rs[qi] = nodes[kind] + tests[kind] - step0;
+        if (kind) a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
+        else a.hit_tri[rid] = tri;                  // hit record rebuilt by the consumer (hit_record())
         act = false;
     };
     for (;;) {
         // ---- refill idle lanes from the wave's sequence
         const uint64_t idle = __ballot(!act);
         const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (next < L && (nidle >= a.refill_min || nidle == 64u)) {
+        if (next < Ltot && (nidle >= a.refill_min || nidle == 64u)) {
             if (!act) {
                 const uint32_t q = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                const uint32_t s = next + q;
+                uint32_t s = next + q;
+                kind = s >= L[0];
+                const uint32_t nk = kind ? n[1] : n[0];
+                if (kind) s -= L[0];
                 const uint32_t k = (w_in + (s >> 6) * wps) * 64u + (s & 63u);
-                if (s < L && k < n) {
-                    qi = qbase + k;
-                    rid = a.queue ? a.queue[qi] : qi;
-                    const float4 o4 = a.ro[rid], d4 = a.rd[rid];
+                if (s < (kind ? L[1] : L[0]) && k < nk) {
+                    const TraceSet& ts = a.set[kind];
+                    qi = shard * ts.shard_cap + k;
+                    rid = ts.queue ? ts.queue[qi] : qi;
+                    const float4 o4 = ts.ro[rid], d4 = ts.rd[rid];
                     o = xyz(o4);
                     d = xyz(d4);
-                    step0 = nodes + tests;
+                    step0 = nodes[kind] + tests[kind];
                     tri = -1;
                     best = K_HUGE;
                     cut = best + best * kCullRel;
@@ -626,7 +508,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace_p(TraceAr
             next += nidle;
         }
         if (__ballot(act) == 0) {
-            if (next >= L) break;
+            if (next >= Ltot) break;
             continue;
         }
         // ---- node phase: one child-pair test per lane holding an interior node
@@ -635,7 +517,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace_p(TraceAr
             if (ref >= 0) {
                 const float4* nd = sc.nodes + 4 * ref;
                 const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-                nodes++;
+                nodes[kind]++;
                 float a0, b0, a1, b1;
                 bool h0, h1;
                 if (fin) {
@@ -681,20 +563,20 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace_p(TraceAr
                 const int id = leaf & 0xffffff;
                 const float4* tp = sc.tri + 3 * id;
                 const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-                tests++;
+                tests[kind]++;
                 float t, u, v;
                 bool done = false;
                 if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) &&
                     !(t < 0.f)) {
-                    if (ANY) {
-                        if (t < K_HUGE) { tri = id; done = true; }
+                    if (kind) {
+                        if (t < K_HUGE) { tri = id; done = true; }  // occluded (tmax 1e32)
                     } else if (t < best || (t == best && id < tri)) {
                         best = t;
                         tri = id;
                         cut = best + best * kCullRel;
                     }
                 }
-                if (done) {  // any-hit: occluded, drop the rest of the traversal
+                if (done) {  // any hit: drop the rest of the traversal
                     leaf = kEnd;
                     ref = kEnd;
                 } else {
@@ -704,7 +586,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace_p(TraceAr
         }
         if (act && ref == kEnd && leaf == kEnd) finish();
     }
-    wave_stats(a, lane, nodes, tests, hits);
+    wave_stats(a.set[0].stats, lane, nodes[0], tests[0], hits[0]);
+    wave_stats(a.set[1].stats, lane, nodes[1], tests[1], hits[1]);
 }
 
 __global__ void k_hit_record(HitRecordArgs a) {  // stage_run(EXTEND) outputs
@@ -802,62 +685,36 @@ __global__ void k_pack(PackArgs a) {  // tile-set pixels -> packed 16 B/px (for 
 void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s) {
     hipLaunchKernelGGL(k_shade, dim3(nblocks), dim3(kBlock), 0, s, a);
 }
-// Trace kernel choice: persistent lane-refill waves (default) or one ray per lane
-// (MCPT_TRACE_KERNEL=ray, kept for A/B measurement).  MCPT_TRACE_WAVES overrides
-// the resident waves per CU the persistent grid is sized for.
-static int trace_mode() {
-    static int mode = [] {
-        const char* e = getenv("MCPT_TRACE_KERNEL");
-        return (e && !strcmp(e, "ray")) ? 0 : 1;
-    }();
-    return mode;
-}
-static uint32_t persistent_waves(bool any) {
-    static uint32_t w[2] = {0, 0};
-    if (!w[any]) {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (any) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_p<true>, kTraceBlock, 0);
-        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_p<false>, kTraceBlock, 0);
-        if (const char* e = getenv("MCPT_TRACE_WAVES")) per_cu = atoi(e);
-        if (cus <= 0) cus = 256;
-        if (per_cu <= 0) per_cu = 16;
-        w[any] = (uint32_t)(cus * per_cu);
-    }
-    return w[any];
-}
+// Persistent grid: resident waves per CU from the occupancy calculator
+// (MCPT_TRACE_WAVES overrides), rounded to a multiple of the shard count.
 static uint32_t env_u32(const char* name, int def, int lo, int hi) {
     const char* e = getenv(name);
     int v = e ? atoi(e) : def;
     return (uint32_t)std::min(hi, std::max(lo, v));
 }
-static uint32_t refill_min() {
-    static uint32_t m = [] {
-        const char* e = getenv("MCPT_REFILL_MIN");
-        int v = e ? atoi(e) : 16;
-        return (uint32_t)std::min(64, std::max(1, v));
+static uint32_t persistent_waves() {
+    static uint32_t w = [] {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace, kTraceBlock, 0);
+        if (const char* e = getenv("MCPT_TRACE_WAVES")) per_cu = atoi(e);
+        if (cus <= 0) cus = 256;
+        if (per_cu <= 0) per_cu = 16;
+        return (uint32_t)(cus * per_cu);
     }();
-    return m;
+    return w;
 }
-void launch_trace(const TraceArgs& args, bool any, hipStream_t s) {
-    if (args.nshards <= 0 || args.shard_cap == 0) return;
+void launch_trace(const TraceArgs& args, hipStream_t s) {
+    if (args.nshards <= 0) return;
     TraceArgs a = args;
-    a.refill_min = refill_min();
+    static const uint32_t refill_min = env_u32("MCPT_REFILL_MIN", 16, 1, 64);
     static const uint32_t tri_min = env_u32("MCPT_TRI_MIN", 16, 0, 64);
+    a.refill_min = refill_min;
     a.tri_min = tri_min;
-    if (trace_mode() == 1) {
-        const uint32_t nsh = (uint32_t)a.nshards;
-        const uint32_t wps = std::max<uint32_t>(1, persistent_waves(any) / nsh);
-        const uint32_t nblocks = wps * nsh;
-        if (any) hipLaunchKernelGGL(k_trace_p<true>, dim3(nblocks), dim3(kTraceBlock), 0, s, a);
-        else hipLaunchKernelGGL(k_trace_p<false>, dim3(nblocks), dim3(kTraceBlock), 0, s, a);
-        return;
-    }
-    const uint32_t nblocks = (uint32_t)(((uint64_t)a.nshards * a.shard_cap + kTraceBlock - 1) / kTraceBlock);
-    if (nblocks == 0) return;
-    if (any) hipLaunchKernelGGL(k_trace<true>, dim3(nblocks), dim3(kTraceBlock), 0, s, a);
-    else hipLaunchKernelGGL(k_trace<false>, dim3(nblocks), dim3(kTraceBlock), 0, s, a);
+    const uint32_t nsh = (uint32_t)a.nshards;
+    const uint32_t wps = std::max<uint32_t>(1, persistent_waves() / nsh);
+    hipLaunchKernelGGL(k_trace, dim3(wps * nsh), dim3(kTraceBlock), 0, s, a);
 }
 void launch_clear(const ClearArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_clear, dim3((a.n + 255) / 256), dim3(256), 0, s, a);

@@ -86,20 +86,25 @@ struct ShadeArgs {
     CounterBlock* cnt;
 };
 
-struct TraceArgs {
-    DevScene scene;
+// One ray set of a trace launch: rays ro/rd[rid] for queue entries
+// queue[s * shard_cap + k], k < count of shard s.
+struct TraceSet {
     const float4 *ro, *rd;
     const uint32_t* queue;      // nullptr => identity
     const uint32_t* count_ptr;  // device count of shard s at count_ptr[s * C_WORDS] (nullptr => count)
     uint32_t count;
-    uint32_t shard_cap;         // queue entries per shard (queue[s * shard_cap + k])
+    uint32_t shard_cap;         // queue entries per shard
+    uint32_t* stats;            // optional: shard s counters at stats[s * C_WORDS + 0..2] (nodes, tests, hits)
+    uint32_t* ray_steps;        // optional per-queue-entry node fetches + triangle tests (diagnostics)
+};
+struct TraceArgs {
+    DevScene scene;
+    TraceSet set[2];            // [0] closest hit -> hit_tri, [1] any hit -> vis
     int nshards;
     int32_t* hit_tri;           // closest-hit output: triangle index or -1
-    uint8_t* vis;               // any-hit output
-    uint32_t* stats;            // optional: shard s counters at stats[s * C_WORDS + 0..2]
-    uint32_t* ray_steps;        // optional per-ray node fetches + triangle tests (diagnostics)
-    uint32_t refill_min;        // persistent kernel: refill when at least this many lanes are idle (set by launch_trace)
-    uint32_t tri_min;           // persistent kernel: run the triangle phase when this many lanes hold a leaf
+    uint8_t* vis;               // any-hit output: 1 = unoccluded
+    uint32_t refill_min;        // refill when at least this many lanes are idle (set by launch_trace)
+    uint32_t tri_min;           // run the triangle phase when this many lanes hold a leaf (set by launch_trace)
 };
 
 struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; uint32_t n; };
@@ -108,7 +113,7 @@ struct TonemapArgs { const float4* Ld; const uint32_t* samples; uchar4* out; flo
 struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* out; };
 
 void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s);
-void launch_trace(const TraceArgs& a, bool any, hipStream_t s);
+void launch_trace(const TraceArgs& a, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);

@@ -413,30 +413,28 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 0), c->stream));
     if (sa.ntiles > 0) launch_shade(sa, sa.ntiles * bpt, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 1), c->stream));
+    // extension (closest hit) and any-hit rays in one persistent launch
     TraceArgs ta{};
     ta.scene = c->scene;
-    ta.ro = c->p.ray_o;
-    ta.rd = c->p.ray_d;
-    ta.queue = c->ext_q;
-    ta.count_ptr = &c->cnt->shard[0][C_EXT];
-    ta.shard_cap = c->ext_cap;
     ta.nshards = kShards;
+    TraceSet& e = ta.set[0];
+    e.ro = c->p.ray_o;
+    e.rd = c->p.ray_d;
+    e.queue = c->ext_q;
+    e.count_ptr = &c->cnt->shard[0][C_EXT];
+    e.shard_cap = c->ext_cap;
+    e.stats = &c->cnt->shard[0][C_STATS];
+    TraceSet& v = ta.set[1];
+    v.ro = c->p.sray_o;
+    v.rd = c->p.sray_d;
+    v.queue = c->any_q;
+    v.count_ptr = &c->cnt->shard[0][C_ANY];
+    v.shard_cap = c->any_cap;
+    v.stats = &c->cnt->shard[0][C_STATS + 3];
     ta.hit_tri = c->p.hit_tri;
-    ta.stats = &c->cnt->shard[0][C_STATS];
-    launch_trace(ta, false, c->stream);
+    ta.vis = c->p.vis;
+    launch_trace(ta, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
-    TraceArgs tb{};
-    tb.scene = c->scene;
-    tb.ro = c->p.sray_o;
-    tb.rd = c->p.sray_d;
-    tb.queue = c->any_q;
-    tb.count_ptr = &c->cnt->shard[0][C_ANY];
-    tb.shard_cap = c->any_cap;
-    tb.nshards = kShards;
-    tb.vis = c->p.vis;
-    tb.stats = &c->cnt->shard[0][C_STATS + 3];
-    launch_trace(tb, true, c->stream);
-    if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 3), c->stream));
     launch_accumulate(c->cnt, c->stream);
     HIPCHK(c, hipGetLastError());
     return MCPT_OK;
@@ -452,7 +450,7 @@ static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st) {
     for (uint32_t i = 0; i < n; i++) {
         // events for at most the first 4096 iterations of a call
         bool timing = i < 4096;
-        if ((rc = enqueue_iteration(c, (size_t)4 * i, timing))) return rc;
+        if ((rc = enqueue_iteration(c, (size_t)3 * i, timing))) return rc;
     }
     HIPCHK(c, hipMemcpyAsync(c->cnt_host, c->cnt, sizeof(CounterBlock), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -472,13 +470,11 @@ static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st) {
         st->any_hits = after.tot_stats[5] - before.tot_stats[5];
         uint32_t tn = std::min<uint32_t>(n, 4096);
         for (uint32_t i = 0; i < tn; i++) {
-            float a = 0, b = 0, d = 0;
-            HIPCHK(c, hipEventElapsedTime(&a, c->events[4 * i + 0], c->events[4 * i + 1]));
-            HIPCHK(c, hipEventElapsedTime(&b, c->events[4 * i + 1], c->events[4 * i + 2]));
-            HIPCHK(c, hipEventElapsedTime(&d, c->events[4 * i + 2], c->events[4 * i + 3]));
+            float a = 0, b = 0;
+            HIPCHK(c, hipEventElapsedTime(&a, c->events[3 * i + 0], c->events[3 * i + 1]));
+            HIPCHK(c, hipEventElapsedTime(&b, c->events[3 * i + 1], c->events[3 * i + 2]));
             st->ms_shade += a;
-            st->ms_extend += b;
-            st->ms_shadow += d;
+            st->ms_extend += b;  // extension + any-hit rays: one k_trace launch (ms_shadow stays 0)
         }
         st->ms_total = st->ms_shade + st->ms_extend + st->ms_shadow;
     }
@@ -557,11 +553,12 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
         return rc;
     TraceArgs ta{};
     ta.scene = c->scene;
-    ta.ro = dro;
-    ta.rd = drd;
-    ta.count = n;
-    ta.shard_cap = (n + kTraceBlock - 1) / kTraceBlock * kTraceBlock;
     ta.nshards = 1;
+    TraceSet& ts = ta.set[stage == MCPT_STAGE_SHADOW ? 1 : 0];
+    ts.ro = dro;
+    ts.rd = drd;
+    ts.count = n;
+    ts.shard_cap = n;
     if (stage == MCPT_STAGE_EXTEND) {
         if ((rc = dalloc(c, c->tmp_bufs, &hp, n)) || (rc = dalloc(c, c->tmp_bufs, &hn, n)) || (rc = dalloc(c, c->tmp_bufs, &ht, n)))
             return rc;
@@ -573,10 +570,10 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
     uint32_t* steps = nullptr;
     if (out->steps) {
         if ((rc = dalloc(c, c->tmp_bufs, &steps, n))) return rc;
-        ta.ray_steps = steps;
+        ts.ray_steps = steps;
     }
     HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
-    launch_trace(ta, stage == MCPT_STAGE_SHADOW, c->stream);
+    launch_trace(ta, c->stream);
     HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
     if (stage == MCPT_STAGE_EXTEND) {
         HitRecordArgs ha{c->scene, dro, drd, ht, hp, hn, n};

@@ -22,7 +22,7 @@ for i in range(3):
     va = pt.trace_any(ro, rd); ta.append(pt.last_stage_ms)
 h += "/" + hashlib.md5(va[idx].tobytes()).hexdigest()[:6]
 st = pt.iterate(20)
-print("%%-24s [%%s] closest(stage) %%.3f any(stage) %%.3f | pipeline shade %%.3f ext %%.3f shadow %%.3f ms/iter" %% (
+print("%%-24s [%%s] closest(stage) %%.3f any(stage) %%.3f | pipeline shade %%.3f trace %%.3f (+%%.3f) ms/iter" %% (
     os.environ.get("VARIANT"), h, min(ts), min(ta), st.ms_shade/20, st.ms_extend/20, st.ms_shadow/20), flush=True)
 ''' % REPO
 # variant: "base", a libmcpt_<name>.so suffix, or env overrides on base: "K=V,K2=V2"
