@@ -205,6 +205,8 @@ def main():
             "tiles": "256x256, rank = (tx+ty) mod N",
             "step": "one wavefront iteration (shade+extend+shadow) over the rank's pixels, steady state",
             "rays_per_step": int(rays_all / K),
+            "rays_per_step_rank0": {"extend": round(st.extend_rays / K), "shadow": round(st.shadow_rays / K),
+                                    "visibility": round(st.vis_rays / K)},
             "parallelism": f"tiles{world}",
             "device": pt.device_name,
         },

@@ -153,14 +153,126 @@ __device__ inline void hit_record(const DevScene& sc, V3 o, V3 d, int tri, V3& p
 }
 
 // ---------------------------------------------------------------------------
-// k_shade: one thread per pixel of the tile set.
+// k_shade: one wavefront iteration's shading for one block of 256 pixels.
+//   phase 1, one thread per pixel: wf_logic (MIS combine, throughput update,
+//     Russian roulette, termination, sample count) and wf_generate for pixels
+//     whose path ended (wavefront_kernels.cu:90-251);
+//   phase 2: the block's continuing paths are compacted through LDS (ballot +
+//     mbcnt + per-wave prefix) onto the first threads of the block, which run
+//     the light choice and wf_mat_mix (:207-215, 295-375).  Without the
+//     compaction the material code -- most of the kernel's instructions --
+//     ran with the terminating / regenerating lanes of each wave masked off.
+//   phase 3: one block-wide push of the extension rays (generated + continued)
+//     and the any-hit rays (light sample + BRDF visibility).
+// Per path the arithmetic is the reference's, so which thread evaluates a path
+// does not change any result.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
+struct MatOut {
+    bool want_ext, want_l, want_b, trivial_ext, vis_ray;
+    uint32_t trivial_any;
+};
+
+// Light choice + wf_mat_mix for the continuing path pid (vertex len, sample
+// `samples`, throughput `beta_store` after the logic update).
+__device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t samples, uint32_t len, V3 beta_store) {
+    const DevScene& sc = a.scene;
+    MatOut mo{false, false, false, false, false, 0u};
+    const Rng r{rng_key(a.seed, pid, samples), len};
+    const V3 ro = xyz(a.p.ray_o[pid]), rdir = xyz(a.p.ray_d[pid]);
+    V3 pos, n;
+    int mat;
+    float t_hit;
+    hit_record(sc, ro, rdir, a.p.hit_tri[pid], pos, n, mat, t_hit);
+    const V3 wo = -rdir;
+    int l_id = (int)(r(SL_LIGHT) * (float)(sc.nlights - 0) + (float)0);
+    const int light_id = (l_id == sc.nlights) ? 0 : l_id;
+    V3 ldir;
+    if (light_id == 0) ldir = env_dir(sc.env, r);
+    else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
+    const V3 so_l = pos + n * 0.01f, sd_l = ldir;
+    const Mat m = load_mat(sc.mats + 8 * mat);
+    const bool delta = light_id > 0;
+    V3 f_l = brdf_f(m, n, ldir, wo);
+    V3 Li_l = light_L(sc, light_id, ldir);
+    float pdfl_x = light_pdf(sc, light_id, ldir);
+    float pdfb_y = !delta ? brdf_pdf(m, n, ldir, wo) : 1.f;
+    float wL = power_heuristic(pdfl_x, pdfb_y);
+    V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
+    uint32_t nf = 0;
+    if (wL > 0.f && pdfl_x > 0.f) nf |= F_CONDL;
+    V3 cB = v3(0.f, 0.f, 0.f);
+    V3 so_b = v3(0, 0, 0), sd_b = v3(0, 0, 0);
+    if (!delta) {
+        V3 wi_b = (r(SL_MAT_LOBE) < 0.5f) ? spec_get_wi(m, n, wo, r, SL_MAT_E0) : diff_get_wi(n, r, SL_MAT_E0);
+        so_b = pos + wi_b * 0.001f;
+        sd_b = wi_b;
+        V3 f_b = brdf_f(m, n, wi_b, wo);
+        V3 Li_b = light_L(sc, light_id, wi_b);
+        float pdfb_x = brdf_pdf(m, n, wi_b, wo);
+        float pdfl_y = light_pdf(sc, light_id, wi_b);
+        float wB = power_heuristic(pdfb_x, pdfl_y);
+        cB = ((f_b * Li_b) * wB) / pdfb_x;
+        if (wB > 0.f && pdfb_x > 0.f) nf |= F_CONDB;
+        nf |= F_HASVIS;
+        mo.want_b = true;
+        mo.vis_ray = true;
+    }
+    V3 wi_s = (r(SL_CONT_LOBE) < 0.5f) ? spec_get_wi(m, n, wo, r, SL_CONT_E0) : diff_get_wi(n, r, SL_CONT_E0);
+    float pdf_s = brdf_pdf(m, n, wi_s, wo);
+    V3 f_s = brdf_f(m, n, wi_s, wo);
+    if ((f_s.x == 0.f && f_s.y == 0.f && f_s.z == 0.f) || pdf_s == 0.f) nf |= F_FZERO;
+    V3 rr = f_s / pdf_s;
+    const V3 new_o = pos + n * 0.001f;  // :358
+    const V3 new_d = wi_s;
+    a.p.beta[pid] = f4(beta_store, rr.x);
+    a.p.nee0[pid] = f4(cL, rr.y);
+    a.p.nee1[pid] = f4(cB, rr.z);
+    a.p.flags[pid] = nf | ((len + 1) << F_LEN_SHIFT);  // extend increments len (:270)
+    a.p.ray_o[pid] = f4(new_o, 0.f);
+    a.p.ray_d[pid] = f4(new_d, 0.f);
+    mo.want_ext = true;
+    if (ray_misses_scene(sc, new_o, new_d)) {  // resolved here: isect stays "not found"
+        a.p.hit_tri[pid] = -1;
+        mo.want_ext = false;
+        mo.trivial_ext = true;
+    }
+    if (ray_misses_scene(sc, so_l, sd_l)) {
+        a.p.vis[2 * pid] = 1;
+        mo.trivial_any++;
+    } else {
+        a.p.sray_o[2 * pid] = f4(so_l, 0.f);
+        a.p.sray_d[2 * pid] = f4(sd_l, 0.f);
+        mo.want_l = true;
+    }
+    if (mo.want_b) {
+        if (ray_misses_scene(sc, so_b, sd_b)) {
+            a.p.vis[2 * pid + 1] = 1;
+            mo.want_b = false;
+            mo.trivial_any++;
+        } else {
+            a.p.sray_o[2 * pid + 1] = f4(so_b, 0.f);
+            a.p.sray_d[2 * pid + 1] = f4(sd_b, 0.f);
+        }
+    }
+    return mo;
+}
+
+#ifdef MCPT_SHADE_WPE
+#define MCPT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_SHADE_WPE, MCPT_SHADE_WPE)))
+#else
+#define MCPT_SHADE_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
+    __shared__ uint32_t s_pid[kBlock];      // pid | len << 24 of the block's continuing paths
+    __shared__ uint32_t s_samples[kBlock];
+    __shared__ float s_beta[3][kBlock];
+    __shared__ uint32_t s_wave_cnt[kBlock / 64];
     const DevScene& sc = a.scene;
     const int tile_px = a.tile_w * a.tile_h;
     const int bpt = (tile_px + kBlock - 1) / kBlock;
     const int tile = blockIdx.x / bpt;
     const int li = (blockIdx.x - tile * bpt) * kBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     bool valid = tile < a.ntiles && li < tile_px;
     uint32_t pid = 0;
     int x = 0, y = 0;
@@ -171,31 +283,25 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
         valid = x < a.W - 1 && y < a.H - 1;  // last column and row never rendered (wavefront_kernels.cu:110)
         pid = (uint32_t)y * (uint32_t)a.W + (uint32_t)x;
     }
-    bool want_ext = false, want_l = false, want_b = false;
-    bool new_path = false, trivial_ext = false;
-    uint32_t trivial_any = 0;
-    bool fl_vis_ray = false;
-    uint32_t nflags = 0, fl = F_DEAD;
-    V3 new_o = v3(0, 0, 0), new_d = v3(0, 0, 0);
-    V3 so_l = v3(0, 0, 0), sd_l = v3(0, 0, 0), so_b = v3(0, 0, 0), sd_b = v3(0, 0, 0);
+    // ---- phase 1: logic + generate (one thread per pixel)
+    bool gen_ext = false, gen_trivial = false, cont = false;
+    uint32_t cont_len = 0, cont_samples = 0;
+    V3 beta_store = v3(0.f, 0.f, 0.f);
     if (valid) {
-        fl = a.p.flags[pid];
-        nflags = fl;
+        const uint32_t fl = a.p.flags[pid];
         uint32_t samples = a.p.samples[pid];
         bool dead = (fl & F_DEAD) != 0;
         const uint32_t spp = (uint32_t)a.spp;
         if (!dead && samples < spp) {  // wavefront_kernels.cu:124
             const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
             const Rng r{rng_key(a.seed, pid, samples), len};
-            const int htri = a.p.hit_tri[pid];
-            const bool found = htri >= 0;
+            const bool found = a.p.hit_tri[pid] >= 0;
             float4 b4 = a.p.beta[pid];
             const V3 B = xyz(b4);
             float4 ld4 = a.p.Ld[pid];
             V3 film = xyz(ld4);
             bool terminate = false;
-            V3 beta_store = B;
-            V3 wo = v3(0, 0, 0);
+            beta_store = B;
             if (len == 1) {  // :129-140
                 if (found) {
                     film = film + v3(0.f, 0.f, 0.f) * B;
@@ -232,125 +338,86 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
                 dead = true;
                 samples++;
                 a.p.samples[pid] = samples;
-                nflags = F_DEAD;
             } else {
-                // ---- continue: light choice (:207-215) fused with wf_mat_mix (:295-375)
-                const V3 ro = xyz(a.p.ray_o[pid]), rdir = xyz(a.p.ray_d[pid]);
-                V3 pos, n;
-                int mat;
-                float t_hit;
-                hit_record(sc, ro, rdir, htri, pos, n, mat, t_hit);
-                wo = -rdir;
-                int l_id = (int)(r(SL_LIGHT) * (float)(sc.nlights - 0) + (float)0);
-                const int light_id = (l_id == sc.nlights) ? 0 : l_id;
-                V3 ldir;
-                if (light_id == 0) ldir = env_dir(sc.env, r);
-                else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
-                so_l = pos + n * 0.01f;
-                sd_l = ldir;
-                const Mat m = load_mat(sc.mats + 8 * mat);
-                const bool delta = light_id > 0;
-                V3 f_l = brdf_f(m, n, ldir, wo);
-                V3 Li_l = light_L(sc, light_id, ldir);
-                float pdfl_x = light_pdf(sc, light_id, ldir);
-                float pdfb_y = !delta ? brdf_pdf(m, n, ldir, wo) : 1.f;
-                float wL = power_heuristic(pdfl_x, pdfb_y);
-                V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
-                uint32_t nf = 0;
-                if (wL > 0.f && pdfl_x > 0.f) nf |= F_CONDL;
-                V3 cB = v3(0.f, 0.f, 0.f);
-                if (!delta) {
-                    V3 wi_b = (r(SL_MAT_LOBE) < 0.5f) ? spec_get_wi(m, n, wo, r, SL_MAT_E0) : diff_get_wi(n, r, SL_MAT_E0);
-                    so_b = pos + wi_b * 0.001f;
-                    sd_b = wi_b;
-                    V3 f_b = brdf_f(m, n, wi_b, wo);
-                    V3 Li_b = light_L(sc, light_id, wi_b);
-                    float pdfb_x = brdf_pdf(m, n, wi_b, wo);
-                    float pdfl_y = light_pdf(sc, light_id, wi_b);
-                    float wB = power_heuristic(pdfb_x, pdfl_y);
-                    cB = ((f_b * Li_b) * wB) / pdfb_x;
-                    if (wB > 0.f && pdfb_x > 0.f) nf |= F_CONDB;
-                    nf |= F_HASVIS;
-                    want_b = true;
-                    fl_vis_ray = true;
-                }
-                V3 wi_s = (r(SL_CONT_LOBE) < 0.5f) ? spec_get_wi(m, n, wo, r, SL_CONT_E0) : diff_get_wi(n, r, SL_CONT_E0);
-                float pdf_s = brdf_pdf(m, n, wi_s, wo);
-                V3 f_s = brdf_f(m, n, wi_s, wo);
-                if ((f_s.x == 0.f && f_s.y == 0.f && f_s.z == 0.f) || pdf_s == 0.f) nf |= F_FZERO;
-                V3 rr = f_s / pdf_s;
-                new_o = pos + n * 0.001f;  // :358
-                new_d = wi_s;
-                a.p.beta[pid] = f4(beta_store, rr.x);
-                a.p.nee0[pid] = f4(cL, rr.y);
-                a.p.nee1[pid] = f4(cB, rr.z);
-                nflags = nf | ((len + 1) << F_LEN_SHIFT);  // extend increments len (:270)
-                want_ext = true;
-                want_l = true;
+                cont = true;
+                cont_len = len;
+                cont_samples = samples;
             }
         }
+        uint32_t nflags = fl;
+        if (dead) nflags = F_DEAD;
         if (dead && samples < spp) {  // :219-222 + wf_generate (:225-251)
             const Rng r0{rng_key(a.seed, pid, samples), 0u};
+            V3 new_o, new_d;
             gen_ray(a.cam, a.W, a.H, x, y, r0, new_o, new_d);
             a.p.beta[pid] = make_float4(1.f, 1.f, 1.f, 0.f);
             nflags = 1u << F_LEN_SHIFT;
-            want_ext = true;
-            new_path = true;
-        }
-        if (want_ext || nflags != fl) a.p.flags[pid] = nflags;
-        if (want_ext) {
             a.p.ray_o[pid] = f4(new_o, 0.f);
             a.p.ray_d[pid] = f4(new_d, 0.f);
+            gen_ext = true;
             if (ray_misses_scene(sc, new_o, new_d)) {  // resolved here: isect stays "not found"
                 a.p.hit_tri[pid] = -1;
-                want_ext = false;
-                trivial_ext = true;
+                gen_ext = false;
+                gen_trivial = true;
             }
         }
-        if (want_l) {
-            if (ray_misses_scene(sc, so_l, sd_l)) {
-                a.p.vis[2 * pid] = 1;
-                want_l = false;
-                trivial_any++;
-            } else {
-                a.p.sray_o[2 * pid] = f4(so_l, 0.f);
-                a.p.sray_d[2 * pid] = f4(sd_l, 0.f);
-            }
-        }
-        if (want_b) {
-            if (ray_misses_scene(sc, so_b, sd_b)) {
-                a.p.vis[2 * pid + 1] = 1;
-                want_b = false;
-                trivial_any++;
-            } else {
-                a.p.sray_o[2 * pid + 1] = f4(so_b, 0.f);
-                a.p.sray_d[2 * pid + 1] = f4(sd_b, 0.f);
-            }
-        }
+        if (!cont && nflags != fl) a.p.flags[pid] = nflags;  // continuing paths: written by material()
     }
-    (void)new_path;
-    // ---- compaction: ext queue and any-hit queue (light + vis rays)
-    const int shard = blockIdx.x % kShards;
-    uint32_t* sc_ctr = a.cnt->shard[shard];
-    bool want[3] = {want_ext, want_l, want_b};
-    uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
-    uint32_t slot[3], total[3];
-    block_push<3>(want, ctr, slot, total);
-    if (want_ext) a.ext_q[shard * a.ext_cap + slot[0]] = pid;
-    if (want_l) a.any_q[shard * a.any_cap + slot[1]] = 2 * pid;
-    if (want_b) a.any_q[shard * a.any_cap + slot[2]] = 2 * pid + 1;
-    // ray statistics: queued + resolved-in-place rays of each kind (per-wave reduce)
-    uint32_t n_ext = want_ext || trivial_ext, n_any = (want_l ? 1u : 0u) + (want_b ? 1u : 0u) + trivial_any;
-    uint32_t n_vis = (fl_vis_ray ? 1u : 0u);
-    for (int off = 32; off > 0; off >>= 1) {
-        n_ext += __shfl_xor(n_ext, off);
-        n_any += __shfl_xor(n_any, off);
-        n_vis += __shfl_xor(n_vis, off);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        if (n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
-        if (n_any) atomicAdd(sc_ctr + C_ANY_RAYS, n_any);
-        if (n_vis) atomicAdd(sc_ctr + C_VIS, n_vis);
+    // ---- phase 2: compact the continuing paths onto the first threads of the block
+    {
+        const uint64_t m = __ballot(cont);
+        const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (lane == 0) s_wave_cnt[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t base = 0, ncont = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; w++) {
+            const uint32_t c = s_wave_cnt[w];
+            base += (w < wave) ? c : 0u;
+            ncont += c;
+        }
+        if (cont) {
+            const uint32_t i = base + pre;
+            s_pid[i] = pid | (cont_len << 24);
+            s_samples[i] = cont_samples;
+            s_beta[0][i] = beta_store.x;
+            s_beta[1][i] = beta_store.y;
+            s_beta[2][i] = beta_store.z;
+        }
+        __syncthreads();
+        MatOut mo{false, false, false, false, false, 0u};
+        uint32_t mpid = 0;
+        if (threadIdx.x < ncont) {
+            const uint32_t e = s_pid[threadIdx.x];
+            mpid = e & 0xffffffu;
+            mo = material(a, mpid, s_samples[threadIdx.x], e >> 24,
+                          v3(s_beta[0][threadIdx.x], s_beta[1][threadIdx.x], s_beta[2][threadIdx.x]));
+        }
+        // ---- phase 3: queue pushes (one atomic per block and queue)
+        const int shard = blockIdx.x % kShards;
+        uint32_t* sc_ctr = a.cnt->shard[shard];
+        bool want[4] = {gen_ext, mo.want_ext, mo.want_l, mo.want_b};
+        uint32_t* ctr[4] = {sc_ctr + C_EXT, sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
+        uint32_t slot[4], total[4];
+        block_push<4>(want, ctr, slot, total);
+        if (gen_ext) a.ext_q[shard * a.ext_cap + slot[0]] = pid;
+        if (mo.want_ext) a.ext_q[shard * a.ext_cap + slot[1]] = mpid;
+        if (mo.want_l) a.any_q[shard * a.any_cap + slot[2]] = 2 * mpid;
+        if (mo.want_b) a.any_q[shard * a.any_cap + slot[3]] = 2 * mpid + 1;
+        // ray statistics: queued + resolved-in-place rays of each kind (per-wave reduce)
+        uint32_t n_ext = (gen_ext || gen_trivial ? 1u : 0u) + (mo.want_ext || mo.trivial_ext ? 1u : 0u);
+        uint32_t n_any = (mo.want_l ? 1u : 0u) + (mo.want_b ? 1u : 0u) + mo.trivial_any;
+        uint32_t n_vis = mo.vis_ray ? 1u : 0u;
+        for (int off = 32; off > 0; off >>= 1) {
+            n_ext += __shfl_xor(n_ext, off);
+            n_any += __shfl_xor(n_any, off);
+            n_vis += __shfl_xor(n_vis, off);
+        }
+        if (lane == 0) {
+            if (n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
+            if (n_any) atomicAdd(sc_ctr + C_ANY_RAYS, n_any);
+            if (n_vis) atomicAdd(sc_ctr + C_VIS, n_vis);
+        }
     }
 }
 

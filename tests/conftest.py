@@ -44,6 +44,13 @@ def scene_c2(mcpt_mod):
 
 
 @pytest.fixture(scope="session")
+def scene_c3(mcpt_mod):
+    """Config-3 deep-BVH proxy: 871,414-triangle displaced icosphere + ground."""
+    s = mcpt_mod.build_config_scene(3)
+    return s, s.arrays()
+
+
+@pytest.fixture(scope="session")
 def scene_cube(mcpt_mod):
     """Cube.glb (12 tris, exactly axis-aligned normals: the gram_schmidt NaN-frame case)."""
     s = mcpt_mod.Scene()

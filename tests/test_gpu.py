@@ -58,6 +58,41 @@ def test_trace_parity_random_rays(request, mcpt_mod, oracle, which):
     pt.close()
 
 
+def test_trace_parity_deep_bvh(mcpt_mod, oracle, scene_c3):
+    """Config-3 proxy (871,416 triangles, SAH depth 25): bitwise closest/any hits vs the oracle."""
+    s, a = scene_c3
+    pt = mcpt_mod.PathTracer(0)
+    pt.upload_scene(s)
+    ro, rd = random_rays(20000, 5, box=2.5)
+    ro[:, 1] += 1.0  # the proxy is centred at (0, 1, 0)
+    gp, gn, gt = pt.trace_closest(ro, rd)
+    op_, on, ot = oracle.trace_closest(a, ro, rd)
+    assert np.array_equal(gt, ot)
+    assert np.array_equal(gp.view(np.uint32), op_.view(np.uint32))
+    assert np.array_equal(gn.view(np.uint32), on.view(np.uint32))
+    assert np.array_equal(pt.trace_any(ro, rd), oracle.trace_any(a, ro, rd))
+    assert (gt >= 0).mean() > 0.3  # the rays do hit the surface
+    pt.close()
+
+
+def test_config3_1080p_band_parity(mcpt_mod, oracle, scene_c3):
+    """Config 3 (deep BVH) at 1080p, 1 spp on the GPU; a band of rows through the proxy's
+    silhouette re-executed by the oracle matches bit for bit."""
+    rc = mcpt_mod.CONFIGS[3]
+    W, H = rc.width, rc.height
+    cam = mcpt_mod.config_camera(rc)
+    pt = make_pt(mcpt_mod, scene_c3[0], cam, W, H, 1, rc.max_depth)
+    st = pt.render()
+    Ld, smp = pt.film()
+    assert st.live_paths == 0 and np.all(smp[:-1, :-1] == 1)
+    r0, r1 = 600, 604
+    rL, rs, _ = oracle.render(scene_c3[1], cam, W, H, 1, rc.max_depth, rows=(r0, r1))
+    assert np.array_equal(smp[r0:r1], rs[r0:r1])
+    ok, nbad = film_close(Ld[r0:r1], rL[r0:r1])
+    assert ok, f"{nbad} radiance values differ"
+    pt.close()
+
+
 def test_trace_golden_fixtures(mcpt_mod, scene_c1, scene_cube):
     for name, (s, _) in (("c1", scene_c1), ("cube", scene_cube)):
         g = np.load(os.path.join(GOLDEN, f"trace_{name}_256.npz"))

@@ -1,0 +1,51 @@
+"""Steady-state throughput of every BASELINE config on one GPU (all tiles of the full frame).
+
+Prints one line per config: Mray/s over `--iters` wavefront iterations after `--warmup`,
+per-kernel ms per iteration, rays per iteration and BVH size.  Configs 4/5 are the
+8-GPU configs run here on a single device over the whole frame.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "mc-path-tracer_amd"))
+import mcpt  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--configs", default="1,2,3,4,5")
+ap.add_argument("--warmup", type=int, default=20)
+ap.add_argument("--iters", type=int, default=30)
+ap.add_argument("--out", default=None)
+args = ap.parse_args()
+res = []
+for c in [int(x) for x in args.configs.split(",")]:
+    rc = mcpt.CONFIGS[c]
+    t0 = time.time()
+    scene = mcpt.build_config_scene(c)
+    t_build = time.time() - t0
+    a = scene.arrays()
+    pt = mcpt.PathTracer(0, mcpt.default_config(spp=rc.spp, max_depth=rc.max_depth))
+    pt.upload_scene(scene)
+    pt.set_camera(mcpt.config_camera(rc))
+    pt.resize(rc.width, rc.height)
+    pt.iterate(args.warmup)
+    t1 = time.time()
+    st = pt.iterate(args.iters)
+    wall = time.time() - t1
+    rays = st.extend_rays + st.shadow_rays + st.vis_rays
+    r = {"config": c, "W": rc.width, "H": rc.height, "spp": rc.spp, "depth": rc.max_depth,
+         "tris": int(len(a["mat"])), "bvh_depth": scene.bvh_depth, "host_build_s": round(t_build, 2),
+         "mray_s": round(rays / (st.ms_total * 1e-3) / 1e6, 1), "mray_s_wall": round(rays / wall / 1e6, 1),
+         "ms_trace": round(st.ms_extend / args.iters, 4), "ms_shade": round(st.ms_shade / args.iters, 4),
+         "rays_per_iter": {"extend": st.extend_rays // args.iters, "shadow": st.shadow_rays // args.iters,
+                           "vis": st.vis_rays // args.iters},
+         "ext_nodes_per_ray": round(st.ext_nodes / max(1, st.extend_rays), 2),
+         "any_nodes_per_ray": round(st.any_nodes / max(1, st.shadow_rays + st.vis_rays), 2)}
+    print(json.dumps(r), flush=True)
+    res.append(r)
+    pt.close()
+if args.out:
+    json.dump(res, open(args.out, "w"), indent=1)
