@@ -3,9 +3,10 @@
 // One wavefront iteration (= one reference wavefront_pathtrace call,
 // wavefront_kernels.cu:377-442, widened from one 256x256 tile to a tile set):
 //   k_shade   fused wf_logic + wf_generate + wf_mat_mix  (wavefront_kernels.cu:90-251, 295-375)
-//   k_extend  wf_extend: closest-hit BVH traversal      (wavefront_kernels.cu:253-272, Triangle.cu:144-203)
-//   k_anyhit  wf_shadow + the BRDF visibility ray that the reference traces inline in
-//             wf_mat_mix (wavefront_kernels.cu:274-293, 334-336; Triangle.cu:204-243)
+//   k_trace   one persistent launch for both ray sets: wf_extend closest hit
+//             (wavefront_kernels.cu:253-272, Triangle.cu:144-203) and wf_shadow + the BRDF
+//             visibility ray that the reference traces inline in wf_mat_mix
+//             (wavefront_kernels.cu:274-293, 334-336; Triangle.cu:204-243)
 // The material stage evaluates the BRDF-sample terms unconditionally and the
 // visibility bit selects them in the next k_shade; this is exactly the
 // reference's result (f_brdf = Li_brdf = 0, pdf_brdf.x = pdf_light.y = 1 when
