@@ -144,6 +144,10 @@ int mcpt_device_name(mcpt_ctx *ctx, char *buf, int32_t len);
  * device time of the last mcpt_stage_run kernel. */
 int mcpt_debug_queue_rays(mcpt_ctx *ctx, int which, float *ray_o, float *ray_d, uint32_t *n_inout);
 float mcpt_debug_last_stage_ms(const mcpt_ctx *ctx);
+/* k_trace loop profile (diagnostics builds with -DMCPT_TRACE_PROF; returns 0 and zeros otherwise):
+ * out8 = {loop trips, refills, node lane-steps, triangle phases, triangle lane-steps, -, idle lane-trips, -}
+ * summed over waves since the last reset. */
+int mcpt_debug_trace_profile(mcpt_ctx *ctx, uint64_t *out8, int reset);
 
 /* ---- host scene builder (Scene.cu:24-470, EnvironmentLight.cu:329-452, BVH.cu) ---- */
 mcpt_scene *mcpt_scene_new(void);

@@ -103,23 +103,32 @@ constexpr int kEnd = -1;  // not a valid leaf: offset + count <= ntri < 2^24
 
 __device__ inline bool keep_box(float t0, float t1, float cut) { return !(t1 < -kCullAbs) && !(t0 > cut); }
 
-// Same decisions as slab() for rays whose inverse direction is finite in all
-// three components (no slab product can be NaN then): per axis the entry t is
-// <= the exit t (monotone rounding), so the reference's pairwise overlap tests
-// reduce to max3(entries) <= min3(exits) (Helly in 1-D), and the returned t0/t1
-// equal the reference's running max/min up to the sign of zero.  Rays with an
-// infinite inverse component take slab().
-__device__ inline bool slab_fast(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, V3 o, V3 inv,
-                                 int nx, int ny, int nz, float& t0, float& t1) {
-    float bx0 = nx ? mxx : mnx, bx1 = nx ? mnx : mxx;
-    float by0 = ny ? mxy : mny, by1 = ny ? mny : mxy;
-    float bz0 = nz ? mxz : mnz, bz1 = nz ? mnz : mxz;
-    const float tmin = (bx0 - o.x) * inv.x, tmax = (bx1 - o.x) * inv.x;
-    const float tymin = (by0 - o.y) * inv.y, tymax = (by1 - o.y) * inv.y;
-    const float tzmin = (bz0 - o.z) * inv.z, tzmax = (bz1 - o.z) * inv.z;
-    t0 = __builtin_fmaxf(__builtin_fmaxf(tmin, tymin), tzmin);
-    t1 = __builtin_fminf(__builtin_fminf(tmax, tymax), tzmax);
-    return t0 <= t1;
+// Both child boxes of a pair node at once, for rays whose inverse direction is
+// finite in all three components (then no slab product can be NaN).  The six
+// plane differences and products per box run as packed fp32 pairs (one
+// v_pk_add_f32 + one v_pk_mul_f32 per axis and plane: the two boxes' planes
+// sit side by side in the node).  Entry/exit per axis are min/max of the two
+// products: by monotone rounding they equal the reference's sign-selected near
+// and far products (Bounds3f.h:121-153), and the reference's pairwise overlap
+// tests reduce to max3(entries) <= min3(exits) (Helly in 1-D); t0/t1 equal its
+// running max/min up to the sign of zero.  Rays with an infinite inverse
+// component take slab().
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ inline void pair_slab(float4 qx, float4 qy, float4 qz, V3 o, V3 inv, float& t0a, float& t1a, float& t0b,
+                                 float& t1b) {
+    const f2v ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const f2v ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+    const f2v ax = (f2v{qx.x, qx.y} - ox) * ix, bx = (f2v{qx.z, qx.w} - ox) * ix;
+    const f2v ay = (f2v{qy.x, qy.y} - oy) * iy, by = (f2v{qy.z, qy.w} - oy) * iy;
+    const f2v az = (f2v{qz.x, qz.y} - oz) * iz, bz = (f2v{qz.z, qz.w} - oz) * iz;
+    t0a = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax.x, bx.x), __builtin_fminf(ay.x, by.x)),
+                          __builtin_fminf(az.x, bz.x));
+    t1a = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax.x, bx.x), __builtin_fmaxf(ay.x, by.x)),
+                          __builtin_fmaxf(az.x, bz.x));
+    t0b = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax.y, bx.y), __builtin_fminf(ay.y, by.y)),
+                          __builtin_fminf(az.y, bz.y));
+    t1b = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax.y, bx.y), __builtin_fmaxf(ay.y, by.y)),
+                          __builtin_fmaxf(az.y, bz.y));
 }
 
 // The first test the traversal makes: a NaN/zero direction or a ray that misses
@@ -462,6 +471,15 @@ __device__ inline void wave_stats(uint32_t* stats, int lane, uint32_t nodes, uin
     }
 }
 
+// Optional loop profile of k_trace (diagnostics build, -DMCPT_TRACE_PROF): per
+// launch sums of wave-level events, read back with mcpt_debug_trace_profile().
+#ifdef MCPT_TRACE_PROF
+__device__ unsigned long long g_trace_prof[8];
+#define PROF_ADD(i, v) (prof[i] += (v))
+#else
+#define PROF_ADD(i, v) ((void)0)
+#endif
+
 #ifdef MCPT_TRACE_WPE
 #define MCPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_TRACE_WPE, MCPT_TRACE_WPE)))
 #else
@@ -485,14 +503,16 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     if (Ltot == 0) return;
     const DevScene& sc = a.scene;
 
-    uint32_t nodes[2] = {0, 0}, tests[2] = {0, 0}, hits[2] = {0, 0};
+    // work counters: per ray (rn, rt), folded into per-set totals when the ray finishes
+    // (a runtime-indexed array here would be placed in LDS by the compiler)
+    uint32_t rn = 0, rt = 0, tot_n0 = 0, tot_t0 = 0, tot_h0 = 0, tot_n1 = 0, tot_t1 = 0, tot_h1 = 0;
     uint32_t next = 0;  // wave-uniform position in the sequence
     bool act = false;
     int kind = 0;  // 0 closest, 1 any
-    uint32_t rid = 0, qi = 0, step0 = 0;
+    uint32_t rid = 0, qi = 0;
     V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
     int nx = 0, ny = 0, nz = 0, ref = kEnd, leaf = kEnd, sp = 0, tri = -1;
-    bool fin = true;  // inverse direction finite: slab_fast() is exact
+    bool fin = true;  // inverse direction finite: pair_slab() is exact
     float best = K_HUGE, cut = K_HUGE;
 #ifndef MCPT_X_NOSPILL
     int2 spill[kMaxStack - kLdsStack];
@@ -519,14 +539,20 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         return kEnd;
     };
     auto finish = [&]() {
-        hits[kind] += tri >= 0;
+        const uint32_t h = tri >= 0;
+        if (kind) { tot_n1 += rn; tot_t1 += rt; tot_h1 += h; }
+        else { tot_n0 += rn; tot_t0 += rt; tot_h0 += h; }
         uint32_t* rs = a.set[kind].ray_steps;
-        if (rs) rs[qi] = nodes[kind] + tests[kind] - step0;
+        if (rs) rs[qi] = rn + rt;
         if (kind) a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
         else a.hit_tri[rid] = tri;                  // hit record rebuilt by the consumer (hit_record())
         act = false;
     };
+#ifdef MCPT_TRACE_PROF
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // trips, refills, node lanes, tri phases, tri lanes, finishes, idle lanes
+#endif
     for (;;) {
+        PROF_ADD(0, 1);
         // ---- refill idle lanes from the wave's sequence
         const uint64_t idle = __ballot(!act);
         const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -546,7 +572,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     const float4 o4 = ts.ro[rid], d4 = ts.rd[rid];
                     o = xyz(o4);
                     d = xyz(d4);
-                    step0 = nodes[kind] + tests[kind];
+                    rn = 0;
+                    rt = 0;
                     tri = -1;
                     best = K_HUGE;
                     cut = best + best * kCullRel;
@@ -574,6 +601,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 }
             }
             next += nidle;
+            PROF_ADD(1, 1);
         }
         if (__ballot(act) == 0) {
             if (next >= Ltot) break;
@@ -585,15 +613,18 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             if (ref >= 0) {
                 const float4* nd = sc.nodes + 4 * ref;
                 const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-                nodes[kind]++;
+                rn++;
                 float a0, b0, a1, b1;
                 bool h0, h1;
+                // node layout (SoA pairs): q0 = (mn.x, mn.x', mx.x, mx.x'), q1 = y, q2 = z,
+                // q3 = (child ref, child ref', axis, -); unprimed = first child
                 if (fin) {
-                    h0 = slab_fast(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, o, inv, nx, ny, nz, a0, b0);
-                    h1 = slab_fast(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, o, inv, nx, ny, nz, a1, b1);
+                    pair_slab(q0, q1, q2, o, inv, a0, b0, a1, b1);
+                    h0 = a0 <= b0;
+                    h1 = a1 <= b1;
                 } else {
-                    h0 = slab(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, o, inv, nx, ny, nz, a0, b0);
-                    h1 = slab(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, o, inv, nx, ny, nz, a1, b1);
+                    h0 = slab(q0.x, q1.x, q2.x, q0.z, q1.z, q2.z, o, inv, nx, ny, nz, a0, b0);
+                    h1 = slab(q0.y, q1.y, q2.y, q0.w, q1.w, q2.w, o, inv, nx, ny, nz, a1, b1);
                 }
                 h0 = h0 && keep_box(a0, b0, cut);
                 h1 = h1 && keep_box(a1, b1, cut);
@@ -626,12 +657,16 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         // leaf, or no lane has node work left, each parked leaf tests one triangle
         const uint32_t n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
         const uint32_t n_node = (uint32_t)__popcll(__ballot(act && ref >= 0));
+        PROF_ADD(2, n_node);
+        PROF_ADD(6, (uint32_t)__popcll(__ballot(!act)));
         if (n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node)) {
+            PROF_ADD(3, 1);
+            PROF_ADD(4, n_tri);
             if (leaf != kEnd) {
                 const int id = leaf & 0xffffff;
                 const float4* tp = sc.tri + 3 * id;
                 const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-                tests[kind]++;
+                rt++;
                 float t, u, v;
                 bool done = false;
                 if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) &&
@@ -654,8 +689,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         }
         if (act && ref == kEnd && leaf == kEnd) finish();
     }
-    wave_stats(a.set[0].stats, lane, nodes[0], tests[0], hits[0]);
-    wave_stats(a.set[1].stats, lane, nodes[1], tests[1], hits[1]);
+#ifdef MCPT_TRACE_PROF
+    if (lane == 0)
+        for (int i = 0; i < 8; i++) atomicAdd(&g_trace_prof[i], (unsigned long long)prof[i]);
+#endif
+    wave_stats(a.set[0].stats, lane, tot_n0, tot_t0, tot_h0);
+    wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);
 }
 
 __global__ void k_hit_record(HitRecordArgs a) {  // stage_run(EXTEND) outputs
@@ -783,6 +822,20 @@ void launch_trace(const TraceArgs& args, hipStream_t s) {
     const uint32_t nsh = (uint32_t)a.nshards;
     const uint32_t wps = std::max<uint32_t>(1, persistent_waves() / nsh);
     hipLaunchKernelGGL(k_trace, dim3(wps * nsh), dim3(kTraceBlock), 0, s, a);
+}
+int trace_profile(unsigned long long* out, int reset) {  // diagnostics build only
+#ifdef MCPT_TRACE_PROF
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace_prof), sizeof(g_trace_prof)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_trace_prof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 8;
+#else
+    (void)out;
+    (void)reset;
+    return 0;
+#endif
 }
 void launch_clear(const ClearArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_clear, dim3((a.n + 255) / 256), dim3(256), 0, s, a);

@@ -115,6 +115,7 @@ struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; 
 void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s);
 void launch_trace(const TraceArgs& a, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
+int trace_profile(unsigned long long* out, int reset);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);
 void launch_accumulate(CounterBlock* c, hipStream_t s);

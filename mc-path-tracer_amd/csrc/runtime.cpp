@@ -191,9 +191,10 @@ int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) {
         int c0 = i + 1, c1 = d->offset[i];
         const float *a0 = d->bmin + 3 * c0, *b0 = d->bmax + 3 * c0, *a1 = d->bmin + 3 * c1, *b1 = d->bmax + 3 * c1;
         float4* q = &pn[(size_t)pair_of[i] * 4];
-        q[0] = make_float4(a0[0], a0[1], a0[2], b0[0]);
-        q[1] = make_float4(b0[1], b0[2], a1[0], a1[1]);
-        q[2] = make_float4(a1[2], b1[0], b1[1], b1[2]);
+        // SoA pairs: per axis (min child 0, min child 1, max child 0, max child 1)
+        q[0] = make_float4(a0[0], a1[0], b0[0], b1[0]);
+        q[1] = make_float4(a0[1], a1[1], b0[1], b1[1]);
+        q[2] = make_float4(a0[2], a1[2], b0[2], b1[2]);
         int r0 = ref_of(c0), r1 = ref_of(c1);
         float fr0, fr1, fax;
         int ax = d->axis[i];
@@ -686,4 +687,13 @@ int mcpt_debug_queue_rays(mcpt_ctx* c, int which, float* ro, float* rd, uint32_t
     return MCPT_OK;
 }
 float mcpt_debug_last_stage_ms(const mcpt_ctx* c) { return c ? c->last_stage_ms : -1.f; }
+
+int mcpt_debug_trace_profile(mcpt_ctx* c, uint64_t* out8, int reset) {
+    if (!c || !out8) return MCPT_E_INVALID;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int n = trace_profile(v, reset);
+    for (int i = 0; i < 8; i++) out8[i] = v[i];
+    return n;
+}
 }

@@ -101,6 +101,7 @@ ABI = {
     "mcpt_device_name": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
     "mcpt_debug_queue_rays": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _u]),
     "mcpt_debug_last_stage_ms": (C.c_float, [C.c_void_p]),
+    "mcpt_debug_trace_profile": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "mcpt_scene_new": (C.c_void_p, []),
     "mcpt_scene_free": (None, [C.c_void_p]),
     "mcpt_scene_load_glb": (C.c_int, [C.c_void_p, C.c_char_p, _f]),
@@ -392,6 +393,13 @@ class PathTracer:
     @property
     def last_stage_ms(self) -> float:
         return lib().mcpt_debug_last_stage_ms(self.h)
+
+    def trace_profile(self, reset=True):
+        """k_trace loop profile (diagnostics build only): dict of summed wave-level counts."""
+        v = (C.c_uint64 * 8)()
+        n = lib().mcpt_debug_trace_profile(self.h, v, int(reset))
+        names = ("trips", "refills", "node_lanes", "tri_phases", "tri_lanes", "_5", "idle_lanes", "_7")
+        return {k: int(x) for k, x in zip(names, v)} if n > 0 else None
 
     def queue_rays(self):
         """Rays of the current extension queue (diagnostics)."""

@@ -1,0 +1,20 @@
+"""k_trace loop profile on steady-state config-2 iterations (needs the -DMCPT_TRACE_PROF build)."""
+import os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "mc-path-tracer_amd")]
+import mcpt
+rc = mcpt.CONFIGS[2]
+pt = mcpt.PathTracer(0, mcpt.default_config(spp=256, max_depth=5))
+pt.upload_scene(mcpt.build_config_scene(2)); pt.set_camera(mcpt.config_camera(rc)); pt.resize(rc.width, rc.height)
+pt.iterate(30)
+pt.trace_profile(reset=True)
+N = 10
+st = pt.iterate(N)
+p = pt.trace_profile()
+waves = 7168
+print({k: v / N for k, v in p.items()})
+trips = p["trips"] / N
+print("per iteration: trips/wave %.0f  node-lane util %.3f  idle-lane frac %.3f  tri phases/trip %.3f  tri lanes/phase %.1f" % (
+    trips / waves, p["node_lanes"] / (64 * p["trips"]), p["idle_lanes"] / (64 * p["trips"]), p["tri_phases"] / p["trips"],
+    p["tri_lanes"] / max(1, p["tri_phases"])))
+print("units: nodes %.1fM tests %.1fM  | ms trace %.3f" % ((st.ext_nodes + st.any_nodes) / N / 1e6, (st.ext_tests + st.any_tests) / N / 1e6, st.ms_extend / N))
