@@ -145,9 +145,10 @@ int mcpt_device_name(mcpt_ctx *ctx, char *buf, int32_t len);
 int mcpt_debug_queue_rays(mcpt_ctx *ctx, int which, float *ray_o, float *ray_d, uint32_t *n_inout);
 float mcpt_debug_last_stage_ms(const mcpt_ctx *ctx);
 /* k_trace loop profile (diagnostics builds with -DMCPT_TRACE_PROF; returns 0 and zeros otherwise):
- * out8 = {loop trips, refills, node lane-steps, triangle phases, triangle lane-steps, -, idle lane-trips, -}
+ * out12 = {loop trips, refills, node lane-steps, triangle phases, triangle lane-steps, trips with a finish,
+ * idle lane-trips, trips with a pop, popping lanes, trips with a non-finite-direction slab, finishing lanes, -}
  * summed over waves since the last reset. */
-int mcpt_debug_trace_profile(mcpt_ctx *ctx, uint64_t *out8, int reset);
+int mcpt_debug_trace_profile(mcpt_ctx *ctx, uint64_t *out12, int reset);
 
 /* ---- host scene builder (Scene.cu:24-470, EnvironmentLight.cu:329-452, BVH.cu) ---- */
 mcpt_scene *mcpt_scene_new(void);

@@ -474,11 +474,16 @@ __device__ inline void wave_stats(uint32_t* stats, int lane, uint32_t nodes, uin
 // Optional loop profile of k_trace (diagnostics build, -DMCPT_TRACE_PROF): per
 // launch sums of wave-level events, read back with mcpt_debug_trace_profile().
 #ifdef MCPT_TRACE_PROF
-__device__ unsigned long long g_trace_prof[8];
+__device__ unsigned long long g_trace_prof[12];
 #define PROF_ADD(i, v) (prof[i] += (v))
 #else
 #define PROF_ADD(i, v) ((void)0)
 #endif
+
+#ifndef MCPT_NODE_STEPS
+#define MCPT_NODE_STEPS 4
+#endif
+constexpr int kNodeSteps = MCPT_NODE_STEPS;
 
 #ifdef MCPT_TRACE_WPE
 #define MCPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_TRACE_WPE, MCPT_TRACE_WPE)))
@@ -542,14 +547,14 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         const uint32_t h = tri >= 0;
         if (kind) { tot_n1 += rn; tot_t1 += rt; tot_h1 += h; }
         else { tot_n0 += rn; tot_t0 += rt; tot_h0 += h; }
-        uint32_t* rs = a.set[kind].ray_steps;
+        uint32_t* rs = kind ? a.set[1].ray_steps : a.set[0].ray_steps;
         if (rs) rs[qi] = rn + rt;
         if (kind) a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
         else a.hit_tri[rid] = tri;                  // hit record rebuilt by the consumer (hit_record())
         act = false;
     };
 #ifdef MCPT_TRACE_PROF
-    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // trips, refills, node lanes, tri phases, tri lanes, finishes, idle lanes
+    uint64_t prof[12] = {};  // see mcpt_debug_trace_profile
 #endif
     for (;;) {
         PROF_ADD(0, 1);
@@ -566,10 +571,14 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 if (kind) s -= L[0];
                 const uint32_t k = (w_in + (s >> 6) * wps) * 64u + (s & 63u);
                 if (s < (kind ? L[1] : L[0]) && k < nk) {
-                    const TraceSet& ts = a.set[kind];
-                    qi = shard * ts.shard_cap + k;
-                    rid = ts.queue ? ts.queue[qi] : qi;
-                    const float4 o4 = ts.ro[rid], d4 = ts.rd[rid];
+                    // select the set's fields with ternaries: indexing a.set[kind] with a
+                    // per-lane kind makes hipcc fetch them from kernarg memory per lane
+                    const uint32_t* qp = kind ? a.set[1].queue : a.set[0].queue;
+                    const float4* rop = kind ? a.set[1].ro : a.set[0].ro;
+                    const float4* rdp = kind ? a.set[1].rd : a.set[0].rd;
+                    qi = shard * (kind ? a.set[1].shard_cap : a.set[0].shard_cap) + k;
+                    rid = qp ? qp[qi] : qi;
+                    const float4 o4 = rop[rid], d4 = rdp[rid];
                     o = xyz(o4);
                     d = xyz(d4);
                     rn = 0;
@@ -607,8 +616,11 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             if (next >= Ltot) break;
             continue;
         }
-        // ---- node phase: one child-pair test per lane holding an interior node
+        // ---- node phase: up to kNodeSteps child-pair tests per lane holding an
+        // interior node (amortises the per-trip bookkeeping over several steps)
         if (act) {
+#pragma unroll 1
+          for (int it = 0; it < kNodeSteps; it++) {
             bool need_pop = false;
             if (ref >= 0) {
                 const float4* nd = sc.nodes + 4 * ref;
@@ -651,7 +663,14 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 leaf = ref;
                 need_pop = true;
             }
+#ifdef MCPT_TRACE_PROF
+            PROF_ADD(7, __ballot(need_pop) != 0);
+            PROF_ADD(8, (uint32_t)__popcll(__ballot(need_pop)));
+            PROF_ADD(9, __ballot(!fin && ref >= 0) != 0);
+#endif
             if (need_pop) ref = pop();
+            if (ref < 0) break;  // parked-leaf slot full or traversal done: wait for the triangle phase
+          }
         }
         // ---- triangle phase (wave-uniform): when enough lanes have a parked
         // leaf, or no lane has node work left, each parked leaf tests one triangle
@@ -687,11 +706,15 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 }
             }
         }
+#ifdef MCPT_TRACE_PROF
+        PROF_ADD(5, __ballot(act && ref == kEnd && leaf == kEnd) != 0);
+        PROF_ADD(10, (uint32_t)__popcll(__ballot(act && ref == kEnd && leaf == kEnd)));
+#endif
         if (act && ref == kEnd && leaf == kEnd) finish();
     }
 #ifdef MCPT_TRACE_PROF
     if (lane == 0)
-        for (int i = 0; i < 8; i++) atomicAdd(&g_trace_prof[i], (unsigned long long)prof[i]);
+        for (int i = 0; i < 12; i++) atomicAdd(&g_trace_prof[i], (unsigned long long)prof[i]);
 #endif
     wave_stats(a.set[0].stats, lane, tot_n0, tot_t0, tot_h0);
     wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);
@@ -827,10 +850,10 @@ int trace_profile(unsigned long long* out, int reset) {  // diagnostics build on
 #ifdef MCPT_TRACE_PROF
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace_prof), sizeof(g_trace_prof)) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[12] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_trace_prof), z, sizeof(z)) != hipSuccess) return -1;
     }
-    return 8;
+    return 12;
 #else
     (void)out;
     (void)reset;

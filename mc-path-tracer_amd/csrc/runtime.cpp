@@ -688,12 +688,12 @@ int mcpt_debug_queue_rays(mcpt_ctx* c, int which, float* ro, float* rd, uint32_t
 }
 float mcpt_debug_last_stage_ms(const mcpt_ctx* c) { return c ? c->last_stage_ms : -1.f; }
 
-int mcpt_debug_trace_profile(mcpt_ctx* c, uint64_t* out8, int reset) {
+int mcpt_debug_trace_profile(mcpt_ctx* c, uint64_t* out8, int reset) {  // out8: 12 words
     if (!c || !out8) return MCPT_E_INVALID;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long v[12] = {};
     int n = trace_profile(v, reset);
-    for (int i = 0; i < 8; i++) out8[i] = v[i];
+    for (int i = 0; i < 12; i++) out8[i] = v[i];
     return n;
 }
 }

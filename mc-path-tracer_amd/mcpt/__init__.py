@@ -396,9 +396,10 @@ class PathTracer:
 
     def trace_profile(self, reset=True):
         """k_trace loop profile (diagnostics build only): dict of summed wave-level counts."""
-        v = (C.c_uint64 * 8)()
+        v = (C.c_uint64 * 12)()
         n = lib().mcpt_debug_trace_profile(self.h, v, int(reset))
-        names = ("trips", "refills", "node_lanes", "tri_phases", "tri_lanes", "_5", "idle_lanes", "_7")
+        names = ("trips", "refills", "node_lanes", "tri_phases", "tri_lanes", "finish_trips", "idle_lanes",
+                 "pop_trips", "pop_lanes", "slow_slab_trips", "finish_lanes", "_11")
         return {k: int(x) for k, x in zip(names, v)} if n > 0 else None
 
     def queue_rays(self):

@@ -33,5 +33,6 @@ for v in sys.argv[1:]:
         lib = os.path.join(REPO, "mc-path-tracer_amd", "libmcpt.so")
     else:
         lib = os.path.join(REPO, "mc-path-tracer_amd", "libmcpt.so" if v == "base" else f"libmcpt_{v}.so")
-    env = dict(os.environ, MCPT_LIB=lib, VARIANT=v, **extra)
+    env = dict(os.environ, MCPT_LIB=lib, VARIANT=v)
+    env.update(extra)
     subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=300)

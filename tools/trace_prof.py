@@ -17,4 +17,8 @@ trips = p["trips"] / N
 print("per iteration: trips/wave %.0f  node-lane util %.3f  idle-lane frac %.3f  tri phases/trip %.3f  tri lanes/phase %.1f" % (
     trips / waves, p["node_lanes"] / (64 * p["trips"]), p["idle_lanes"] / (64 * p["trips"]), p["tri_phases"] / p["trips"],
     p["tri_lanes"] / max(1, p["tri_phases"])))
+T = p["trips"]
+print("per trip: finish %.2f pop %.2f (lanes/pop %.1f) slow-slab %.3f refill %.3f tri %.3f" % (
+    p["finish_trips"] / T, p["pop_trips"] / T, p["pop_lanes"] / max(1, p["pop_trips"]), p["slow_slab_trips"] / T,
+    p["refills"] / T, p["tri_phases"] / T))
 print("units: nodes %.1fM tests %.1fM  | ms trace %.3f" % ((st.ext_nodes + st.any_nodes) / N / 1e6, (st.ext_tests + st.any_tests) / N / 1e6, st.ms_extend / N))
