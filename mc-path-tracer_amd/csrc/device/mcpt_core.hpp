@@ -280,7 +280,14 @@ MCPT_HD int upper_bound(const float* list, int size, float val) {  // Helpers.cu
     if (left < size && list[left] <= val) left++;
     return left;
 }
-MCPT_HD int wrapi(int i, int n) { int r = i % n; return r < 0 ? r + n : r; }
+MCPT_HD int wrapi(int i, int n) {  // i mod n in [0, n); one conditional add/subtract covers |i| < 2n
+    int r = i < 0 ? i + n : (i >= n ? i - n : i);
+    if ((unsigned)r >= (unsigned)n) {
+        r = i % n;
+        r = r < 0 ? r + n : r;
+    }
+    return r;
+}
 MCPT_HD float q8(float a) { return __builtin_floorf(a * 256.f + 0.5f) * (1.0f / 256.f); }
 // Software tex2DLod<float4>: linear filter, wrap, normalized coords, 8-bit
 // fractional weights like the texture unit (dTexture.cu:265-271).  NaN -> 0.
@@ -309,10 +316,26 @@ MCPT_HD V3 env_L(const EnvView& e, V3 wi) {  // EnvironmentLight.cu:34-47
     spherical_map(wi, u, v);
     return tex_bilinear(e.tex, e.w, e.h, u, v);
 }
+MCPT_HD float env_pdf_uv(const EnvView& e, float u, float v);
 MCPT_HD float env_pdf(const EnvView& e, V3 wi) {  // EnvironmentLight.cu:65-85
     if (e.mode == 0 || e.tex == nullptr) return ONE_4PI_F;
     float u, v;
     spherical_map(wi, u, v);
+    return env_pdf_uv(e, u, v);
+}
+// env_L and env_pdf of one direction sharing its spherical map (same values as the two calls)
+MCPT_HD void env_L_pdf(const EnvView& e, V3 wi, V3& L, float& pdf) {
+    if (e.mode == 0 || e.tex == nullptr) {
+        L = v3(e.color[0], e.color[1], e.color[2]) * e.ls;
+        pdf = ONE_4PI_F;
+        return;
+    }
+    float u, v;
+    spherical_map(wi, u, v);
+    L = tex_bilinear(e.tex, e.w, e.h, u, v);
+    pdf = env_pdf_uv(e, u, v);
+}
+MCPT_HD float env_pdf_uv(const EnvView& e, float u, float v) {
     float fx = u * (float)(unsigned)(e.w - 1), fy = v * (float)(unsigned)(e.h - 1);
     int px = (fx == fx && fx >= 0.f && fx < (float)e.w) ? (int)fx : 0;
     int py = (fy == fy && fy >= 0.f && fy < (float)e.h) ? (int)fy : 0;

@@ -67,6 +67,15 @@ __device__ inline V3 light_L(const DevScene& sc, int id, V3 wi) {
     const float* p = sc.dirs + 7 * (id - 1);  // DirectionalLight.cu:34
     return v3(p[3], p[4], p[5]) * p[6];
 }
+__device__ inline void light_L_pdf(const DevScene& sc, int id, V3 wi, V3& L, float& pdf) {
+    if (id == 0) {
+        env_L_pdf(sc.env, wi, L, pdf);
+    } else {
+        const float* p = sc.dirs + 7 * (id - 1);  // DirectionalLight.cu:34, :40-43
+        L = v3(p[3], p[4], p[5]) * p[6];
+        pdf = 1.f;
+    }
+}
 __device__ inline float light_pdf(const DevScene& sc, int id, V3 wi) {
     if (id == 0) return env_pdf(sc.env, wi);
     return 1.f;  // DirectionalLight.cu:40-43
@@ -136,6 +145,12 @@ __device__ inline void pair_slab(float4 qx, float4 qy, float4 qz, V3 o, V3 inv, 
 // place instead of queueing them.
 __device__ inline bool ray_misses_scene(const DevScene& sc, V3 o, V3 d) {
     if (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f)) return true;
+    // An origin inside the root box cannot miss it: per axis (mn - o) <= 0 <= (mx - o)
+    // exactly, so entry <= 0 <= exit (or NaN, which passes), and the cull keeps the
+    // box.  Skips the three IEEE divisions for every bounce ray inside the scene.
+    if (o.x >= sc.root_mn[0] && o.x <= sc.root_mx[0] && o.y >= sc.root_mn[1] && o.y <= sc.root_mx[1] &&
+        o.z >= sc.root_mn[2] && o.z <= sc.root_mx[2])
+        return false;
     const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
     float t0, t1;
     const float cut = K_HUGE + K_HUGE * kCullRel;
@@ -203,8 +218,9 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     const Mat m = load_mat(sc.mats + 8 * mat);
     const bool delta = light_id > 0;
     V3 f_l = brdf_f(m, n, ldir, wo);
-    V3 Li_l = light_L(sc, light_id, ldir);
-    float pdfl_x = light_pdf(sc, light_id, ldir);
+    V3 Li_l;
+    float pdfl_x;
+    light_L_pdf(sc, light_id, ldir, Li_l, pdfl_x);
     float pdfb_y = !delta ? brdf_pdf(m, n, ldir, wo) : 1.f;
     float wL = power_heuristic(pdfl_x, pdfb_y);
     V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
@@ -217,9 +233,10 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
         so_b = pos + wi_b * 0.001f;
         sd_b = wi_b;
         V3 f_b = brdf_f(m, n, wi_b, wo);
-        V3 Li_b = light_L(sc, light_id, wi_b);
+        V3 Li_b;
+        float pdfl_y;
+        light_L_pdf(sc, light_id, wi_b, Li_b, pdfl_y);
         float pdfb_x = brdf_pdf(m, n, wi_b, wo);
-        float pdfl_y = light_pdf(sc, light_id, wi_b);
         float wB = power_heuristic(pdfb_x, pdfl_y);
         cB = ((f_b * Li_b) * wB) / pdfb_x;
         if (wB > 0.f && pdfb_x > 0.f) nf |= F_CONDB;
