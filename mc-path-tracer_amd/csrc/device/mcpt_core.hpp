@@ -97,6 +97,28 @@ MCPT_HD float dcos(float xx) {
     float r = (j == 1 || j == 2) ? sin_poly(x, z) : cos_poly(z);
     return sign < 0 ? -r : r;
 }
+// dsin and dcos of one argument with a shared range reduction: bit-identical to
+// the two separate calls (same reduction, same polynomials, same sign rules).
+MCPT_HD void dsincos(float xx, float& so, float& co) {
+    float x = xx;
+    if (x != x) { so = x; co = x; return; }
+    int ss = 1, cs = 1;
+    if (x < 0.f) { x = -x; ss = -1; }
+    if (!(x <= 8192.f)) { so = qnan(); co = qnan(); return; }
+    int j = (int)(FOPI * x);
+    float y = (float)j;
+    if (j & 1) { j += 1; y += 1.0f; }
+    j &= 7;
+    if (j > 3) { ss = -ss; cs = -cs; j -= 4; }
+    if (j > 1) cs = -cs;
+    x = ((x - y * DP1) - y * DP2) - y * DP3;
+    float z = x * x;
+    const float sp = sin_poly(x, z), cp = cos_poly(z);
+    const bool swap = (j == 1 || j == 2);
+    const float rs = swap ? cp : sp, rc = swap ? sp : cp;
+    so = ss < 0 ? -rs : rs;
+    co = cs < 0 ? -rc : rc;
+}
 MCPT_HD float dasin(float xx) {
     float a, x, z;
     int sign, flag;
@@ -248,11 +270,13 @@ MCPT_HD void spherical_map(V3 d, float& u, float& v) {
 MCPT_HD V3 spherical_direction(float u, float v) {
     float phi = (float)((double)(2.f * PI_F) * ((double)u - 0.5));  // fp64 island
     float theta = PI_F * v;
-    float st = dsin(theta);
+    float st, ct, sp, cp;
+    dsincos(theta, st, ct);
+    dsincos(phi, sp, cp);
     V3 n;
-    n.x = dcos(phi) * st;
-    n.z = dsin(phi) * st;
-    n.y = dcos(theta);
+    n.x = cp * st;
+    n.z = sp * st;
+    n.y = ct;
     return n;
 }
 
@@ -268,7 +292,13 @@ struct EnvView {
     const float* marginal_y;  // h
     const float* conds_y;     // h*w
     const float* pdf;         // h*w
+    // Optional search guides (device only, built at upload when the CDFs are
+    // sorted): guide_m[k] = upper_bound(marginal_y, h, k / kEnvGuide), k = 0..kEnvGuide,
+    // and the same per conditional row at guide_c[y * (kEnvGuide + 1) + k].
+    const int* guide_m;
+    const int* guide_c;
 };
+constexpr int kEnvGuide = 64;
 
 MCPT_HD int upper_bound(const float* list, int size, float val) {  // Helpers.cu:15-30
     int middle, left = 0, right = size;
@@ -278,6 +308,21 @@ MCPT_HD int upper_bound(const float* list, int size, float val) {  // Helpers.cu
         else right = middle;
     }
     if (left < size && list[left] <= val) left++;
+    return left;
+}
+// upper_bound on a sorted list whose answers at the bin edges k / kEnvGuide are
+// precomputed: for val in [k/G, (k+1)/G) (exact bin: G is a power of two) the
+// answer lies in [guide[k], guide[k+1]] by monotonicity, and the same bisection
+// restricted to that range returns it.  val in [0, 1) (rand_float).
+MCPT_HD int upper_bound_guided(const float* list, const int* guide, float val) {
+    int k = (int)(val * (float)kEnvGuide);
+    k = k < 0 ? 0 : (k > kEnvGuide - 1 ? kEnvGuide - 1 : k);
+    int left = guide[k], right = guide[k + 1];
+    while (left < right) {
+        const int middle = (right - left) / 2 + left;
+        if (val >= list[middle]) left = middle + 1;
+        else right = middle;
+    }
     return left;
 }
 MCPT_HD int wrapi(int i, int n) {  // i mod n in [0, n); one conditional add/subtract covers |i| < 2n
@@ -352,9 +397,16 @@ MCPT_HD V3 env_dir(const EnvView& e, const Rng& r) {  // EnvironmentLight.cu:10-
     }
     float ex = r(SL_ENV_U);
     float ey = r(SL_ENV_V);
-    int y = (int)((float)upper_bound(e.marginal_y, e.h, ey) - 1.f);
-    if (y < 0) y = 0;  // unreachable (marginal_y[0] == 0); reference reads row -1
-    int x = (int)((float)upper_bound(e.conds_y + (int64_t)y * e.w, e.w, ex) - 1.f);
+    int y, x;
+    if (e.guide_m) {
+        y = (int)((float)upper_bound_guided(e.marginal_y, e.guide_m, ey) - 1.f);
+        if (y < 0) y = 0;  // unreachable (marginal_y[0] == 0); reference reads row -1
+        x = (int)((float)upper_bound_guided(e.conds_y + (int64_t)y * e.w, e.guide_c + y * (kEnvGuide + 1), ex) - 1.f);
+    } else {
+        y = (int)((float)upper_bound(e.marginal_y, e.h, ey) - 1.f);
+        if (y < 0) y = 0;
+        x = (int)((float)upper_bound(e.conds_y + (int64_t)y * e.w, e.w, ex) - 1.f);
+    }
     float u = (float)x / (float)e.w;
     float v = (float)y / (float)e.h;
     return spherical_direction(u, v);
@@ -399,8 +451,10 @@ MCPT_HD V3 diff_get_wi(V3 N, const Rng& r, uint32_t s0) {  // dMaterial.cu:232-2
     float e1 = r(s0 + 1);
     float sinTheta = __builtin_sqrtf(1.f - e0 * e0);
     float phi = (2.f * PI_F) * e1;
-    float x = sinTheta * dcos(phi);
-    float z = sinTheta * dsin(phi);
+    float sp, cp;
+    dsincos(phi, sp, cp);
+    float x = sinTheta * cp;
+    float z = sinTheta * sp;
     V3 T = gram_schmidt(N, r, s0 + 2);
     V3 B = normalize(cross(N, T));
     return normalize((T * x + N * e0) + B * z);
@@ -421,8 +475,10 @@ MCPT_HD V3 spec_get_wi(const Mat& m, V3 N, V3 wo, const Rng& r, uint32_t s0) {  
     float e1 = r(s0 + 1);
     float theta = dacos(__builtin_sqrtf((1.f - e0) / (e0 * (a2 - 1.f) + 1.f)));
     float phi = TWO_PI_F * e1;
-    float st = dsin(theta);
-    V3 h = v3(st * dcos(phi), dcos(theta), st * dsin(phi));
+    float st, ct, sp, cp;
+    dsincos(theta, st, ct);
+    dsincos(phi, sp, cp);
+    V3 h = v3(st * cp, ct, st * sp);
     V3 T = gram_schmidt(N, r, s0 + 2);
     V3 B = normalize(cross(N, T));
     V3 smp = normalize((T * h.x + N * h.y) + B * h.z);
@@ -473,8 +529,10 @@ MCPT_HD void concentric_disk(const Rng& r, float& dx, float& dy) {  // Sample.cu
     float theta, rr;
     if (__builtin_fabsf(ox) > __builtin_fabsf(oy)) { rr = ox; theta = PI_4_F * (oy / ox); }
     else { rr = oy; theta = PI_2_F - PI_4_F * (ox / oy); }
-    dx = rr * dcos(theta);
-    dy = rr * dsin(theta);
+    float st, ct;
+    dsincos(theta, st, ct);
+    dx = rr * ct;
+    dy = rr * st;
 }
 MCPT_HD void gen_ray(const CamView& c, int W, int H, int xi, int yi, const Rng& r, V3& o, V3& d) {
     float x = (float)xi, y = (float)yi;

@@ -256,6 +256,7 @@ int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) {
     s.env.w = d->env_w;
     s.env.h = d->env_h;
     s.env.tex = nullptr;
+    s.env.guide_m = s.env.guide_c = nullptr;
     if (d->env_mode == 1) {
         float4* tx;
         float *my, *cy, *pd;
@@ -265,6 +266,31 @@ int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) {
         if ((rc = dupload(c, c->scene_bufs, &cy, d->env_conds_y, WH))) return rc;
         if ((rc = dupload(c, c->scene_bufs, &pd, d->env_pdf, WH))) return rc;
         s.env.tex = tx; s.env.marginal_y = my; s.env.conds_y = cy; s.env.pdf = pd;
+        // search guides for env_dir (only valid on sorted, NaN-free CDFs, which prefix sums
+        // of non-negative luminance are; otherwise the plain bisection is used)
+        auto sorted = [](const float* a, int n) {
+            for (int i = 0; i < n; i++)
+                if (!(a[i] == a[i]) || (i > 0 && a[i] < a[i - 1])) return false;
+            return true;
+        };
+        bool ok = sorted(d->env_marginal_y, d->env_h);
+        for (int y = 0; ok && y < d->env_h; y++) ok = sorted(d->env_conds_y + (size_t)y * d->env_w, d->env_w);
+        s.env.guide_m = s.env.guide_c = nullptr;
+        if (ok) {
+            const int G = mcpt::kEnvGuide;
+            std::vector<int> gm(G + 1), gc((size_t)d->env_h * (G + 1));
+            for (int k = 0; k <= G; k++) {
+                const float val = (float)k / (float)G;
+                gm[k] = mcpt::upper_bound(d->env_marginal_y, d->env_h, val);
+                for (int y = 0; y < d->env_h; y++)
+                    gc[(size_t)y * (G + 1) + k] = mcpt::upper_bound(d->env_conds_y + (size_t)y * d->env_w, d->env_w, val);
+            }
+            int *dgm, *dgc;
+            if ((rc = dupload(c, c->scene_bufs, &dgm, gm.data(), gm.size()))) return rc;
+            if ((rc = dupload(c, c->scene_bufs, &dgc, gc.data(), gc.size()))) return rc;
+            s.env.guide_m = dgm;
+            s.env.guide_c = dgc;
+        }
     }
     c->scene = s;
     c->has_scene = true;
