@@ -138,6 +138,13 @@ int mcpt_film_read(mcpt_ctx *ctx, float *Ld_rgb, uint32_t *samples);         /* 
 int mcpt_film_read_device(mcpt_ctx *ctx, void *d_Ld_rgb, void *d_samples);  /* device-to-device */
 int mcpt_film_pack_tiles(mcpt_ctx *ctx, void *d_out, uint32_t *npix);       /* tile-set pixels -> packed 16 B/px (rgb f32, samples u32) */
 int mcpt_film_tonemap_rgba8(mcpt_ctx *ctx, float exposure, uint8_t *out);   /* == draw_to_surface */
+int mcpt_film_size(const mcpt_ctx *ctx, uint32_t *w, uint32_t *h);
+/* Film output (replaces stbi_write_png of the display buffer, RenderingContext.cpp:114-118):
+ * PNG = tonemapped 8-bit RGB, row 0 = top; PFM = float RGB radiance Ld/samples (0 where no sample). */
+int mcpt_film_write_png(mcpt_ctx *ctx, float exposure, const char *path);
+int mcpt_film_write_pfm(mcpt_ctx *ctx, const char *path);
+int mcpt_image_write_png(const char *path, uint32_t w, uint32_t h, const uint8_t *rgba8);
+int mcpt_image_write_pfm(const char *path, uint32_t w, uint32_t h, const float *rgb);
 int mcpt_sync(mcpt_ctx *ctx);
 int mcpt_device_name(mcpt_ctx *ctx, char *buf, int32_t len);
 /* diagnostics: rays of the current extension (which=0) or any-hit (which=1) queue, and the

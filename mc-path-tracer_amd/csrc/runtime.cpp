@@ -667,6 +667,14 @@ int mcpt_film_pack_tiles(mcpt_ctx* c, void* d_out, uint32_t* npix) {
     return MCPT_OK;
 }
 
+int mcpt_film_size(const mcpt_ctx* c, uint32_t* w, uint32_t* h) {
+    if (!c || !w || !h) return MCPT_E_INVALID;
+    if (!c->P) return set_err(const_cast<mcpt_ctx*>(c), MCPT_E_INVALID, "film not allocated");
+    *w = c->W;
+    *h = c->H;
+    return MCPT_OK;
+}
+
 int mcpt_film_tonemap_rgba8(mcpt_ctx* c, float exposure, uint8_t* out) {
     if (!c || !c->P || !out) return set_err(c, MCPT_E_INVALID, "bad argument");
     HIPCHK(c, hipSetDevice(c->device));

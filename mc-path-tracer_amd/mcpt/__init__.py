@@ -101,6 +101,11 @@ ABI = {
     "mcpt_device_name": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
     "mcpt_debug_queue_rays": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _u]),
     "mcpt_debug_last_stage_ms": (C.c_float, [C.c_void_p]),
+    "mcpt_film_size": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "mcpt_film_write_png": (C.c_int, [C.c_void_p, C.c_float, C.c_char_p]),
+    "mcpt_film_write_pfm": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "mcpt_image_write_png": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]),
+    "mcpt_image_write_pfm": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_float)]),
     "mcpt_debug_trace_profile": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "mcpt_scene_new": (C.c_void_p, []),
     "mcpt_scene_free": (None, [C.c_void_p]),
@@ -394,6 +399,14 @@ class PathTracer:
     def last_stage_ms(self) -> float:
         return lib().mcpt_debug_last_stage_ms(self.h)
 
+    def write_png(self, path, exposure=1.0):
+        """Tonemapped film as 8-bit RGB PNG (mcpt_film_write_png)."""
+        self._ck(lib().mcpt_film_write_png(self.h, exposure, os.fsencode(path)))
+
+    def write_pfm(self, path):
+        """Averaged radiance Ld/samples as float RGB PFM (mcpt_film_write_pfm)."""
+        self._ck(lib().mcpt_film_write_pfm(self.h, os.fsencode(path)))
+
     def trace_profile(self, reset=True):
         """k_trace loop profile (diagnostics build only): dict of summed wave-level counts."""
         v = (C.c_uint64 * 12)()
@@ -433,6 +446,24 @@ CONFIGS = {
     4: RenderConfig(4, 3840, 2160, 1024, 8, (0.0, 0.0, 2.5)),
     5: RenderConfig(5, 4096, 4096, 4096, 12, (0.0, 1.2, 3.0), pitch=-5.0),
 }
+
+
+def write_png(path, rgba8):
+    """Write an (H, W, 4) uint8 buffer as RGB PNG (mcpt_image_write_png; host-only, no GPU)."""
+    a = np.ascontiguousarray(rgba8, np.uint8)
+    h, w = a.shape[:2]
+    rc = lib().mcpt_image_write_png(os.fsencode(path), w, h, a.ctypes.data_as(C.POINTER(C.c_uint8)))
+    if rc != 0:
+        raise McptError(f"mcpt_image_write_png failed ({rc})")
+
+
+def write_pfm(path, rgb):
+    """Write an (H, W, 3) float buffer as PFM (mcpt_image_write_pfm; host-only, no GPU)."""
+    a = np.ascontiguousarray(rgb, np.float32)
+    h, w = a.shape[:2]
+    rc = lib().mcpt_image_write_pfm(os.fsencode(path), w, h, a.ctypes.data_as(C.POINTER(C.c_float)))
+    if rc != 0:
+        raise McptError(f"mcpt_image_write_pfm failed ({rc})")
 
 
 def build_config_scene(cid: int, asset_dir=ASSET_DIR) -> Scene:

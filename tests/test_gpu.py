@@ -236,3 +236,21 @@ def test_errors_are_reported(mcpt_mod):
     with pytest.raises(mcpt_mod.McptError):
         pt.trace_closest(np.zeros((1, 3), np.float32), np.ones((1, 3), np.float32))
     pt.close()
+
+
+def test_film_writers(mcpt_mod, scene_c1, tmp_path):
+    """mcpt_film_write_png / _pfm on a rendered film: PNG == tonemap RGB, PFM == Ld / samples."""
+    from test_image_io import read_pfm, read_png
+
+    rc = mcpt_mod.CONFIGS[1]
+    W, H = 64, 48
+    cam = mcpt_mod.config_camera(rc, W, H)
+    pt = make_pt(mcpt_mod, scene_c1[0], cam, W, H, 4, rc.max_depth)
+    pt.render()
+    Ld, smp = pt.film()
+    pt.write_png(tmp_path / "f.png", 1.5)
+    pt.write_pfm(tmp_path / "f.pfm")
+    assert np.array_equal(read_png(tmp_path / "f.png"), pt.tonemap(1.5)[..., :3])
+    want = np.where(smp[..., None] > 0, Ld / np.maximum(smp, 1)[..., None].astype(np.float32), 0).astype(np.float32)
+    assert np.array_equal(read_pfm(tmp_path / "f.pfm"), want)
+    pt.close()
