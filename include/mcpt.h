@@ -43,8 +43,15 @@ typedef struct mcpt_config {
     int32_t rr_depth;    /* Russian roulette when 'path_length > rr_depth' */
     int32_t tile_w;      /* film tile (Film.cu:17: 256x256) */
     int32_t tile_h;
-    int32_t flags;       /* reserved, 0 */
+    int32_t flags;       /* MCPT_FLAG_* (0 = reference mode) */
 } mcpt_config;
+
+/* Quality mode: fixes the reference quirks of Appendix A.4-A.7, A.9 and
+ * A.11 -- background added once, Russian-roulette survivors reweighted by 1/(1-q) with q from
+ * the updated throughput, light-selection pdf 1/N, MIS weight 1 for delta lights, textbook
+ * Gram-Schmidt, env sampling and pdf on matched (clamped) cells.  An alternative integrator:
+ * never compared against the reference, only against the oracle's fixed mode. */
+#define MCPT_FLAG_FIXED 1
 
 /* Scene as flat, BVH-ordered arrays (the device data model of Scene.h:24-33,
  * BVH.h:63-72, Triangle.h:11-23, dMaterial.cuh:11-33, EnvironmentLight.h:17-40). */

@@ -251,11 +251,18 @@ MCPT_HD float luminance(V3 c) {                                                 
 MCPT_HD V3 ld3(const float* p, int64_t i) { return V3{p[3 * i], p[3 * i + 1], p[3 * i + 2]}; }
 
 // jek::gram_schmidt (Vector.h:1128-1139): component-wise divide quirk kept.
+// FIXED (quality mode): the textbook projection
+// T = normalize(x - vn (x . vn)) with the normalised normal vn.
+template <bool FIXED = false>
 MCPT_HD V3 gram_schmidt(V3 v, const Rng& r, uint32_t slot0) {
     float rx = r(slot0 + 0) * 2.f + -1.f;  // rand_float(-1,1): Random.cu:39-42
     float ry = r(slot0 + 1) * 2.f + -1.f;
     float rz = r(slot0 + 2) * 2.f + -1.f;
     V3 x = v3(rx, ry, rz);
+    if (FIXED) {
+        const V3 vn = normalize(v);
+        return normalize(x - vn * dot(x, vn));
+    }
     float x_dot_v = dot(x, v);
     V3 vn = normalize(v);
     V3 vn2 = vn * vn;
@@ -361,14 +368,36 @@ MCPT_HD V3 env_L(const EnvView& e, V3 wi) {  // EnvironmentLight.cu:34-47
     spherical_map(wi, u, v);
     return tex_bilinear(e.tex, e.w, e.h, u, v);
 }
-MCPT_HD float env_pdf_uv(const EnvView& e, float u, float v);
+// FIXED (quality mode): the pdf is read from the cell the sampler draws from
+// ((int)(u W), (int)(v H), clamped) instead of the reference's (u (W-1), v (H-1))
+// cell (EnvironmentLight.cu:76), and env_dir samples cell centres with the row /
+// column index clamped to the table (the reference's off-by-one can give -1).
+template <bool FIXED = false>
+MCPT_HD float env_pdf_uv(const EnvView& e, float u, float v) {
+    int px, py;
+    if (FIXED) {
+        const float fx = u * (float)e.w, fy = v * (float)e.h;
+        px = (fx == fx && fx >= 0.f) ? (fx < (float)(e.w - 1) ? (int)fx : e.w - 1) : 0;
+        py = (fy == fy && fy >= 0.f) ? (fy < (float)(e.h - 1) ? (int)fy : e.h - 1) : 0;
+    } else {
+        const float fx = u * (float)(unsigned)(e.w - 1), fy = v * (float)(unsigned)(e.h - 1);
+        px = (fx == fx && fx >= 0.f && fx < (float)e.w) ? (int)fx : 0;
+        py = (fy == fy && fy >= 0.f && fy < (float)e.h) ? (int)fy : 0;
+    }
+    float pdf = e.pdf[(int64_t)py * e.w + px];
+    float sin_theta = dsin(PI_F * v);
+    if (sin_theta == 0.f) return 0.f;
+    return pdf * (float)((unsigned)e.w * (unsigned)e.h) / (((2.f * sin_theta) * PI_F) * PI_F);
+}
+template <bool FIXED = false>
 MCPT_HD float env_pdf(const EnvView& e, V3 wi) {  // EnvironmentLight.cu:65-85
     if (e.mode == 0 || e.tex == nullptr) return ONE_4PI_F;
     float u, v;
     spherical_map(wi, u, v);
-    return env_pdf_uv(e, u, v);
+    return env_pdf_uv<FIXED>(e, u, v);
 }
 // env_L and env_pdf of one direction sharing its spherical map (same values as the two calls)
+template <bool FIXED = false>
 MCPT_HD void env_L_pdf(const EnvView& e, V3 wi, V3& L, float& pdf) {
     if (e.mode == 0 || e.tex == nullptr) {
         L = v3(e.color[0], e.color[1], e.color[2]) * e.ls;
@@ -378,17 +407,9 @@ MCPT_HD void env_L_pdf(const EnvView& e, V3 wi, V3& L, float& pdf) {
     float u, v;
     spherical_map(wi, u, v);
     L = tex_bilinear(e.tex, e.w, e.h, u, v);
-    pdf = env_pdf_uv(e, u, v);
+    pdf = env_pdf_uv<FIXED>(e, u, v);
 }
-MCPT_HD float env_pdf_uv(const EnvView& e, float u, float v) {
-    float fx = u * (float)(unsigned)(e.w - 1), fy = v * (float)(unsigned)(e.h - 1);
-    int px = (fx == fx && fx >= 0.f && fx < (float)e.w) ? (int)fx : 0;
-    int py = (fy == fy && fy >= 0.f && fy < (float)e.h) ? (int)fy : 0;
-    float pdf = e.pdf[(int64_t)py * e.w + px];
-    float sin_theta = dsin(PI_F * v);
-    if (sin_theta == 0.f) return 0.f;
-    return pdf * (float)((unsigned)e.w * (unsigned)e.h) / (((2.f * sin_theta) * PI_F) * PI_F);
-}
+template <bool FIXED = false>
 MCPT_HD V3 env_dir(const EnvView& e, const Rng& r) {  // EnvironmentLight.cu:10-33
     if (e.mode == 0 || e.tex == nullptr) {
         float u = r(SL_ENV_U);
@@ -406,6 +427,11 @@ MCPT_HD V3 env_dir(const EnvView& e, const Rng& r) {  // EnvironmentLight.cu:10-
         y = (int)((float)upper_bound(e.marginal_y, e.h, ey) - 1.f);
         if (y < 0) y = 0;
         x = (int)((float)upper_bound(e.conds_y + (int64_t)y * e.w, e.w, ex) - 1.f);
+    }
+    if (FIXED) {
+        y = y > e.h - 1 ? e.h - 1 : y;
+        x = x < 0 ? 0 : (x > e.w - 1 ? e.w - 1 : x);
+        return spherical_direction(((float)x + 0.5f) / (float)e.w, ((float)y + 0.5f) / (float)e.h);
     }
     float u = (float)x / (float)e.w;
     float v = (float)y / (float)e.h;
@@ -446,6 +472,7 @@ MCPT_HD float g1_schlick_ggx(V3 v, V3 n, float r) {  // dMaterial.cu:205-213
     float n_dot_v = fmx(dot(n, v), BRDF_EPS);
     return n_dot_v / fmx(n_dot_v * (1.f - k) + k, BRDF_EPS);
 }
+template <bool FIXED = false>
 MCPT_HD V3 diff_get_wi(V3 N, const Rng& r, uint32_t s0) {  // dMaterial.cu:232-254
     float e0 = r(s0 + 0);
     float e1 = r(s0 + 1);
@@ -455,7 +482,7 @@ MCPT_HD V3 diff_get_wi(V3 N, const Rng& r, uint32_t s0) {  // dMaterial.cu:232-2
     dsincos(phi, sp, cp);
     float x = sinTheta * cp;
     float z = sinTheta * sp;
-    V3 T = gram_schmidt(N, r, s0 + 2);
+    V3 T = gram_schmidt<FIXED>(N, r, s0 + 2);
     V3 B = normalize(cross(N, T));
     return normalize((T * x + N * e0) + B * z);
 }
@@ -468,6 +495,7 @@ MCPT_HD V3 diff_get_f(const Mat& m, V3 n, V3 wi, V3 wo) {  // dMaterial.cu:259-2
     kD = kD * (1.f - m.metal);
     return ((kD * m.base) * n_dot_wi) * ONE_PI_F;
 }
+template <bool FIXED = false>
 MCPT_HD V3 spec_get_wi(const Mat& m, V3 N, V3 wo, const Rng& r, uint32_t s0) {  // dMaterial.cu:278-307
     float rr = m.rough;
     float a2 = ((rr * rr) * rr) * rr;
@@ -479,7 +507,7 @@ MCPT_HD V3 spec_get_wi(const Mat& m, V3 N, V3 wo, const Rng& r, uint32_t s0) {  
     dsincos(theta, st, ct);
     dsincos(phi, sp, cp);
     V3 h = v3(st * cp, ct, st * sp);
-    V3 T = gram_schmidt(N, r, s0 + 2);
+    V3 T = gram_schmidt<FIXED>(N, r, s0 + 2);
     V3 B = normalize(cross(N, T));
     V3 smp = normalize((T * h.x + N * h.y) + B * h.z);
     return normalize(reflect(-wo, smp));

@@ -67,9 +67,10 @@ __device__ inline V3 light_L(const DevScene& sc, int id, V3 wi) {
     const float* p = sc.dirs + 7 * (id - 1);  // DirectionalLight.cu:34
     return v3(p[3], p[4], p[5]) * p[6];
 }
+template <bool FIXED>
 __device__ inline void light_L_pdf(const DevScene& sc, int id, V3 wi, V3& L, float& pdf) {
     if (id == 0) {
-        env_L_pdf(sc.env, wi, L, pdf);
+        env_L_pdf<FIXED>(sc.env, wi, L, pdf);
     } else {
         const float* p = sc.dirs + 7 * (id - 1);  // DirectionalLight.cu:34, :40-43
         L = v3(p[3], p[4], p[5]) * p[6];
@@ -199,6 +200,12 @@ struct MatOut {
 
 // Light choice + wf_mat_mix for the continuing path pid (vertex len, sample
 // `samples`, throughput `beta_store` after the logic update).
+//
+// FIXED (quality mode, mcpt_config.flags & MCPT_FLAG_FIXED) changes, each
+// a reference quirk of Appendix A: light-selection pdf 1/N folded into both light pdfs
+// (A.6), delta lights get MIS weight 1 (pdf_brdf.y = 0 instead of 1, A.7), textbook
+// Gram-Schmidt (A.9), env sampling/pdf on matched, clamped cells (A.11).
+template <bool FIXED>
 __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t samples, uint32_t len, V3 beta_store) {
     const DevScene& sc = a.scene;
     MatOut mo{false, false, false, false, false, 0u};
@@ -212,7 +219,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     int l_id = (int)(r(SL_LIGHT) * (float)(sc.nlights - 0) + (float)0);
     const int light_id = (l_id == sc.nlights) ? 0 : l_id;
     V3 ldir;
-    if (light_id == 0) ldir = env_dir(sc.env, r);
+    if (light_id == 0) ldir = env_dir<FIXED>(sc.env, r);
     else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
     const V3 so_l = pos + n * 0.01f, sd_l = ldir;
     const Mat m = load_mat(sc.mats + 8 * mat);
@@ -220,8 +227,10 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     V3 f_l = brdf_f(m, n, ldir, wo);
     V3 Li_l;
     float pdfl_x;
-    light_L_pdf(sc, light_id, ldir, Li_l, pdfl_x);
-    float pdfb_y = !delta ? brdf_pdf(m, n, ldir, wo) : 1.f;
+    light_L_pdf<FIXED>(sc, light_id, ldir, Li_l, pdfl_x);
+    const float sel = FIXED ? 1.f / (float)sc.nlights : 1.f;  // light-selection pdf
+    if (FIXED) pdfl_x = pdfl_x * sel;
+    float pdfb_y = !delta ? brdf_pdf(m, n, ldir, wo) : (FIXED ? 0.f : 1.f);
     float wL = power_heuristic(pdfl_x, pdfb_y);
     V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
     uint32_t nf = 0;
@@ -229,13 +238,15 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     V3 cB = v3(0.f, 0.f, 0.f);
     V3 so_b = v3(0, 0, 0), sd_b = v3(0, 0, 0);
     if (!delta) {
-        V3 wi_b = (r(SL_MAT_LOBE) < 0.5f) ? spec_get_wi(m, n, wo, r, SL_MAT_E0) : diff_get_wi(n, r, SL_MAT_E0);
+        V3 wi_b = (r(SL_MAT_LOBE) < 0.5f) ? spec_get_wi<FIXED>(m, n, wo, r, SL_MAT_E0)
+                                           : diff_get_wi<FIXED>(n, r, SL_MAT_E0);
         so_b = pos + wi_b * 0.001f;
         sd_b = wi_b;
         V3 f_b = brdf_f(m, n, wi_b, wo);
         V3 Li_b;
         float pdfl_y;
-        light_L_pdf(sc, light_id, wi_b, Li_b, pdfl_y);
+        light_L_pdf<FIXED>(sc, light_id, wi_b, Li_b, pdfl_y);
+        if (FIXED) pdfl_y = pdfl_y * sel;
         float pdfb_x = brdf_pdf(m, n, wi_b, wo);
         float wB = power_heuristic(pdfb_x, pdfl_y);
         cB = ((f_b * Li_b) * wB) / pdfb_x;
@@ -244,7 +255,8 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
         mo.want_b = true;
         mo.vis_ray = true;
     }
-    V3 wi_s = (r(SL_CONT_LOBE) < 0.5f) ? spec_get_wi(m, n, wo, r, SL_CONT_E0) : diff_get_wi(n, r, SL_CONT_E0);
+    V3 wi_s = (r(SL_CONT_LOBE) < 0.5f) ? spec_get_wi<FIXED>(m, n, wo, r, SL_CONT_E0)
+                                        : diff_get_wi<FIXED>(n, r, SL_CONT_E0);
     float pdf_s = brdf_pdf(m, n, wi_s, wo);
     V3 f_s = brdf_f(m, n, wi_s, wo);
     if ((f_s.x == 0.f && f_s.y == 0.f && f_s.z == 0.f) || pdf_s == 0.f) nf |= F_FZERO;
@@ -289,6 +301,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
 #else
 #define MCPT_SHADE_ATTR
 #endif
+template <bool FIXED>
 __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     __shared__ uint32_t s_pid[kBlock];      // pid | len << 24 of the block's continuing paths
     __shared__ uint32_t s_samples[kBlock];
@@ -334,7 +347,8 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
                     film = film + v3(0.f, 0.f, 0.f) * B;
                 } else {
                     float4 rd = a.p.ray_d[pid];
-                    for (int i = 0; i < sc.nlights; i++) film = film + env_L(sc.env, xyz(rd)) * B;
+                    const int nbg = FIXED ? 1 : sc.nlights;  // reference adds it once per light (A.4)
+                    for (int i = 0; i < nbg; i++) film = film + env_L(sc.env, xyz(rd)) * B;
                 }
             }
             if (len > (uint32_t)a.max_depth || !found) terminate = true;  // :142-146
@@ -355,8 +369,14 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
                 } else {
                     beta_store = B * v3(b4.w, n0.w, n1.w);  // paths->beta *= f_sample / pdf_sample (:187)
                     if (len > (uint32_t)a.rr_depth) {        // :189-196
-                        float q = fmx(0.05f, 1.f - B.y);
-                        if (r(SL_RR) < q) terminate = true;
+                        if (FIXED) {  // q from the updated throughput, survivors reweighted (A.5)
+                            float q = fmx(0.05f, 1.f - beta_store.y);
+                            if (r(SL_RR) < q) terminate = true;
+                            else beta_store = beta_store / (1.f - q);
+                        } else {
+                            float q = fmx(0.05f, 1.f - B.y);
+                            if (r(SL_RR) < q) terminate = true;
+                        }
                     }
                 }
             }
@@ -417,7 +437,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         if (threadIdx.x < ncont) {
             const uint32_t e = s_pid[threadIdx.x];
             mpid = e & 0xffffffu;
-            mo = material(a, mpid, s_samples[threadIdx.x], e >> 24,
+            mo = material<FIXED>(a, mpid, s_samples[threadIdx.x], e >> 24,
                           v3(s_beta[0][threadIdx.x], s_beta[1][threadIdx.x], s_beta[2][threadIdx.x]));
         }
         // ---- phase 3: queue pushes (one atomic per block and queue)
@@ -829,8 +849,9 @@ __global__ void k_pack(PackArgs a) {  // tile-set pixels -> packed 16 B/px (for 
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s) {
-    hipLaunchKernelGGL(k_shade, dim3(nblocks), dim3(kBlock), 0, s, a);
+void launch_shade(const ShadeArgs& a, int nblocks, bool fixed_mode, hipStream_t s) {
+    if (fixed_mode) hipLaunchKernelGGL(k_shade<true>, dim3(nblocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_shade<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
 }
 // Persistent grid: resident waves per CU from the occupancy calculator
 // (MCPT_TRACE_WAVES overrides), rounded to a multiple of the shard count.

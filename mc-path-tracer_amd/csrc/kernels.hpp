@@ -112,7 +112,7 @@ struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n; }
 struct TonemapArgs { const float4* Ld; const uint32_t* samples; uchar4* out; float exposure; uint32_t n; };
 struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* out; };
 
-void launch_shade(const ShadeArgs& a, int nblocks, hipStream_t s);
+void launch_shade(const ShadeArgs& a, int nblocks, bool fixed_mode, hipStream_t s);
 void launch_trace(const TraceArgs& a, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
 int trace_profile(unsigned long long* out, int reset);

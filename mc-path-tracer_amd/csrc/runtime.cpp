@@ -438,7 +438,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     sa.cnt = c->cnt;
     int bpt = (int)((c->tile_w * c->tile_h + kBlock - 1) / kBlock);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 0), c->stream));
-    if (sa.ntiles > 0) launch_shade(sa, sa.ntiles * bpt, c->stream);
+    if (sa.ntiles > 0) launch_shade(sa, sa.ntiles * bpt, (c->cfg.flags & MCPT_FLAG_FIXED) != 0, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 1), c->stream));
     // extension (closest hit) and any-hit rays in one persistent launch
     TraceArgs ta{};

@@ -154,8 +154,11 @@ def fptr(a: np.ndarray):
     return a.ctypes.data_as(_f)
 
 
-def default_config(spp=16, max_depth=5, rr_depth=3, seed=0x5EED2026, tile=256) -> Config:
-    return Config(seed, spp, max_depth, rr_depth, tile, tile, 0)
+FLAG_FIXED = 1  # MCPT_FLAG_FIXED: quality-mode integrator
+
+
+def default_config(spp=16, max_depth=5, rr_depth=3, seed=0x5EED2026, tile=256, fixed=False) -> Config:
+    return Config(seed, spp, max_depth, rr_depth, tile, tile, FLAG_FIXED if fixed else 0)
 
 
 def make_camera(position, yaw_deg=-90.0, pitch_deg=0.0, fovy_deg=45.0, aspect=1.0, znear=0.01, zfar=1e4,

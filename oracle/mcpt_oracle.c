@@ -269,12 +269,17 @@ static float luminance(v3 c) {
     return (float)(0.299 * (double)c.x + 0.587 * (double)c.y + 0.114 * (double)c.z);
 }
 
-/* gram_schmidt (cuda_math/Vector.h:1128-1139): component-wise division quirk. */
-static v3 gram_schmidt(v3 v, const rng_t *r, uint32_t slot0) {
+/* gram_schmidt (cuda_math/Vector.h:1128-1139): component-wise division quirk.
+ * fixed mode: textbook projection normalize(x - vn (x . vn)). */
+static v3 gram_schmidt(v3 v, const rng_t *r, uint32_t slot0, int fixed) {
     float rx = rnd(r, slot0 + 0) * 2.f + -1.f; /* rand_float(-1,1): Random.cu:39-42 */
     float ry = rnd(r, slot0 + 1) * 2.f + -1.f;
     float rz = rnd(r, slot0 + 2) * 2.f + -1.f;
     v3 x = V(rx, ry, rz);
+    if (fixed) {
+        v3 vn = normalize3(v);
+        return normalize3(vsub(x, vscale(vn, dot3(x, vn))));
+    }
     float x_dot_v = dot3(x, v);
     v3 v_norm = normalize3(v);
     v3 v_norm_2 = vmul(v_norm, v_norm);
@@ -349,20 +354,27 @@ static v3 env_L(const or_scene *sc, v3 wi) {                    /* EnvironmentLi
     spherical_map(wi, &u, &v);
     return tex_bilinear(sc->env_tex, sc->env_w, sc->env_h, u, v);
 }
-static float env_pdf(const or_scene *sc, v3 wi) {               /* EnvironmentLight.cu:65-85 */
+static float env_pdf(const or_scene *sc, v3 wi, int fixed) {    /* EnvironmentLight.cu:65-85 */
     if (sc->env_mode == 0 || sc->env_tex == NULL) return ONE_4PI_F;
     float u, v;
     spherical_map(wi, &u, &v);
     int W = sc->env_w, H = sc->env_h;
-    float fx = u * (float)(unsigned)(W - 1), fy = v * (float)(unsigned)(H - 1);
-    int px = (fx == fx && fx >= 0.f && fx < (float)W) ? (int)fx : 0; /* NaN -> 0 (DEVIATION) */
-    int py = (fy == fy && fy >= 0.f && fy < (float)H) ? (int)fy : 0;
+    int px, py;
+    if (fixed) { /* the sampled cell (int)(u W), (int)(v H), clamped */
+        float fx = u * (float)W, fy = v * (float)H;
+        px = (fx == fx && fx >= 0.f) ? (fx < (float)(W - 1) ? (int)fx : W - 1) : 0;
+        py = (fy == fy && fy >= 0.f) ? (fy < (float)(H - 1) ? (int)fy : H - 1) : 0;
+    } else {
+        float fx = u * (float)(unsigned)(W - 1), fy = v * (float)(unsigned)(H - 1);
+        px = (fx == fx && fx >= 0.f && fx < (float)W) ? (int)fx : 0; /* NaN -> 0 (DEVIATION) */
+        py = (fy == fy && fy >= 0.f && fy < (float)H) ? (int)fy : 0;
+    }
     float pdf = sc->env_pdf[(int64_t)py * W + px];
     float sin_theta = or_sinf(PI_F * v);
     if (sin_theta == 0.f) return 0.f;
     return pdf * (float)((unsigned)W * (unsigned)H) / (((2.f * sin_theta) * PI_F) * PI_F);
 }
-static v3 env_dir(const or_scene *sc, const rng_t *r) {         /* EnvironmentLight.cu:10-33 */
+static v3 env_dir(const or_scene *sc, const rng_t *r, int fixed) { /* EnvironmentLight.cu:10-33 */
     if (sc->env_mode == 0 || sc->env_tex == NULL) {
         float u = rnd(r, SL_ENV_U);
         float v = rnd(r, SL_ENV_V);
@@ -374,6 +386,11 @@ static v3 env_dir(const or_scene *sc, const rng_t *r) {         /* EnvironmentLi
     int y = (int)((float)or_upper_bound(sc->env_marginal_y, H, ey) - 1.f);
     if (y < 0) y = 0; /* unreachable: marginal_y[0] == 0; reference reads row -1 */
     int x = (int)((float)or_upper_bound(sc->env_conds_y + (int64_t)y * W, W, ex) - 1.f);
+    if (fixed) { /* clamped indices, cell centres */
+        y = y > H - 1 ? H - 1 : y;
+        x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
+        return spherical_direction(((float)x + 0.5f) / (float)W, ((float)y + 0.5f) / (float)H);
+    }
     float u = (float)x / (float)W;
     float v = (float)y / (float)H;
     return spherical_direction(u, v);
@@ -386,10 +403,10 @@ void or_env_dir(const or_scene *sc, float ex, float ey, float *wi) {
     v3 d = spherical_direction((float)x / (float)W, (float)y / (float)H);
     wi[0] = d.x; wi[1] = d.y; wi[2] = d.z;
 }
-float or_env_pdf(const or_scene *sc, float dx, float dy, float dz) { return env_pdf(sc, V(dx, dy, dz)); }
+float or_env_pdf(const or_scene *sc, float dx, float dy, float dz) { return env_pdf(sc, V(dx, dy, dz), 0); }
 
-static void light_dir(const or_scene *sc, int id, const rng_t *r, v3 *wi) {
-    if (id == 0) *wi = env_dir(sc, r);
+static void light_dir(const or_scene *sc, int id, const rng_t *r, v3 *wi, int fixed) {
+    if (id == 0) *wi = env_dir(sc, r, fixed);
     else *wi = ld3(sc->dir_params + 7 * (id - 1), 0);           /* DirectionalLight.cu:8-11 */
 }
 static v3 light_L(const or_scene *sc, int id, v3 wi) {
@@ -397,8 +414,8 @@ static v3 light_L(const or_scene *sc, int id, v3 wi) {
     const float *p = sc->dir_params + 7 * (id - 1);             /* DirectionalLight.cu:34 */
     return vscale(V(p[3], p[4], p[5]), p[6]);
 }
-static float light_pdf(const or_scene *sc, int id, v3 wi) {
-    if (id == 0) return env_pdf(sc, wi);
+static float light_pdf(const or_scene *sc, int id, v3 wi, int fixed) {
+    if (id == 0) return env_pdf(sc, wi, fixed);
     return 1.f;                                                 /* DirectionalLight.cu:40-43 */
 }
 
@@ -488,14 +505,14 @@ static float g1_schlick_ggx(v3 v, v3 n, float r) {              /* :205-213 */
     float n_dot_v = fmx(dot3(n, v), BRDF_EPS);
     return n_dot_v / fmx(n_dot_v * (1.f - k) + k, BRDF_EPS);
 }
-static v3 diff_get_wi(v3 N, const rng_t *r, uint32_t s0) {       /* :232-254 */
+static v3 diff_get_wi(v3 N, const rng_t *r, uint32_t s0, int fixed) {       /* :232-254 */
     float e0 = rnd(r, s0 + 0);
     float e1 = rnd(r, s0 + 1);
     float sinTheta = sqrtf(1.f - e0 * e0);
     float phi = (2.f * PI_F) * e1;
     float x = sinTheta * or_cosf(phi);
     float z = sinTheta * or_sinf(phi);
-    v3 T = gram_schmidt(N, r, s0 + 2);
+    v3 T = gram_schmidt(N, r, s0 + 2, fixed);
     v3 B = normalize3(cross3(N, T));
     return normalize3(vadd(vadd(vscale(T, x), vscale(N, e0)), vscale(B, z)));
 }
@@ -508,7 +525,7 @@ static v3 diff_get_f(const mat_t *m, v3 n, v3 wi, v3 wo) {      /* :259-276 */
     kD = vscale(kD, 1.f - m->metal);
     return vscale(vscale(vmul(kD, m->base), n_dot_wi), ONE_PI_F);
 }
-static v3 spec_get_wi(const mat_t *m, v3 N, v3 wo, const rng_t *r, uint32_t s0) { /* :278-307 */
+static v3 spec_get_wi(const mat_t *m, v3 N, v3 wo, const rng_t *r, uint32_t s0, int fixed) { /* :278-307 */
     float rr = m->rough;
     float a2 = ((rr * rr) * rr) * rr;
     float e0 = rnd(r, s0 + 0);
@@ -517,7 +534,7 @@ static v3 spec_get_wi(const mat_t *m, v3 N, v3 wo, const rng_t *r, uint32_t s0) 
     float phi = TWO_PI_F * e1;
     float st = or_sinf(theta);
     v3 h = V(st * or_cosf(phi), or_cosf(theta), st * or_sinf(phi));
-    v3 T = gram_schmidt(N, r, s0 + 2);
+    v3 T = gram_schmidt(N, r, s0 + 2, fixed);
     v3 B = normalize3(cross3(N, T));
     v3 smp = normalize3(vadd(vadd(vscale(T, h.x), vscale(N, h.y)), vscale(B, h.z)));
     return normalize3(reflect3(vneg(wo), smp));
@@ -850,7 +867,8 @@ static void wf_logic(ctx_t *c, queues_t *q, int x, int y) {
             Ld[0] = Ld[0] + z.x; Ld[1] = Ld[1] + z.y; Ld[2] = Ld[2] + z.z;
         }
         if (len == 1 && !p->isect.was_found) {                 /* :134-139 */
-            for (int i = 0; i < nmb_lights; i++) {
+            int nbg = c->cfg->fixed ? 1 : nmb_lights;           /* fixed: background once */
+            for (int i = 0; i < nbg; i++) {
                 v3 Le = vmul(env_L(sc, p->ray.d), beta);
                 Ld[0] = Ld[0] + Le.x; Ld[1] = Ld[1] + Le.y; Ld[2] = Ld[2] + Le.z;
             }
@@ -873,9 +891,15 @@ static void wf_logic(ctx_t *c, queues_t *q, int x, int y) {
             }
             p->beta = vmul(p->beta, vdivs(p->f_sample, p->pdf_sample));
             if (len > (uint32_t)c->cfg->rr_depth) {
-                float qq = fmx(0.05f, 1.f - beta.y);
-                if (rnd(&r, SL_RR) < qq) { terminate = 1; goto TERMINATE; }
-                /* beta /= 1-q applies to a local and is never stored (:195) */
+                if (c->cfg->fixed) { /* fixed: q from the updated throughput, survivors reweighted */
+                    float qq = fmx(0.05f, 1.f - p->beta.y);
+                    if (rnd(&r, SL_RR) < qq) { terminate = 1; goto TERMINATE; }
+                    p->beta = vdivs(p->beta, 1.f - qq);
+                } else {
+                    float qq = fmx(0.05f, 1.f - beta.y);
+                    if (rnd(&r, SL_RR) < qq) { terminate = 1; goto TERMINATE; }
+                    /* beta /= 1-q applies to a local and is never stored (:195) */
+                }
             }
         }
 TERMINATE:
@@ -886,7 +910,7 @@ TERMINATE:
             int l_id = (int)(rnd(&r, SL_LIGHT) * (float)(nmb_lights - 0) + (float)0); /* rand_int :48-51 */
             p->light_id = (uint32_t)((l_id == nmb_lights) ? 0 : l_id);
             v3 ldir;
-            light_dir(sc, (int)p->light_id, &r, &ldir);
+            light_dir(sc, (int)p->light_id, &r, &ldir, c->cfg->fixed);
             p->ray_light.o = vadd(p->isect.position, vscale(p->isect.normal, 0.01f));
             p->ray_light.d = ldir;
             q->matq[q->nmat++] = (int32_t)pid;
@@ -946,11 +970,15 @@ static void wf_mat_mix(ctx_t *c, queues_t *q, uint32_t id) {
 
     f_light = vadd(spec_get_f(&m, n, light_wi, wo), diff_get_f(&m, n, light_wi, wo)); /* :326 */
     Li_light = light_L(sc, light_id, light_wi);
-    pdf_light[0] = light_pdf(sc, light_id, light_wi);
-    pdf_brdf[1] = !delta ? (diff_get_pdf() + spec_get_pdf(&m, n, light_wi, wo)) * 0.5f : 1.f;
+    int fixed = c->cfg->fixed;
+    float sel = fixed ? 1.f / (float)(1 + sc->ndir) : 1.f;   /* fixed: light-selection pdf 1/N */
+    pdf_light[0] = light_pdf(sc, light_id, light_wi, fixed);
+    if (fixed) pdf_light[0] = pdf_light[0] * sel;
+    pdf_brdf[1] = !delta ? (diff_get_pdf() + spec_get_pdf(&m, n, light_wi, wo)) * 0.5f
+                         : (fixed ? 0.f : 1.f);               /* fixed: delta-light MIS weight 1 */
     if (!delta) {                                              /* :332-345 */
-        v3 wi_brdf = (rnd(&r, SL_MAT_LOBE) < 0.5f) ? spec_get_wi(&m, n, wo, &r, SL_MAT_E0)
-                                                   : diff_get_wi(n, &r, SL_MAT_E0);
+        v3 wi_brdf = (rnd(&r, SL_MAT_LOBE) < 0.5f) ? spec_get_wi(&m, n, wo, &r, SL_MAT_E0, fixed)
+                                                   : diff_get_wi(n, &r, SL_MAT_E0, fixed);
         ray_t vis;
         vis.o = vadd(is->position, vscale(wi_brdf, 0.001f));
         vis.d = wi_brdf;
@@ -963,11 +991,12 @@ static void wf_mat_mix(ctx_t *c, queues_t *q, uint32_t id) {
             f_brdf = vadd(spec_get_f(&m, n, wi_brdf, wo), diff_get_f(&m, n, wi_brdf, wo));
             Li_brdf = light_L(sc, light_id, wi_brdf);
             pdf_brdf[0] = (diff_get_pdf() + spec_get_pdf(&m, n, wi_brdf, wo)) * 0.5f;
-            pdf_light[1] = light_pdf(sc, light_id, wi_brdf);
+            pdf_light[1] = light_pdf(sc, light_id, wi_brdf, fixed);
+            if (fixed) pdf_light[1] = pdf_light[1] * sel;
         }
     }
-    v3 wi_s = (rnd(&r, SL_CONT_LOBE) < 0.5f) ? spec_get_wi(&m, n, wo, &r, SL_CONT_E0)  /* :353 */
-                                             : diff_get_wi(n, &r, SL_CONT_E0);
+    v3 wi_s = (rnd(&r, SL_CONT_LOBE) < 0.5f) ? spec_get_wi(&m, n, wo, &r, SL_CONT_E0, fixed)  /* :353 */
+                                             : diff_get_wi(n, &r, SL_CONT_E0, fixed);
     float pdf_s = (diff_get_pdf() + spec_get_pdf(&m, n, wi_s, wo)) * 0.5f;
     v3 f_s = vadd(spec_get_f(&m, n, wi_s, wo), diff_get_f(&m, n, wi_s, wo));
     p->Li_light = Li_light; p->Li_brdf = Li_brdf;

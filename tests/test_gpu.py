@@ -254,3 +254,45 @@ def test_film_writers(mcpt_mod, scene_c1, tmp_path):
     want = np.where(smp[..., None] > 0, Ld / np.maximum(smp, 1)[..., None].astype(np.float32), 0).astype(np.float32)
     assert np.array_equal(read_pfm(tmp_path / "f.pfm"), want)
     pt.close()
+
+
+@pytest.mark.parametrize("which", ["scene_c1", "scene_c2"])
+def test_fixed_mode_parity(request, mcpt_mod, oracle, which):
+    """Quality mode (MCPT_FLAG_FIXED) on the GPU against the oracle's fixed mode, with Russian
+    roulette active (depth 5 > rr_depth 3)."""
+    s, a = request.getfixturevalue(which)
+    rc = mcpt_mod.CONFIGS[1 if which == "scene_c1" else 2]
+    W, H = 96, 64
+    cam = mcpt_mod.config_camera(rc, W, H)
+    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=3, max_depth=5, fixed=True))
+    pt.upload_scene(s)
+    pt.set_camera(cam)
+    pt.resize(W, H)
+    pt.render()
+    Ld, smp = pt.film()
+    rL, rs, _ = oracle.render(a, cam, W, H, 3, 5, fixed=True)
+    assert np.array_equal(smp, rs)
+    ok, nbad = film_close(Ld, rL)
+    assert ok, f"{nbad} radiance values differ"
+    pt.close()
+
+
+def test_fixed_mode_delta_light_parity(mcpt_mod, oracle):
+    """Fixed mode with a directional (delta) light: selection pdf 1/2 and MIS weight 1."""
+    from test_fixed_mode import cube_scene
+
+    s = cube_scene(mcpt_mod, with_dir_light=True)
+    a = s.arrays()
+    cam = mcpt_mod.make_camera((0.5, 0.7, 3.0))
+    W = H = 48
+    for fixed in (False, True):
+        pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=4, max_depth=5, fixed=fixed))
+        pt.upload_scene(s)
+        pt.set_camera(cam)
+        pt.resize(W, H)
+        pt.render()
+        Ld, smp = pt.film()
+        rL, rs, _ = oracle.render(a, cam, W, H, 4, 5, fixed=fixed)
+        assert np.array_equal(smp, rs)
+        assert film_close(Ld, rL)[0]
+        pt.close()
