@@ -133,6 +133,11 @@ int mcpt_create(int device, const mcpt_config *cfg, mcpt_ctx **out);
 void mcpt_destroy(mcpt_ctx *ctx);
 const char *mcpt_last_error(const mcpt_ctx *ctx);   /* ctx may be NULL: last global error */
 int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_scene_desc *desc);
+/* Same scene with the BVH built on the GPU (linear BVH: Morton codes + Karras radix tree,
+ * one triangle per leaf) instead of taken from desc (its BVH arrays are
+ * ignored and may be empty).  Hits and films are identical to mcpt_scene_upload's: the
+ * traversal's result does not depend on the tree. */
+int mcpt_scene_upload_gpu_bvh(mcpt_ctx *ctx, const mcpt_scene_desc *desc);
 int mcpt_camera_set(mcpt_ctx *ctx, const mcpt_camera *cam);
 int mcpt_film_resize(mcpt_ctx *ctx, uint32_t w, uint32_t h, uint32_t tile_w, uint32_t tile_h);
 int mcpt_film_clear(mcpt_ctx *ctx);                                          /* == clear_dfilm */
@@ -158,6 +163,7 @@ int mcpt_device_name(mcpt_ctx *ctx, char *buf, int32_t len);
  * device time of the last mcpt_stage_run kernel. */
 int mcpt_debug_queue_rays(mcpt_ctx *ctx, int which, float *ray_o, float *ray_d, uint32_t *n_inout);
 float mcpt_debug_last_stage_ms(const mcpt_ctx *ctx);
+float mcpt_debug_last_build_ms(const mcpt_ctx *ctx);  /* device time of the last GPU BVH build */
 /* k_trace loop profile (diagnostics builds with -DMCPT_TRACE_PROF; returns 0 and zeros otherwise):
  * out12 = {loop trips, refills, node lane-steps, triangle phases, triangle lane-steps, trips with a finish,
  * idle lane-trips, trips with a pop, popping lanes, trips with a non-finite-direction slab, finishing lanes, -}

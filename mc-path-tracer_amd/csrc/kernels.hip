@@ -554,6 +554,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     uint32_t rid = 0, qi = 0;
     V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
     int nx = 0, ny = 0, nz = 0, ref = kEnd, leaf = kEnd, sp = 0, tri = -1;
+    int tri_key = 0x7fffffff;  // tie-break key of the best hit: its index in the uploaded scene
     bool fin = true;  // inverse direction finite: pair_slab() is exact
     float best = K_HUGE, cut = K_HUGE;
 #ifndef MCPT_X_NOSPILL
@@ -621,6 +622,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     rn = 0;
                     rt = 0;
                     tri = -1;
+                    tri_key = 0x7fffffff;
                     best = K_HUGE;
                     cut = best + best * kCullRel;
                     sp = 0;
@@ -729,9 +731,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     !(t < 0.f)) {
                     if (kind) {
                         if (t < K_HUGE) { tri = id; done = true; }  // occluded (tmax 1e32)
-                    } else if (t < best || (t == best && id < tri)) {
+                    } else if (t < best || (t == best && __float_as_int(w2.y) < tri_key)) {
+                        // exact-t ties go to the lower scene index (tri record .y of the
+                        // third float4), whatever order the BVH build stored triangles in
                         best = t;
                         tri = id;
+                        tri_key = __float_as_int(w2.y);
                         cut = best + best * kCullRel;
                     }
                 }
@@ -764,8 +769,10 @@ __global__ void k_hit_record(HitRecordArgs a) {  // stage_run(EXTEND) outputs
     if (tri < 0) {
         a.hit_p[i] = make_float4(0.f, 0.f, 0.f, K_HUGE);
         a.hit_n[i] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+        a.scene_tri[i] = -1;
         return;
     }
+    a.scene_tri[i] = __float_as_int(a.scene.tri[3 * tri + 2].y);  // storage position -> scene index
     V3 pos, nrm;
     int mat;
     float t;

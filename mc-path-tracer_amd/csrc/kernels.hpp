@@ -107,7 +107,7 @@ struct TraceArgs {
     uint32_t tri_min;           // run the triangle phase when this many lanes hold a leaf (set by launch_trace)
 };
 
-struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; uint32_t n; };
+struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; int32_t* scene_tri; uint32_t n; };
 struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n; };
 struct TonemapArgs { const float4* Ld; const uint32_t* samples; uchar4* out; float exposure; uint32_t n; };
 struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* out; };
@@ -115,6 +115,16 @@ struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; 
 void launch_shade(const ShadeArgs& a, int nblocks, bool fixed_mode, hipStream_t s);
 void launch_trace(const TraceArgs& a, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
+
+// GPU linear BVH (bvh_build.hip).  Inputs: host vertex arrays (3 floats per
+// triangle each) and the device triangle / shading records in scene order.
+struct LbvhInput { int ntri; const float *v0, *v1, *v2; const float4 *d_tri, *d_sh; };
+struct LbvhOutput {
+    float4 *nodes = nullptr, *tri = nullptr, *tri_sh = nullptr;  // hipMalloc'ed, owned by the caller
+    int nnodes = 0, root_ref = 0, depth = 0;
+    float root_mn[3], root_mx[3];
+};
+int build_lbvh(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
 int trace_profile(unsigned long long* out, int reset);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);

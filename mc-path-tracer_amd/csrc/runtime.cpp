@@ -57,6 +57,7 @@ struct mcpt_ctx {
     // stage_run scratch
     std::vector<void*> tmp_bufs;
     float last_stage_ms = 0.f;
+    float last_build_ms = 0.f;  // last GPU BVH build (mcpt_scene_upload_gpu_bvh)
 };
 
 static int set_err(mcpt_ctx* c, int rc, const std::string& msg) {
@@ -155,11 +156,12 @@ int mcpt_device_name(mcpt_ctx* c, char* buf, int32_t len) {
 
 // Scene upload: LinearBVHNode (BVH.h:63-72) -> child-pair nodes, dTriangle
 // (Triangle.h:11-23, 288 B) -> 48-B intersection + 48-B shading records.
-int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) {
+static hipEvent_t ev(mcpt_ctx* c, size_t i);
+static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     if (!c || !d) return set_err(c, MCPT_E_INVALID, "null argument");
     if (d->ntri < 0 || d->nnodes < 0 || d->nmat < 0 || d->ndir < 0) return set_err(c, MCPT_E_INVALID, "negative sizes");
     if (d->ntri >= (1 << 24)) return set_err(c, MCPT_E_INVALID, "more than 2^24 triangles");
-    if (d->ntri > 0 && d->nnodes == 0) return set_err(c, MCPT_E_INVALID, "triangles without BVH");
+    if (d->ntri > 0 && d->nnodes == 0 && !gpu_bvh) return set_err(c, MCPT_E_INVALID, "triangles without BVH");
     for (int32_t i = 0; i < d->ntri; i++)
         if (d->mat[i] < 0 || d->mat[i] >= d->nmat) return set_err(c, MCPT_E_INVALID, "material id out of range");
     if (d->env_mode == 1 && (!d->env_tex || !d->env_marginal_y || !d->env_conds_y || !d->env_pdf || d->env_w < 2 || d->env_h < 2))
@@ -168,7 +170,7 @@ int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     free_list(c->scene_bufs);
     c->has_scene = false;
-    const int N = d->nnodes;
+    const int N = gpu_bvh ? 0 : d->nnodes;  // gpu_bvh: the desc's BVH arrays are ignored
     // pair-node numbering of interior nodes + validation
     std::vector<int> pair_of(N, -1);
     int npair = 0;
@@ -222,7 +224,9 @@ int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) {
         mcpt::V3 e1 = p1 - p0, e2 = p2 - p0;  // Triangle.cu:13-14
         tri[3 * i + 0] = make_float4(p0.x, p0.y, p0.z, e1.x);
         tri[3 * i + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
-        tri[3 * i + 2] = make_float4(e2.z, 0.f, 0.f, 0.f);
+        float fi;
+        memcpy(&fi, &i, 4);  // scene index: the traversal's tie-break key and the API's triangle id
+        tri[3 * i + 2] = make_float4(e2.z, fi, 0.f, 0.f);
         mcpt::V3 n0 = mcpt::ld3(d->n0, i), n1 = mcpt::ld3(d->n1, i), n2 = mcpt::ld3(d->n2, i);
         float fm;
         int mm = d->mat[i];
@@ -238,11 +242,32 @@ int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) {
     if ((rc = dupload(c, c->scene_bufs, &dn, pn.data(), pn.size()))) return rc;
     if ((rc = dupload(c, c->scene_bufs, &dt, tri.data(), tri.size()))) return rc;
     if ((rc = dupload(c, c->scene_bufs, &dsh, sh.data(), sh.size()))) return rc;
+    LbvhOutput lb;
+    c->last_build_ms = 0.f;
+    if (gpu_bvh && d->ntri > 0) {
+        HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
+        LbvhInput li{d->ntri, d->v0, d->v1, d->v2, dt, dsh};
+        const int brc = build_lbvh(li, lb, c->stream);
+        for (void* q : {(void*)lb.nodes, (void*)lb.tri, (void*)lb.tri_sh})
+            if (q) c->scene_bufs.push_back(q);
+        if (brc) return set_err(c, MCPT_E_HIP, "GPU BVH build failed (" + std::to_string(brc) + ")");
+        HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
+        HIPCHK(c, hipEventSynchronize(c->events[1]));
+        HIPCHK(c, hipEventElapsedTime(&c->last_build_ms, c->events[0], c->events[1]));
+        if (lb.depth > kMaxStack) return set_err(c, MCPT_E_INVALID, "GPU BVH deeper than the 64-entry traversal stack");
+        dn = lb.nodes;
+        dt = lb.tri;
+        dsh = lb.tri_sh;
+        c->pair_depth = lb.depth;
+    }
     if ((rc = dupload(c, c->scene_bufs, &dm, d->mat_params, (size_t)d->nmat * 8))) return rc;
     if ((rc = dupload(c, c->scene_bufs, &dd, d->dir_params, (size_t)d->ndir * 7))) return rc;
     s.nodes = dn; s.tri = dt; s.tri_sh = dsh; s.mats = dm; s.dirs = dd;
     s.nlights = 1 + d->ndir;
-    if (N > 0) {
+    if (gpu_bvh && d->ntri > 0) {
+        for (int k = 0; k < 3; k++) { s.root_mn[k] = lb.root_mn[k]; s.root_mx[k] = lb.root_mx[k]; }
+        s.root_ref = lb.root_ref;
+    } else if (N > 0) {
         for (int k = 0; k < 3; k++) { s.root_mn[k] = d->bmin[k]; s.root_mx[k] = d->bmax[k]; }
         s.root_ref = ref_of(0);
     } else {
@@ -296,6 +321,10 @@ int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) {
     c->has_scene = true;
     return MCPT_OK;
 }
+
+int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) { return scene_upload(c, d, false); }
+int mcpt_scene_upload_gpu_bvh(mcpt_ctx* c, const mcpt_scene_desc* d) { return scene_upload(c, d, true); }
+float mcpt_debug_last_build_ms(const mcpt_ctx* c) { return c ? c->last_build_ms : -1.f; }
 
 int mcpt_camera_set(mcpt_ctx* c, const mcpt_camera* cam) {
     if (!c || !cam) return set_err(c, MCPT_E_INVALID, "null argument");
@@ -603,7 +632,7 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
     launch_trace(ta, c->stream);
     HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
     if (stage == MCPT_STAGE_EXTEND) {
-        HitRecordArgs ha{c->scene, dro, drd, ht, hp, hn, n};
+        HitRecordArgs ha{c->scene, dro, drd, ht, hp, hn, ht, n};  // ht: positions in, scene indices out
         launch_hit_record(ha, c->stream);
     }
     HIPCHK(c, hipGetLastError());

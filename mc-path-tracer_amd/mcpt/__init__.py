@@ -101,6 +101,8 @@ ABI = {
     "mcpt_device_name": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
     "mcpt_debug_queue_rays": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _u]),
     "mcpt_debug_last_stage_ms": (C.c_float, [C.c_void_p]),
+    "mcpt_debug_last_build_ms": (C.c_float, [C.c_void_p]),
+    "mcpt_scene_upload_gpu_bvh": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mcpt_film_size": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "mcpt_film_write_png": (C.c_int, [C.c_void_p, C.c_float, C.c_char_p]),
     "mcpt_film_write_pfm": (C.c_int, [C.c_void_p, C.c_char_p]),
@@ -324,9 +326,16 @@ class PathTracer:
         self._ck(lib().mcpt_device_name(self.h, buf, 256))
         return buf.value.decode()
 
-    def upload_scene(self, scene):
+    def upload_scene(self, scene, gpu_bvh=False):
+        """mcpt_scene_upload (host BVH from the scene), or with gpu_bvh=True
+        mcpt_scene_upload_gpu_bvh (linear BVH built on the device; same hits)."""
         d = scene.desc() if isinstance(scene, Scene) else scene
-        self._ck(lib().mcpt_scene_upload(self.h, C.byref(d)))
+        fn = lib().mcpt_scene_upload_gpu_bvh if gpu_bvh else lib().mcpt_scene_upload
+        self._ck(fn(self.h, C.byref(d)))
+
+    @property
+    def last_build_ms(self) -> float:
+        return lib().mcpt_debug_last_build_ms(self.h)
 
     def set_camera(self, cam: Camera):
         self._ck(lib().mcpt_camera_set(self.h, C.byref(cam)))

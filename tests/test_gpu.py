@@ -296,3 +296,42 @@ def test_fixed_mode_delta_light_parity(mcpt_mod, oracle):
         assert np.array_equal(smp, rs)
         assert film_close(Ld, rL)[0]
         pt.close()
+
+
+@pytest.mark.parametrize("which", ["scene_c1", "scene_c2", "scene_cube", "scene_c3"])
+def test_gpu_bvh_same_hits(request, mcpt_mod, oracle, which):
+    """GPU-built linear BVH (mcpt_scene_upload_gpu_bvh): hits bit-identical to the oracle, which
+    traverses the host SAH tree -- the traversal's result does not depend on the tree."""
+    s, a = request.getfixturevalue(which)
+    pt = mcpt_mod.PathTracer(0)
+    pt.upload_scene(s, gpu_bvh=True)
+    assert pt.last_build_ms > 0
+    n = 20000 if which == "scene_c3" else 100000
+    ro, rd = random_rays(n, 31, box=2.5)
+    if which == "scene_c3":
+        ro[:, 1] += 1.0
+    ro[:4] = [[0, 0, 5], [0, 0, 5], [0, 0, 5], [0, 0, 1]]
+    rd[:4] = [[np.nan, 0, -1], [0, 0, 0], [0, 0, -1], [1, 0, 0]]
+    gp, gn, gt = pt.trace_closest(ro, rd)
+    op_, on, ot = oracle.trace_closest(a, ro, rd)
+    assert np.array_equal(gt, ot)
+    assert np.array_equal(gp.view(np.uint32), op_.view(np.uint32))
+    assert np.array_equal(gn.view(np.uint32), on.view(np.uint32))
+    assert np.array_equal(pt.trace_any(ro, rd), oracle.trace_any(a, ro, rd))
+    pt.close()
+
+
+def test_gpu_bvh_film_parity(mcpt_mod, oracle, scene_c2):
+    rc = mcpt_mod.CONFIGS[2]
+    W, H = 160, 90
+    cam = mcpt_mod.config_camera(rc, W, H)
+    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=3, max_depth=rc.max_depth))
+    pt.upload_scene(scene_c2[0], gpu_bvh=True)
+    pt.set_camera(cam)
+    pt.resize(W, H)
+    pt.render()
+    Ld, smp = pt.film()
+    rL, rs, _ = oracle.render(scene_c2[1], cam, W, H, 3, rc.max_depth)
+    assert np.array_equal(smp, rs)
+    assert np.array_equal(Ld.view(np.uint32), rL.view(np.uint32))
+    pt.close()
