@@ -603,6 +603,25 @@ MCPT_HD bool tri_test(V3 o, V3 d, V3 p0, V3 e1, V3 e2, float& t, float& u_out, f
     float v = dot(d, qvec);
     if (v < 0.f || u + v > detf) return false;
     float tf = dot(e2, qvec);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // The reference's fp64 island (Triangle.cu:35-38) rounds twice: RN32(x * RN64(1/det)).
+    // For float x and det that equals the correctly rounded fp32 quotient RN32(x / det):
+    // the double product is within ~2^-52 (relative) of x/det, while x/det is never a
+    // float rounding midpoint and lies >= ~2^-49 (relative) away from every one (x, det
+    // have 24-bit significands, a midpoint has 25), so both round the same way.  Normal
+    // range only: a nonzero subnormal quotient takes the fp64 path (flush modes differ).
+    {
+        const float tq = tf / detf, uq = u / detf, vq = v / detf;
+        const float lim = 1.17549435e-38f;
+        if (!((tq != 0.f && __builtin_fabsf(tq) < lim) || (uq != 0.f && __builtin_fabsf(uq) < lim) ||
+              (vq != 0.f && __builtin_fabsf(vq) < lim))) {
+            t = tq;
+            u_out = uq;
+            v_out = vq;
+            return true;
+        }
+    }
+#endif
     double inv_det = 1.0 / (double)detf;
     t = (float)((double)tf * inv_det);
     u_out = (float)((double)u * inv_det);

@@ -628,8 +628,10 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     sp = 0;
                     leaf = kEnd;
                     act = true;
+                    const bool pre = kind ? a.set[1].prefiltered : a.set[0].prefiltered;
                     // NaN / zero direction: a miss / visible
-                    if (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f)) {
+                    if (!pre &&
+                        (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f))) {
                         finish();
                     } else {
                         inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
@@ -639,9 +641,11 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                         fin = __builtin_fabsf(inv.x) < K_INF_F && __builtin_fabsf(inv.y) < K_INF_F &&
                               __builtin_fabsf(inv.z) < K_INF_F;
                         float t0, t1;
-                        if (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1],
-                                  sc.root_mx[2], o, inv, nx, ny, nz, t0, t1) ||
-                            !keep_box(t0, t1, cut))
+                        // (k_shade resolved the rays that miss the root box in place, so the
+                        // queued sets skip this test: same outcome, ray_misses_scene())
+                        if (!pre && (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0],
+                                           sc.root_mx[1], sc.root_mx[2], o, inv, nx, ny, nz, t0, t1) ||
+                                     !keep_box(t0, t1, cut)))
                             finish();
                         else
                             ref = sc.root_ref;

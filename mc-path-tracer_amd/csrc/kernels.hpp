@@ -96,6 +96,7 @@ struct TraceSet {
     uint32_t shard_cap;         // queue entries per shard
     uint32_t* stats;            // optional: shard s counters at stats[s * C_WORDS + 0..2] (nodes, tests, hits)
     uint32_t* ray_steps;        // optional per-queue-entry node fetches + triangle tests (diagnostics)
+    int prefiltered;            // 1: every ray has a valid direction and enters the root box (k_shade checked)
 };
 struct TraceArgs {
     DevScene scene;

@@ -480,6 +480,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     e.count_ptr = &c->cnt->shard[0][C_EXT];
     e.shard_cap = c->ext_cap;
     e.stats = &c->cnt->shard[0][C_STATS];
+    e.prefiltered = 1;  // k_shade queues only rays that enter the root box
     TraceSet& v = ta.set[1];
     v.ro = c->p.sray_o;
     v.rd = c->p.sray_d;
@@ -487,6 +488,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     v.count_ptr = &c->cnt->shard[0][C_ANY];
     v.shard_cap = c->any_cap;
     v.stats = &c->cnt->shard[0][C_STATS + 3];
+    v.prefiltered = 1;
     ta.hit_tri = c->p.hit_tri;
     ta.vis = c->p.vis;
     launch_trace(ta, c->stream);

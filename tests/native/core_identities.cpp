@@ -2,7 +2,9 @@
 // (compiled and run by tests/test_core_identities.py with hipcc (host code) -ffp-contract=off):
 //   dsincos(x) == (dsin(x), dcos(x)) bit for bit;
 //   wrapi's conditional add/subtract == the modulo form for every i;
-//   upper_bound_guided == upper_bound on sorted CDF rows.
+//   upper_bound_guided == upper_bound on sorted CDF rows;
+//   (float)((double)x * (1.0 / (double)d)) == x / d for normal-range quotients (tri_test's
+//   fp32 replacement of the reference's fp64 island).
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -60,6 +62,22 @@ int main() {
                 std::printf("upper_bound_guided n=%d val=%a\n", n, val);
         }
     }
+    // fp64 island == fp32 quotient: random significands and exponents, plus all-ones significands
+    std::uniform_int_distribution<uint32_t> M(0, 0x7FFFFF);
+    std::uniform_int_distribution<int> E(-60, 60);
+    long checked = 0;
+    for (long q = 0; q < 30000000; q++) {
+        uint32_t mx = (q % 7 == 0) ? 0x7FFFFF : M(g), md = (q % 11 == 0) ? 0x7FFFFF : M(g);
+        float x = std::ldexp(1.f + (float)mx / 8388608.f, E(g)) * ((g() & 1) ? -1.f : 1.f);
+        float d = std::ldexp(1.f + (float)md / 8388608.f, E(g) / 3);
+        if (d < 1e-6f) continue;
+        float fast = x / d;
+        if (fast != 0.f && std::fabs(fast) < 1.17549435e-38f) continue;  // subnormal: fp64 path
+        float ref = (float)((double)x * (1.0 / (double)d));
+        checked++;
+        if (bits(fast) != bits(ref) && bad++ < 5) std::printf("div %a / %a: %a vs %a\n", x, d, fast, ref);
+    }
+    std::printf("division pairs checked %ld\n", checked);
     std::printf("bad=%ld\n", bad);
     return bad != 0;
 }
