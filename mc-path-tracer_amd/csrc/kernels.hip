@@ -141,6 +141,25 @@ __device__ inline void pair_slab(float4 qx, float4 qy, float4 qz, V3 o, V3 inv, 
                           __builtin_fmaxf(az.y, bz.y));
 }
 
+// The four child boxes of a 4-wide node, same arithmetic as pair_slab (packed
+// pairs of boxes per axis and plane; entry/exit = min/max of the two products),
+// folded axis by axis (max/min are exact, so the order does not change t0/t1).
+__device__ inline void quad_axis(const float4& mn, const float4& mx, float o, float inv, float (&lo)[4],
+                                 float (&hi)[4], bool first) {
+    const f2v oo = {o, o}, ii = {inv, inv};
+    const f2v a0 = (f2v{mn.x, mn.y} - oo) * ii, a1 = (f2v{mn.z, mn.w} - oo) * ii;
+    const f2v b0 = (f2v{mx.x, mx.y} - oo) * ii, b1 = (f2v{mx.z, mx.w} - oo) * ii;
+    const float l[4] = {__builtin_fminf(a0.x, b0.x), __builtin_fminf(a0.y, b0.y), __builtin_fminf(a1.x, b1.x),
+                        __builtin_fminf(a1.y, b1.y)};
+    const float h[4] = {__builtin_fmaxf(a0.x, b0.x), __builtin_fmaxf(a0.y, b0.y), __builtin_fmaxf(a1.x, b1.x),
+                        __builtin_fmaxf(a1.y, b1.y)};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        lo[k] = first ? l[k] : __builtin_fmaxf(lo[k], l[k]);
+        hi[k] = first ? h[k] : __builtin_fminf(hi[k], h[k]);
+    }
+}
+
 // The first test the traversal makes: a NaN/zero direction or a ray that misses
 // the root box (after the cull) can hit nothing.  k_shade resolves such rays in
 // place instead of queueing them.
@@ -545,16 +564,26 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     if (Ltot == 0) return;
     const DevScene& sc = a.scene;
 
-    // work counters: per ray (rn, rt), folded into per-set totals when the ray finishes
-    // (a runtime-indexed array here would be placed in LDS by the compiler)
-    uint32_t rn = 0, rt = 0, tot_n0 = 0, tot_t0 = 0, tot_h0 = 0, tot_n1 = 0, tot_t1 = 0, tot_h1 = 0;
+    // work counters per set, kept wave-level (ballot popcounts: scalar registers) so they
+    // cost no VGPRs; per-ray step counts only in diagnostics builds (MCPT_RAY_STEPS)
+    uint32_t tot_n0 = 0, tot_t0 = 0, tot_h0 = 0, tot_n1 = 0, tot_t1 = 0, tot_h1 = 0;
+#ifdef MCPT_RAY_STEPS
+    uint32_t rn = 0, rt = 0;
+#define RAY_STEP_NODE() (rn++)
+#define RAY_STEP_TRI() (rt++)
+#else
+#define RAY_STEP_NODE() ((void)0)
+#define RAY_STEP_TRI() ((void)0)
+#endif
     uint32_t next = 0;  // wave-uniform position in the sequence
     bool act = false;
     int kind = 0;  // 0 closest, 1 any
-    uint32_t rid = 0, qi = 0;
+    uint32_t rid = 0;
+#ifdef MCPT_RAY_STEPS
+    uint32_t qi = 0;
+#endif
     V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
-    int nx = 0, ny = 0, nz = 0, ref = kEnd, leaf = kEnd, sp = 0, tri = -1;
-    int tri_key = 0x7fffffff;  // tie-break key of the best hit: its index in the uploaded scene
+    int ref = kEnd, leaf = kEnd, sp = 0, tri = -1;
     bool fin = true;  // inverse direction finite: pair_slab() is exact
     float best = K_HUGE, cut = K_HUGE;
 #ifndef MCPT_X_NOSPILL
@@ -582,11 +611,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         return kEnd;
     };
     auto finish = [&]() {
-        const uint32_t h = tri >= 0;
-        if (kind) { tot_n1 += rn; tot_t1 += rt; tot_h1 += h; }
-        else { tot_n0 += rn; tot_t0 += rt; tot_h0 += h; }
+        tot_h0 += (uint32_t)__popcll(__ballot(kind == 0 && tri >= 0));
+        tot_h1 += (uint32_t)__popcll(__ballot(kind != 0 && tri >= 0));
+#ifdef MCPT_RAY_STEPS
         uint32_t* rs = kind ? a.set[1].ray_steps : a.set[0].ray_steps;
         if (rs) rs[qi] = rn + rt;
+#endif
         if (kind) a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
         else a.hit_tri[rid] = tri;                  // hit record rebuilt by the consumer (hit_record())
         act = false;
@@ -614,15 +644,19 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     const uint32_t* qp = kind ? a.set[1].queue : a.set[0].queue;
                     const float4* rop = kind ? a.set[1].ro : a.set[0].ro;
                     const float4* rdp = kind ? a.set[1].rd : a.set[0].rd;
-                    qi = shard * (kind ? a.set[1].shard_cap : a.set[0].shard_cap) + k;
-                    rid = qp ? qp[qi] : qi;
+                    const uint32_t qslot = shard * (kind ? a.set[1].shard_cap : a.set[0].shard_cap) + k;
+#ifdef MCPT_RAY_STEPS
+                    qi = qslot;
+#endif
+                    rid = qp ? qp[qslot] : qslot;
                     const float4 o4 = rop[rid], d4 = rdp[rid];
                     o = xyz(o4);
                     d = xyz(d4);
+#ifdef MCPT_RAY_STEPS
                     rn = 0;
                     rt = 0;
+#endif
                     tri = -1;
-                    tri_key = 0x7fffffff;
                     best = K_HUGE;
                     cut = best + best * kCullRel;
                     sp = 0;
@@ -635,16 +669,14 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                         finish();
                     } else {
                         inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-                        nx = inv.x < 0.f;
-                        ny = inv.y < 0.f;
-                        nz = inv.z < 0.f;
                         fin = __builtin_fabsf(inv.x) < K_INF_F && __builtin_fabsf(inv.y) < K_INF_F &&
                               __builtin_fabsf(inv.z) < K_INF_F;
                         float t0, t1;
                         // (k_shade resolved the rays that miss the root box in place, so the
                         // queued sets skip this test: same outcome, ray_misses_scene())
                         if (!pre && (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0],
-                                           sc.root_mx[1], sc.root_mx[2], o, inv, nx, ny, nz, t0, t1) ||
+                                           sc.root_mx[1], sc.root_mx[2], o, inv, inv.x < 0.f, inv.y < 0.f, inv.z < 0.f,
+                                           t0, t1) ||
                                      !keep_box(t0, t1, cut)))
                             finish();
                         else
@@ -666,9 +698,69 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
           for (int it = 0; it < kNodeSteps; it++) {
             bool need_pop = false;
             if (ref >= 0) {
+              RAY_STEP_NODE();
+              tot_n0 += (uint32_t)__popcll(__ballot(kind == 0));
+              tot_n1 += (uint32_t)__popcll(__ballot(kind != 0));
+              const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;  // slow-path slab only
+              if constexpr (kNodeWidth == 4) {
+                // 4-wide node: test the four child boxes, visit the nearest hit, push the
+                // other hits far-to-near with their entry t (popped nearest-first)
+                const float4* nd = sc.nodes + 8 * ref;
+                const float4 mnx = nd[0], mxx = nd[1], mny = nd[2], mxy = nd[3], mnz = nd[4], mxz = nd[5], rf = nd[6];
+                float t0[4], t1[4];
+                bool hk[4];
+                if (fin) {
+                    quad_axis(mnx, mxx, o.x, inv.x, t0, t1, true);
+                    quad_axis(mny, mxy, o.y, inv.y, t0, t1, false);
+                    quad_axis(mnz, mxz, o.z, inv.z, t0, t1, false);
+#pragma unroll
+                    for (int k = 0; k < 4; k++) hk[k] = t0[k] <= t1[k];
+                } else {
+                    const float* fmnx = &mnx.x; const float* fmxx = &mxx.x;
+                    const float* fmny = &mny.x; const float* fmxy = &mxy.x;
+                    const float* fmnz = &mnz.x; const float* fmxz = &mxz.x;
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        hk[k] = slab(fmnx[k], fmny[k], fmnz[k], fmxx[k], fmxy[k], fmxz[k], o, inv, nx, ny, nz, t0[k],
+                                     t1[k]);
+                }
+                int rr[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+                float key[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const bool h = hk[k] && rr[k] != kEnd && keep_box(t0[k], t1[k], cut);
+                    // sort key: entry t (a NaN entry from the NaN-passing slab sorts first and
+                    // is never culled on pop), misses last
+                    key[k] = h ? (t0[k] == t0[k] ? t0[k] : -K_INF_F) : K_INF_F;
+                    rr[k] = h ? rr[k] : kEnd;
+                }
+#define MCPT_CAS(i, j)                                                   \
+                if (key[j] < key[i]) {                                    \
+                    const float tk = key[i]; key[i] = key[j]; key[j] = tk; \
+                    const int tr = rr[i]; rr[i] = rr[j]; rr[j] = tr;       \
+                }
+                MCPT_CAS(0, 1) MCPT_CAS(2, 3) MCPT_CAS(0, 2) MCPT_CAS(1, 3) MCPT_CAS(1, 2)
+#undef MCPT_CAS
+                need_pop = rr[0] == kEnd;
+                if (!need_pop) {
+#pragma unroll
+                    for (int k = 3; k >= 1; k--) {
+                        if (rr[k] != kEnd) {
+                            const int2 e = make_int2(rr[k], __float_as_int(key[k]));
+#ifndef MCPT_X_NOSPILL
+                            if (sp < kLdsStack) stk[sp][lane] = e;
+                            else spill[sp - kLdsStack] = e;
+#else
+                            stk[sp < kLdsStack ? sp : kLdsStack - 1][lane] = e;
+#endif
+                            sp++;
+                        }
+                    }
+                    ref = rr[0];
+                }
+              } else {
                 const float4* nd = sc.nodes + 4 * ref;
                 const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-                rn++;
                 float a0, b0, a1, b1;
                 bool h0, h1;
                 // node layout (SoA pairs): q0 = (mn.x, mn.x', mx.x, mx.x'), q1 = y, q2 = z,
@@ -699,6 +791,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 } else {
                     ref = h0 ? c0 : c1;
                 }
+              }
             }
             // a reached leaf is parked in the lane's leaf slot and traversal
             // continues speculatively with the next stack entry
@@ -728,19 +821,21 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 const int id = leaf & 0xffffff;
                 const float4* tp = sc.tri + 3 * id;
                 const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-                rt++;
+                RAY_STEP_TRI();
+                tot_t0 += (uint32_t)__popcll(__ballot(kind == 0));
+                tot_t1 += (uint32_t)__popcll(__ballot(kind != 0));
                 float t, u, v;
                 bool done = false;
                 if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) &&
                     !(t < 0.f)) {
                     if (kind) {
                         if (t < K_HUGE) { tri = id; done = true; }  // occluded (tmax 1e32)
-                    } else if (t < best || (t == best && __float_as_int(w2.y) < tri_key)) {
+                    } else if (t < best ||
+                               (t == best && __float_as_int(w2.y) < __float_as_int(sc.tri[3 * tri + 2].y))) {
                         // exact-t ties go to the lower scene index (tri record .y of the
                         // third float4), whatever order the BVH build stored triangles in
                         best = t;
                         tri = id;
-                        tri_key = __float_as_int(w2.y);
                         cut = best + best * kCullRel;
                     }
                 }

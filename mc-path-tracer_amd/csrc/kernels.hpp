@@ -40,8 +40,17 @@ enum : uint32_t {
     F_HASVIS = 1u << 12     // non-delta light: a BRDF visibility ray was traced
 };
 
+// BVH node width of the traversal (MCPT_BVH_WIDTH, 2 or 4).  Width 2: child-pair
+// nodes, 4 x float4 (per axis (mn0, mn1, mx0, mx1), then refs).  Width 4: 8 x float4:
+// mn.x[4], mx.x[4], mn.y[4], mx.y[4], mn.z[4], mx.z[4], refs[4] (kEnd = empty), pad.
+#ifndef MCPT_BVH_WIDTH
+#define MCPT_BVH_WIDTH 2
+#endif
+constexpr int kNodeWidth = MCPT_BVH_WIDTH;
+constexpr int kNodeF4 = kNodeWidth == 4 ? 8 : 4;  // float4 per node
+
 struct DevScene {
-    const float4* nodes;    // child-pair BVH nodes, 4 x float4 each
+    const float4* nodes;    // BVH nodes (kNodeWidth children each, kNodeF4 x float4)
     const float4* tri;      // 3 x float4: (v0.xyz, e1.x) (e1.yz, e2.xy) (e2.z, -, -, -)
     const float4* tri_sh;   // 3 x float4: (n0.xyz, n1.x) (n1.yz, n2.xy) (n2.z, mat, -, -)
     float root_mn[3], root_mx[3];

@@ -156,6 +156,73 @@ int mcpt_device_name(mcpt_ctx* c, char* buf, int32_t len) {
 
 // Scene upload: LinearBVHNode (BVH.h:63-72) -> child-pair nodes, dTriangle
 // (Triangle.h:11-23, 288 B) -> 48-B intersection + 48-B shading records.
+
+// Collapse a child-pair BVH into 4-wide nodes (kNodeWidth == 4): every 4-wide node
+// is a pair node at even depth; its slots are the children of its two children
+// (a leaf child takes one slot itself).  Boxes are copied, never recomputed, so
+// every leaf box is the pair tree's (and the reference builder's) exact box.
+// Breadth-first numbering keeps the top levels together.  Returns the new root
+// ref and the largest number of stack pushes along any root-to-leaf path.
+static int pairs_to_quads(const std::vector<float4>& pn, int root_ref, std::vector<float4>& qn, int& new_root,
+                          int& max_push) {
+    qn.clear();
+    max_push = 0;
+    if (root_ref < 0) { new_root = root_ref; return 0; }
+    auto ref_at = [&](int p, int k) { int r; memcpy(&r, k ? &pn[4 * p + 3].y : &pn[4 * p + 3].x, 4); return r; };
+    auto comp = [](const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
+    std::vector<int> quad_of(pn.size() / 4, -1), order;
+    std::vector<int> push_depth;  // pushes accumulated on the path to each quad node
+    order.push_back(root_ref);
+    quad_of[root_ref] = 0;
+    push_depth.push_back(0);
+    for (size_t h = 0; h < order.size(); h++) {
+        const int p = order[h];
+        struct Slot { float mn[3], mx[3]; int ref; };
+        Slot sl[4];
+        int n = 0;
+        for (int k = 0; k < 2; k++) {
+            const int r = ref_at(p, k);
+            if (r < 0) {  // leaf child of the pair node: its box is in p
+                for (int a = 0; a < 3; a++) { sl[n].mn[a] = comp(pn[4 * p + a], k); sl[n].mx[a] = comp(pn[4 * p + a], 2 + k); }
+                sl[n++].ref = r;
+            } else {      // interior child: take its two children
+                for (int j = 0; j < 2; j++) {
+                    for (int a = 0; a < 3; a++) { sl[n].mn[a] = comp(pn[4 * r + a], j); sl[n].mx[a] = comp(pn[4 * r + a], 2 + j); }
+                    sl[n++].ref = ref_at(r, j);
+                }
+            }
+        }
+        const int pd = push_depth[h] + (n - 1);
+        max_push = std::max(max_push, pd);
+        for (int k = 0; k < n; k++) {
+            if (sl[k].ref >= 0) {
+                const int g = sl[k].ref;
+                if (quad_of[g] < 0) {
+                    quad_of[g] = (int)order.size();
+                    order.push_back(g);
+                    push_depth.push_back(pd);
+                }
+                sl[k].ref = quad_of[g];
+            }
+        }
+        float4 q[8];
+        float* f = reinterpret_cast<float*>(q);
+        for (int i = 0; i < 32; i++) f[i] = 0.f;
+        for (int k = 0; k < 4; k++) {
+            const bool used = k < n;
+            for (int a = 0; a < 3; a++) {
+                f[(2 * a) * 4 + k] = used ? sl[k].mn[a] : 0.f;      // mn.a[k]
+                f[(2 * a + 1) * 4 + k] = used ? sl[k].mx[a] : 0.f;  // mx.a[k]
+            }
+            int r = used ? sl[k].ref : -1;  // kEnd: empty slot
+            memcpy(&f[6 * 4 + k], &r, 4);
+        }
+        qn.insert(qn.end(), q, q + 8);
+    }
+    new_root = 0;
+    return 0;
+}
+
 static hipEvent_t ev(mcpt_ctx* c, size_t i);
 static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     if (!c || !d) return set_err(c, MCPT_E_INVALID, "null argument");
@@ -263,13 +330,36 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     if ((rc = dupload(c, c->scene_bufs, &dm, d->mat_params, (size_t)d->nmat * 8))) return rc;
     if ((rc = dupload(c, c->scene_bufs, &dd, d->dir_params, (size_t)d->ndir * 7))) return rc;
     s.nodes = dn; s.tri = dt; s.tri_sh = dsh; s.mats = dm; s.dirs = dd;
+    int quad_root = 0;
+    if (kNodeWidth == 4) {
+        // 4-wide traversal: collapse the pair tree (host SAH or GPU LBVH) into 4-wide nodes
+        std::vector<float4> pairs;
+        int proot;
+        if (gpu_bvh && d->ntri > 0) {
+            pairs.resize((size_t)lb.nnodes * 4);
+            if (lb.nnodes) HIPCHK(c, hipMemcpy(pairs.data(), lb.nodes, pairs.size() * sizeof(float4), hipMemcpyDeviceToHost));
+            proot = lb.root_ref;
+        } else {
+            pairs = pn;
+            proot = N > 0 ? ref_of(0) : 0;
+        }
+        std::vector<float4> quads;
+        int max_push = 0;
+        if (d->ntri > 0) {
+            pairs_to_quads(pairs, proot, quads, quad_root, max_push);
+            if (max_push > kMaxStack) return set_err(c, MCPT_E_INVALID, "4-wide BVH needs more than 64 stack entries");
+            float4* dq;
+            if ((rc = dupload(c, c->scene_bufs, &dq, quads.data(), quads.size()))) return rc;
+            s.nodes = dq;
+        }
+    }
     s.nlights = 1 + d->ndir;
     if (gpu_bvh && d->ntri > 0) {
         for (int k = 0; k < 3; k++) { s.root_mn[k] = lb.root_mn[k]; s.root_mx[k] = lb.root_mx[k]; }
-        s.root_ref = lb.root_ref;
+        s.root_ref = kNodeWidth == 4 ? (lb.root_ref < 0 ? lb.root_ref : quad_root) : lb.root_ref;
     } else if (N > 0) {
         for (int k = 0; k < 3; k++) { s.root_mn[k] = d->bmin[k]; s.root_mx[k] = d->bmax[k]; }
-        s.root_ref = ref_of(0);
+        s.root_ref = kNodeWidth == 4 ? (ref_of(0) < 0 ? ref_of(0) : quad_root) : ref_of(0);
     } else {
         // empty scene: a root box that no ray can enter
         for (int k = 0; k < 3; k++) { s.root_mn[k] = 1.f; s.root_mx[k] = -1.f; }
