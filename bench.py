@@ -169,7 +169,7 @@ def main():
             "algorithmic_bytes_per_launch": int(per_launch),
             "note": "logical bytes (SURVEY 8d) count every BVH node/triangle fetch; those are served from L2/MALL, "
                     "so frac can exceed HBM reality - traffic is the measured HBM bytes per launch; the traversal "
-                    "is VALU-issue bound (DESIGN.md)",
+                    "is bound by its divergent issue/latency mix (VALU ~70%, TD ~78%, TA ~64% busy: DESIGN.md)",
             "state_only_frac": round(state / K / (avg_ms * 1e-3) / HBM_PEAK, 4),
             "per_ray": {"ext_pair_nodes": round(st.ext_nodes / max(1, st.extend_rays), 2),
                         "ext_tri_tests": round(st.ext_tests / max(1, st.extend_rays), 2),

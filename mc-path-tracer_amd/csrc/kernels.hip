@@ -564,8 +564,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     if (Ltot == 0) return;
     const DevScene& sc = a.scene;
 
-    // work counters per set, kept wave-level (ballot popcounts: scalar registers) so they
-    // cost no VGPRs; per-ray step counts only in diagnostics builds (MCPT_RAY_STEPS)
+    // per-lane work counters per set (wave-reduced at exit); per-ray step counts only in
+    // diagnostics builds (MCPT_RAY_STEPS)
     uint32_t tot_n0 = 0, tot_t0 = 0, tot_h0 = 0, tot_n1 = 0, tot_t1 = 0, tot_h1 = 0;
 #ifdef MCPT_RAY_STEPS
     uint32_t rn = 0, rt = 0;
@@ -611,8 +611,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         return kEnd;
     };
     auto finish = [&]() {
-        tot_h0 += (uint32_t)__popcll(__ballot(kind == 0 && tri >= 0));
-        tot_h1 += (uint32_t)__popcll(__ballot(kind != 0 && tri >= 0));
+        tot_h0 += (kind == 0 && tri >= 0) ? 1u : 0u;
+        tot_h1 += (kind != 0 && tri >= 0) ? 1u : 0u;
 #ifdef MCPT_RAY_STEPS
         uint32_t* rs = kind ? a.set[1].ray_steps : a.set[0].ray_steps;
         if (rs) rs[qi] = rn + rt;
@@ -699,8 +699,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             bool need_pop = false;
             if (ref >= 0) {
               RAY_STEP_NODE();
-              tot_n0 += (uint32_t)__popcll(__ballot(kind == 0));
-              tot_n1 += (uint32_t)__popcll(__ballot(kind != 0));
+              tot_n0 += kind == 0 ? 1u : 0u;
+              tot_n1 += kind != 0 ? 1u : 0u;
               const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;  // slow-path slab only
               if constexpr (kNodeWidth == 4) {
                 // 4-wide node: test the four child boxes, visit the nearest hit, push the
@@ -822,8 +822,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 const float4* tp = sc.tri + 3 * id;
                 const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
                 RAY_STEP_TRI();
-                tot_t0 += (uint32_t)__popcll(__ballot(kind == 0));
-                tot_t1 += (uint32_t)__popcll(__ballot(kind != 0));
+                tot_t0 += kind == 0 ? 1u : 0u;
+                tot_t1 += kind != 0 ? 1u : 0u;
                 float t, u, v;
                 bool done = false;
                 if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) &&

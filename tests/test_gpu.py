@@ -172,6 +172,11 @@ def test_config2_1080p_band_parity_and_properties(mcpt_mod, oracle, scene_c2):
     Ld, smp = pt.film()
     assert np.all(smp[:-1, :-1] == 2) and np.all(smp[-1] == 0) and np.all(smp[:, -1] == 0)
     assert st.live_paths == 0
+    # traversal work counters: per traced ray, a handful of node pairs and triangle tests
+    rays_any = st.shadow_rays + st.vis_rays
+    assert 1.0 < st.ext_nodes / st.extend_rays < 64.0 and 0.1 < st.ext_tests / st.extend_rays < 32.0
+    assert 1.0 < st.any_nodes / rays_any < 64.0 and 0.1 < st.any_tests / rays_any < 32.0
+    assert 0 < st.ext_hits <= st.extend_rays and st.any_hits <= rays_any
     r0, r1 = 532, 548
     rL, rs, _ = oracle.render(scene_c2[1], cam, W, H, 2, rc.max_depth, rows=(r0, r1))
     assert np.array_equal(smp[r0:r1], rs[r0:r1])
