@@ -13,7 +13,7 @@ SRCS := $(PKG)/csrc/kernels.hip $(PKG)/csrc/bvh_build.hip $(PKG)/csrc/runtime.cp
 OBJS := $(patsubst $(PKG)/csrc/%,$(BUILD)/%.o,$(SRCS))
 HDRS := include/mcpt.h $(PKG)/csrc/kernels.hpp $(PKG)/csrc/device/mcpt_core.hpp $(PKG)/csrc/host/host_internal.hpp
 
-all: $(PKG)/libmcpt.so oracle/liboracle.so
+all: $(PKG)/libmcpt.so oracle/liboracle.so examples/mcpt_render
 
 $(BUILD)/%.o: $(PKG)/csrc/% $(HDRS)
 	@mkdir -p $(dir $@)
@@ -22,11 +22,17 @@ $(BUILD)/%.o: $(PKG)/csrc/% $(HDRS)
 $(PKG)/libmcpt.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
+# C++ example over the C ABI only: render a BASELINE config, write PNG/PFM
+examples/mcpt_render: examples/mcpt_render.cpp include/mcpt.h $(PKG)/libmcpt.so
+	g++ -O2 -std=c++17 -Iinclude $< -L$(PKG) -lmcpt -Wl,-rpath,'$$ORIGIN/../$(PKG)' -o $@
+
+example: examples/mcpt_render
+
 oracle/liboracle.so: oracle/mcpt_oracle.c oracle/mcpt_oracle.h
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(BUILD) $(PKG)/libmcpt.so
+	rm -rf $(BUILD) $(PKG)/libmcpt.so examples/mcpt_render
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean

@@ -66,3 +66,18 @@ def test_camera_matrices(mcpt_mod):
     right = m @ np.array([1, 0, 1, 1.0])
     right = right[:3] / right[3] - near
     np.testing.assert_allclose(right[0] / top[1], 2.0, rtol=1e-5)       # aspect
+
+
+def test_cpp_example_links_against_the_abi():
+    """examples/mcpt_render (C++ over include/mcpt.h only) is built by `make` and resolves every
+    mcpt_* symbol it uses from libmcpt.so."""
+    import subprocess
+
+    exe = os.path.join(REPO, "examples", "mcpt_render")
+    assert os.path.exists(exe)
+    out = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True, text=True, check=True).stdout
+    used = sorted({l.split()[-1] for l in out.splitlines() if "mcpt_" in l})
+    lib = subprocess.run(["nm", "-D", "--defined-only", os.path.join(REPO, "mc-path-tracer_amd", "libmcpt.so")],
+                         capture_output=True, text=True, check=True).stdout
+    defined = {l.split()[-1] for l in lib.splitlines()}
+    assert used and all(u in defined for u in used), [u for u in used if u not in defined]

@@ -340,3 +340,24 @@ def test_gpu_bvh_film_parity(mcpt_mod, oracle, scene_c2):
     assert np.array_equal(smp, rs)
     assert np.array_equal(Ld.view(np.uint32), rL.view(np.uint32))
     pt.close()
+
+
+def test_cpp_example_batch_equals_reference_orchestration(tmp_path):
+    """examples/mcpt_render (C++ over the C ABI only): config 1 at 4 spp in batch mode and in the
+    reference's one-tile-per-call orchestration write bit-identical PFM films."""
+    import subprocess
+
+    from conftest import REPO
+    from test_image_io import read_pfm, read_png
+
+    exe = os.path.join(REPO, "examples", "mcpt_render")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", REPO, "example"], check=True, capture_output=True)
+    env = dict(os.environ, MCPT_ASSETS=os.path.join(REPO, "assets"))
+    for mode, extra in (("batch", []), ("tile", ["--tiles-per-call"])):
+        r = subprocess.run([exe, "1", "4", str(tmp_path / mode)] + extra, capture_output=True, text=True, env=env,
+                           timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+    a, b = read_pfm(tmp_path / "batch.pfm"), read_pfm(tmp_path / "tile.pfm")
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert read_png(tmp_path / "batch.png").shape == (256, 256, 3)
