@@ -52,6 +52,11 @@ typedef struct mcpt_config {
  * Gram-Schmidt, env sampling and pdf on matched (clamped) cells.  An alternative integrator:
  * never compared against the reference, only against the oracle's fixed mode. */
 #define MCPT_FLAG_FIXED 1
+/* The film observes the camera and the scene as in the reference (Film::update -> clear(),
+ * Film.cu:278-281): mcpt_camera_set with a different camera, or a scene re-upload, marks the
+ * film stale and the next mcpt_iterate / mcpt_wavefront_step / mcpt_render clears it first.
+ * This flag turns that off (the caller clears explicitly with mcpt_film_clear). */
+#define MCPT_FLAG_NO_AUTO_CLEAR 2
 
 /* Scene as flat, BVH-ordered arrays (the device data model of Scene.h:24-33,
  * BVH.h:63-72, Triangle.h:11-23, dMaterial.cuh:11-33, EnvironmentLight.h:17-40). */
@@ -169,6 +174,9 @@ float mcpt_debug_last_build_ms(const mcpt_ctx *ctx);  /* device time of the last
  * idle lane-trips, trips with a pop, popping lanes, trips with a non-finite-direction slab, finishing lanes, -}
  * summed over waves since the last reset. */
 int mcpt_debug_trace_profile(mcpt_ctx *ctx, uint64_t *out12, int reset);
+/* diagnostics: the kernels' shared-denominator division (mcpt::quot3, mcpt_core.hpp) on the
+ * device for n host pairs: out[i] = a[i] / b[i] as the kernels compute it (must equal IEEE fp32). */
+int mcpt_debug_quot(mcpt_ctx *ctx, const float *a, const float *b, uint32_t n, float *out);
 
 /* ---- host scene builder (Scene.cu:24-470, EnvironmentLight.cu:329-452, BVH.cu) ---- */
 mcpt_scene *mcpt_scene_new(void);

@@ -207,10 +207,12 @@ MCPT_HD uint32_t rng_key(uint64_t seed, uint32_t pixel, uint32_t sample) {
     uint64_t s = splitmix64((((uint64_t)pixel << 32) | (uint64_t)sample) ^ seed);
     return (uint32_t)(s ^ (s >> 32));
 }
-// rand_float: rand() * 2^-32 in double, rounded to float (Random.cu:31-35).
+// rand_float: rand() * 2^-32 in double, rounded to float (Random.cu:31-35).  The
+// double product is exact, so RN32(d * 2^-32) == RN32(d) * 2^-32 (power-of-two
+// scale, no underflow): one u32 -> f32 conversion and one exact multiply.
 MCPT_HD float rngf(uint32_t key, uint32_t len, uint32_t slot) {
     uint32_t d = lowerbias32(key + (len * 16u + slot) * 0x9E3779B9u);
-    return (float)((double)d * 0.00000000023283064365386962890625);
+    return (float)d * 2.3283064365386962890625e-10f;
 }
 enum : uint32_t {
     SL_GEN_U = 0, SL_GEN_V = 1,
@@ -224,6 +226,53 @@ struct Rng {
 };
 
 // ---------------------------------------------------------------------------
+// Quotients with a shared denominator.  The reference divides in IEEE fp32:
+// RN32(a / b), which gfx950 expands to ~12 VALU operations per quotient
+// (div_scale x2, rcp, 6 fma, div_fmas, div_fixup).  Device code computes one
+// fp64 reciprocal y per denominator (hardware estimate + two Newton steps:
+// |y - 1/b| <= ~2^-52 |1/b|) and RN32(RN64(a * y)) per quotient, 3 operations.
+// Equal to RN32(a / b) for finite nonzero b: the product is within 2^-51
+// (relative) of a/b, while a/b with 24-bit significands is never a float
+// rounding boundary and stays >= 2^-49 (relative) away from every one (a 25-bit
+// midpoint m = a/b would need a = m b with >24 significant bits).  Quotients in
+// the subnormal range redo the IEEE division (the conversion's denormal mode is
+// not relied on).  tests/native/core_identities.cpp checks quot_fp64 against a/b
+// with y perturbed by the reciprocal's error budget.  Host code divides.
+// ---------------------------------------------------------------------------
+struct Recip { float b; double y; bool ok; };
+MCPT_HD bool quot_fp64(float a, double y, float& q) {  // false: redo as a / b
+    q = (float)((double)a * y);
+    return __builtin_fabsf(q) >= 1.17549435e-38f || a == 0.f;
+}
+MCPT_HD Recip recip(float b) {
+    Recip r{b, 0.0, false};
+#if defined(__HIP_DEVICE_COMPILE__)
+    r.ok = __builtin_fabsf(b) <= 3.40282347e38f && b != 0.f;
+    const double bd = (double)b;
+    double y = __builtin_amdgcn_rcp(bd);
+    double e = __builtin_fma(-bd, y, 1.0);
+    y = __builtin_fma(e, y, y);
+    e = __builtin_fma(-bd, y, 1.0);
+    r.y = __builtin_fma(e, y, y);
+#endif
+    return r;
+}
+// The three quotients of one denominator, with one (rarely taken) branch for the
+// whole group: any out-of-range case redoes all three as IEEE divisions.
+MCPT_HD void quot3(float a0, float a1, float a2, float b, float& q0, float& q1, float& q2) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const Recip r = recip(b);
+    bool good = quot_fp64(a0, r.y, q0);
+    good = quot_fp64(a1, r.y, q1) && good;
+    good = quot_fp64(a2, r.y, q2) && good;
+    if (r.ok && good) return;
+#endif
+    q0 = a0 / b;
+    q1 = a1 / b;
+    q2 = a2 / b;
+}
+
+// ---------------------------------------------------------------------------
 // Vec3f (cuda_math/Vector.h): one rounding per component per operator.
 // ---------------------------------------------------------------------------
 struct V3 { float x, y, z; };
@@ -233,7 +282,11 @@ MCPT_HD V3 operator-(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 MCPT_HD V3 operator*(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 MCPT_HD V3 operator/(V3 a, V3 b) { return V3{a.x / b.x, a.y / b.y, a.z / b.z}; }
 MCPT_HD V3 operator*(V3 v, float s) { return V3{s * v.x, s * v.y, s * v.z}; }
-MCPT_HD V3 operator/(V3 v, float s) { return V3{v.x / s, v.y / s, v.z / s}; }
+MCPT_HD V3 operator/(V3 v, float s) {
+    V3 q;
+    quot3(v.x, v.y, v.z, s, q.x, q.y, q.z);
+    return q;
+}
 MCPT_HD V3 operator-(V3 v) { return V3{-v.x, -v.y, -v.z}; }
 MCPT_HD float dot(V3 a, V3 b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }  // Vector.h:790
 MCPT_HD V3 normalize(V3 v) {                                                      // Vector.h:1077
@@ -608,13 +661,16 @@ MCPT_HD bool tri_test(V3 o, V3 d, V3 p0, V3 e1, V3 e2, float& t, float& u_out, f
     // For float x and det that equals the correctly rounded fp32 quotient RN32(x / det):
     // the double product is within ~2^-52 (relative) of x/det, while x/det is never a
     // float rounding midpoint and lies >= ~2^-49 (relative) away from every one (x, det
-    // have 24-bit significands, a midpoint has 25), so both round the same way.  Normal
-    // range only: a nonzero subnormal quotient takes the fp64 path (flush modes differ).
+    // have 24-bit significands, a midpoint has 25), so both round the same way -- and so
+    // does quot_fp64 with the Newton-refined reciprocal (see Recip).  Normal range only:
+    // a nonzero subnormal quotient takes the reference's fp64 path.
     {
-        const float tq = tf / detf, uq = u / detf, vq = v / detf;
-        const float lim = 1.17549435e-38f;
-        if (!((tq != 0.f && __builtin_fabsf(tq) < lim) || (uq != 0.f && __builtin_fabsf(uq) < lim) ||
-              (vq != 0.f && __builtin_fabsf(vq) < lim))) {
+        const Recip r = recip(detf);
+        float tq, uq, vq;
+        bool good = quot_fp64(tf, r.y, tq);
+        good = quot_fp64(u, r.y, uq) && good;
+        good = quot_fp64(v, r.y, vq) && good;
+        if (r.ok && good) {
             t = tq;
             u_out = uq;
             v_out = vq;

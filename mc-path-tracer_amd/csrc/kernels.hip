@@ -761,6 +761,13 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
               } else {
                 const float4* nd = sc.nodes + 4 * ref;
                 const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+#ifdef MCPT_X_EXTRA_FETCH  // experiment: +50% node bytes (the neighbouring node's first half)
+                {
+                    const float4* xn = sc.nodes + 4 * (ref > 0 ? ref - 1 : ref);
+                    const float4 x0 = xn[0], x1 = xn[1];
+                    if (x0.x == 1234.5f && x1.w == 9876.5f) ref = kEnd;
+                }
+#endif
                 float a0, b0, a1, b1;
                 bool h0, h1;
                 // node layout (SoA pairs): q0 = (mn.x, mn.x', mx.x, mx.x'), q1 = y, q2 = z,
@@ -990,6 +997,17 @@ void launch_trace(const TraceArgs& args, hipStream_t s) {
     const uint32_t wps = std::max<uint32_t>(1, persistent_waves() / nsh);
     hipLaunchKernelGGL(k_trace, dim3(wps * nsh), dim3(kTraceBlock), 0, s, a);
 }
+__global__ void k_quot(const float* a, const float* b, float* out, uint32_t n) {  // mcpt_debug_quot
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float q0, q1, q2;
+    quot3(a[i], 1.0f, -a[i], b[i], q0, q1, q2);
+    out[i] = q0;
+}
+void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_quot, dim3((n + 255) / 256), dim3(256), 0, s, a, b, out, n);
+}
+
 int trace_profile(unsigned long long* out, int reset) {  // diagnostics build only
 #ifdef MCPT_TRACE_PROF
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace_prof), sizeof(g_trace_prof)) != hipSuccess) return -1;

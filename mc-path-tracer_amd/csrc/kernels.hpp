@@ -136,6 +136,7 @@ struct LbvhOutput {
 };
 int build_lbvh(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
 int trace_profile(unsigned long long* out, int reset);
+void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStream_t s);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);
 void launch_accumulate(CounterBlock* c, hipStream_t s);

@@ -36,10 +36,15 @@ struct mcpt_ctx {
     std::vector<void*> scene_bufs;
     DevScene scene{};
     bool has_scene = false;
+    bool has_scene_before = false;  // set at the start of a re-upload
     int pair_depth = 0;
     // camera
     mcpt::CamView cam{};
     bool has_cam = false;
+    // Film observes camera and scene (Film::update -> clear(), Film.cu:278-281; notified by
+    // Camera::update, Camera.cu:207, and Scene::notify, Scene.cu:534-545): a change marks the
+    // film stale and the next iteration clears it first (unless MCPT_FLAG_NO_AUTO_CLEAR).
+    bool film_stale = false;
     // film + paths
     uint32_t W = 0, H = 0, tile_w = 256, tile_h = 256;
     size_t P = 0;
@@ -236,6 +241,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     free_list(c->scene_bufs);
+    c->has_scene_before = c->has_scene_before || c->has_scene;
     c->has_scene = false;
     const int N = gpu_bvh ? 0 : d->nnodes;  // gpu_bvh: the desc's BVH arrays are ignored
     // pair-node numbering of interior nodes + validation
@@ -408,6 +414,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         }
     }
     c->scene = s;
+    if (c->has_scene_before) c->film_stale = true;  // a re-upload notifies the film
     c->has_scene = true;
     return MCPT_OK;
 }
@@ -418,10 +425,13 @@ float mcpt_debug_last_build_ms(const mcpt_ctx* c) { return c ? c->last_build_ms 
 
 int mcpt_camera_set(mcpt_ctx* c, const mcpt_camera* cam) {
     if (!c || !cam) return set_err(c, MCPT_E_INVALID, "null argument");
-    memcpy(c->cam.ivp, cam->inv_view_proj, sizeof(c->cam.ivp));
-    memcpy(c->cam.iv, cam->inv_view, sizeof(c->cam.iv));
-    c->cam.lens_radius = cam->lens_radius;
-    c->cam.focal = cam->focal;
+    mcpt::CamView nc = c->cam;
+    memcpy(nc.ivp, cam->inv_view_proj, sizeof(nc.ivp));
+    memcpy(nc.iv, cam->inv_view, sizeof(nc.iv));
+    nc.lens_radius = cam->lens_radius;
+    nc.focal = cam->focal;
+    if (c->has_cam && memcmp(&nc, &c->cam, sizeof(nc)) != 0) c->film_stale = true;
+    c->cam = nc;
     c->has_cam = true;
     return MCPT_OK;
 }
@@ -469,6 +479,7 @@ int mcpt_film_clear(mcpt_ctx* c) {
     ClearArgs a{c->p.flags, c->p.samples, c->p.Ld, (uint32_t)c->P};
     launch_clear(a, c->stream);
     HIPCHK(c, hipGetLastError());
+    c->film_stale = false;
     HIPCHK(c, hipMemsetAsync(c->cnt, 0, sizeof(CounterBlock), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return MCPT_OK;
@@ -592,6 +603,7 @@ static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st) {
     int rc = check_ready(c);
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
+    if (c->film_stale && !(c->cfg.flags & MCPT_FLAG_NO_AUTO_CLEAR) && (rc = mcpt_film_clear(c))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->cnt_host, c->cnt, sizeof(CounterBlock), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     CounterBlock before = *c->cnt_host;
@@ -842,6 +854,27 @@ int mcpt_debug_queue_rays(mcpt_ctx* c, int which, float* ro, float* rd, uint32_t
     return MCPT_OK;
 }
 float mcpt_debug_last_stage_ms(const mcpt_ctx* c) { return c ? c->last_stage_ms : -1.f; }
+
+int mcpt_debug_quot(mcpt_ctx* c, const float* a, const float* b, uint32_t n, float* out) {
+    if (!c || (n && (!a || !b || !out))) return set_err(c, MCPT_E_INVALID, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    float* d = nullptr;
+    if (n == 0) return MCPT_OK;
+    if (hipMalloc(&d, (size_t)3 * n * sizeof(float)) != hipSuccess) return set_err(c, MCPT_E_NOMEM, "quot buffers");
+    int rc = MCPT_OK;
+    if (hipMemcpyAsync(d, a, n * sizeof(float), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(d + n, b, n * sizeof(float), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        rc = set_err(c, MCPT_E_HIP, "copy");
+    if (!rc) {
+        launch_quot(d, d + n, d + 2 * (size_t)n, n, c->stream);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(out, d + 2 * (size_t)n, n * sizeof(float), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            rc = set_err(c, MCPT_E_HIP, "quot kernel");
+    }
+    (void)hipFree(d);
+    return rc;
+}
 
 int mcpt_debug_trace_profile(mcpt_ctx* c, uint64_t* out8, int reset) {  // out8: 12 words
     if (!c || !out8) return MCPT_E_INVALID;

@@ -109,6 +109,7 @@ ABI = {
     "mcpt_image_write_png": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]),
     "mcpt_image_write_pfm": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_float)]),
     "mcpt_debug_trace_profile": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
+    "mcpt_debug_quot": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "mcpt_scene_new": (C.c_void_p, []),
     "mcpt_scene_free": (None, [C.c_void_p]),
     "mcpt_scene_load_glb": (C.c_int, [C.c_void_p, C.c_char_p, _f]),
@@ -157,10 +158,13 @@ def fptr(a: np.ndarray):
 
 
 FLAG_FIXED = 1  # MCPT_FLAG_FIXED: quality-mode integrator
+FLAG_NO_AUTO_CLEAR = 2  # MCPT_FLAG_NO_AUTO_CLEAR: camera / scene changes do not clear the film
 
 
-def default_config(spp=16, max_depth=5, rr_depth=3, seed=0x5EED2026, tile=256, fixed=False) -> Config:
-    return Config(seed, spp, max_depth, rr_depth, tile, tile, FLAG_FIXED if fixed else 0)
+def default_config(spp=16, max_depth=5, rr_depth=3, seed=0x5EED2026, tile=256, fixed=False,
+                   auto_clear=True) -> Config:
+    flags = (FLAG_FIXED if fixed else 0) | (0 if auto_clear else FLAG_NO_AUTO_CLEAR)
+    return Config(seed, spp, max_depth, rr_depth, tile, tile, flags)
 
 
 def make_camera(position, yaw_deg=-90.0, pitch_deg=0.0, fovy_deg=45.0, aspect=1.0, znear=0.01, zfar=1e4,
@@ -426,6 +430,14 @@ class PathTracer:
         names = ("trips", "refills", "node_lanes", "tri_phases", "tri_lanes", "finish_trips", "idle_lanes",
                  "pop_trips", "pop_lanes", "slow_slab_trips", "finish_lanes", "_11")
         return {k: int(x) for k, x in zip(names, v)} if n > 0 else None
+
+    def debug_quot(self, a, b):
+        """a / b as the kernels divide (shared fp64 reciprocal, mcpt_core.hpp quot3)."""
+        a = np.ascontiguousarray(a, np.float32)
+        b = np.ascontiguousarray(b, np.float32)
+        out = np.empty_like(a)
+        self._ck(lib().mcpt_debug_quot(self.h, a.ctypes.data, b.ctypes.data, a.size, out.ctypes.data))
+        return out
 
     def queue_rays(self):
         """Rays of the current extension queue (diagnostics)."""

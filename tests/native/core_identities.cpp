@@ -4,7 +4,10 @@
 //   wrapi's conditional add/subtract == the modulo form for every i;
 //   upper_bound_guided == upper_bound on sorted CDF rows;
 //   (float)((double)x * (1.0 / (double)d)) == x / d for normal-range quotients (tri_test's
-//   fp32 replacement of the reference's fp64 island).
+//   fp32 replacement of the reference's fp64 island);
+//   quot_fp64(a, y) == a / b whenever it reports success, for y = 1/b off by up to 8 ulp of
+//   fp64 (the device's Newton-refined reciprocal is within ~1 ulp), over the full exponent
+//   range including overflow to inf and quotients at the subnormal boundary.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -78,6 +81,78 @@ int main() {
         if (bits(fast) != bits(ref) && bad++ < 5) std::printf("div %a / %a: %a vs %a\n", x, d, fast, ref);
     }
     std::printf("division pairs checked %ld\n", checked);
+    // rngf's fp32 form == the reference's (float)((double)d * 2^-32) for every d
+    for (uint64_t d = 0; d <= 0xFFFFFFFFull; d += (d < (1ull << 26) ? 1 : 997)) {
+        float f = (float)(uint32_t)d * 2.3283064365386962890625e-10f;
+        float ref = (float)((double)(uint32_t)d * 0.00000000023283064365386962890625);
+        if (bits(f) != bits(ref) && bad++ < 5) std::printf("rngf %llu\n", (unsigned long long)d);
+    }
+    // shared-reciprocal quotients (Recip / quot3 / tri_test on the device)
+    long qchecked = 0, qfallback = 0;
+    std::uniform_int_distribution<int> EA(-149, 127), EB(-149, 127), K(-8, 8);
+    for (long q = 0; q < 40000000; q++) {
+        const int mode = (int)(q % 5);
+        uint32_t ma = (q % 7 == 0) ? 0x7FFFFF : M(g), mb = (q % 13 == 0) ? 0x7FFFFF : M(g);
+        if (q % 17 == 0) mb = 0;  // power-of-two denominators
+        int ea = EA(g), eb;
+        if (mode == 0) eb = EB(g);                          // anything (overflow, underflow, subnormal b)
+        else if (mode == 1) eb = ea - (int)(g() % 40);      // large quotients
+        else if (mode == 2) eb = ea + 100 + (int)(g() % 30); // near the subnormal boundary
+        else eb = ea - 20 + (int)(g() % 40);                // the common case
+        if (eb < -149 || eb > 127) continue;
+        float a = std::ldexp(1.f + (float)ma / 8388608.f, ea), b = std::ldexp(1.f + (float)mb / 8388608.f, eb);
+        if (ea < -126) a = std::ldexp((float)(ma | 1), -149);  // subnormal operands
+        if (eb < -126) b = std::ldexp((float)(mb | 1), -149);
+        if (g() & 1) a = -a;
+        if (g() & 1) b = -b;
+        if (b == 0.f || !std::isfinite(a) || !std::isfinite(b)) continue;
+        double y = 1.0 / (double)b;
+        int k = K(g);
+        for (int i = 0; i < (k < 0 ? -k : k); i++) y = std::nextafter(y, k < 0 ? 0.0 : 2.0 * y);
+        float fast;
+        if (!quot_fp64(a, y, fast)) { qfallback++; continue; }
+        qchecked++;
+        float ref = a / b;
+        if (bits(fast) != bits(ref) && bad++ < 5) std::printf("quot %a / %a (k=%d): %a vs %a\n", a, b, k, fast, ref);
+    }
+    for (float a : {0.f, -0.f, 1.f, -3.f})  // signed zeros
+        for (float b : {1.f, -2.f, 1e-40f, -3e38f}) {
+            float fast;
+            if (quot_fp64(a, 1.0 / (double)b, fast) && bits(fast) != bits(a / b) && bad++ < 5)
+                std::printf("quot %a / %a: %a vs %a\n", a, b, fast, a / b);
+        }
+    std::printf("shared-reciprocal quotients checked %ld (fallback %ld)\n", qchecked, qfallback);
+    // hardest cases: a / b = M / 2^25 + 1 / (2^25 B) with M odd (a float rounding midpoint),
+    // i.e. |a/b - midpoint| = 1 / (M B) ~ 2^-49 relative, the minimum the argument allows.
+    // With y within 2 ulp (the device budget) every one must round right; perturbing y by
+    // 2^-45 must break some -- proof that these cases are near the boundary.
+    long hard = 0, broken = 0;
+    for (long q = 0; hard < 2000000 && q < 40000000; q++) {
+        uint32_t B = (uint32_t)(0x800000u | (M(g) | 1u));  // odd 24-bit
+        uint32_t inv = B;                                  // inverse of B mod 2^32 (Newton)
+        for (int i = 0; i < 5; i++) inv *= 2u - B * inv;
+        uint32_t Mv = (0u - inv) & 0x1FFFFFFu;             // M B == -1 (mod 2^25)
+        if (!(Mv & 0x1000000u)) continue;                  // M must have 25 bits
+        uint64_t num = (uint64_t)Mv * B + 1u;
+        if (num & 0x1FFFFFFu) continue;
+        uint64_t A = num >> 25;
+        if (A < 0x800000u || A > 0xFFFFFFu) continue;
+        int e = (int)(g() % 120) - 60;
+        float a = std::ldexp((float)A, e), b = std::ldexp((float)B, e);
+        hard++;
+        for (int k = -2; k <= 2; k++) {
+            double y = 1.0 / (double)b;
+            for (int i = 0; i < (k < 0 ? -k : k); i++) y = std::nextafter(y, k < 0 ? 0.0 : 2.0 * y);
+            float fast;
+            if (quot_fp64(a, y, fast) && bits(fast) != bits(a / b) && bad++ < 5)
+                std::printf("hard quot %a / %a (k=%d): %a vs %a\n", a, b, k, fast, a / b);
+        }
+        float wrong;
+        quot_fp64(a, (1.0 / (double)b) * (1.0 - std::ldexp(1.0, -45)), wrong);
+        if (bits(wrong) != bits(a / b)) broken++;
+    }
+    std::printf("hard quotients %ld, broken by a 2^-45 reciprocal error %ld\n", hard, broken);
+    if (hard < 100000 || broken == 0) { std::printf("hard-case generator ineffective\n"); bad++; }
     std::printf("bad=%ld\n", bad);
     return bad != 0;
 }

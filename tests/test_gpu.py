@@ -361,3 +361,77 @@ def test_cpp_example_batch_equals_reference_orchestration(tmp_path):
     a, b = read_pfm(tmp_path / "batch.pfm"), read_pfm(tmp_path / "tile.pfm")
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert read_png(tmp_path / "batch.png").shape == (256, 256, 3)
+
+
+def test_film_observes_camera_and_scene(mcpt_mod):
+    """Film::update -> clear() (Film.cu:278-281) on Camera::update / Scene::notify: a different
+    camera or a scene re-upload clears the film before the next iteration; the same camera does
+    not; MCPT_FLAG_NO_AUTO_CLEAR leaves clearing to the caller."""
+    from test_fixed_mode import cube_scene
+
+    s = cube_scene(mcpt_mod, False)
+    cam = mcpt_mod.make_camera((0.5, 0.7, 3.0))
+    cam2 = mcpt_mod.make_camera((0.4, 0.7, 3.0))
+    W = H = 32
+    for auto in (True, False):
+        pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=2, max_depth=3, auto_clear=auto))
+        pt.upload_scene(s)
+        pt.set_camera(cam)
+        pt.resize(W, H)
+        pt.render()
+        full = pt.film()[1].copy()
+        assert full[: H - 1, : W - 1].min() == 2
+        pt.set_camera(cam)  # unchanged camera: no notification
+        pt.iterate(1)
+        assert np.array_equal(pt.film()[1], full)
+        pt.set_camera(cam2)
+        pt.iterate(1)
+        smp = pt.film()[1]
+        if auto:
+            assert smp.max() <= 1 and smp.sum() < full.sum()
+        else:
+            assert np.array_equal(smp, full)
+        if auto:
+            pt.render()
+            pt.upload_scene(s)  # re-upload notifies the film
+            pt.iterate(1)
+            assert pt.film()[1].max() <= 1
+        pt.close()
+
+
+def test_device_division_is_ieee(mcpt_mod):
+    """The kernels divide by a shared fp64 reciprocal (mcpt_core.hpp Recip/quot3); on the device
+    that must equal IEEE fp32 division bit for bit: random pairs over the whole exponent range,
+    special values, and the hardest cases (a/b within ~2^-49 of a rounding midpoint)."""
+    g = np.random.default_rng(5)
+    n = 1 << 20
+    a = g.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    b = g.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    # near-1 quotients and signed zeros / infinities / NaN / subnormals
+    c = g.uniform(0.5, 2.0, n).astype(np.float32)
+    d = g.uniform(0.5, 2.0, n).astype(np.float32)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-40, 3.4e38, 1.0, -1.0], np.float32)
+    sa, sb = np.meshgrid(sp, sp)
+    # hard cases: A = (M B + 1) / 2^25 with M an odd 25-bit integer, so a/b sits 1/(M B) above a midpoint
+    B = (g.integers(0, 1 << 23, 4 * n) | (1 << 23) | 1).astype(np.uint64)
+    inv = B.copy()
+    for _ in range(6):
+        inv = (inv * (2 - B * inv)) & 0xFFFFFFFF
+    M = (-inv) & 0x1FFFFFF
+    ok = (M >> 24) == 1
+    A = (M * B + 1) >> 25
+    ok &= (((M * B + 1) & 0x1FFFFFF) == 0) & (A >= (1 << 23)) & (A < (1 << 24))
+    e = g.integers(-60, 60, ok.sum())
+    ha = np.ldexp(A[ok].astype(np.float64), e).astype(np.float32)
+    hb = np.ldexp(B[ok].astype(np.float64), e).astype(np.float32)
+    assert ha.size > 100000
+    aa = np.concatenate([a, c, sa.ravel(), ha])
+    bb = np.concatenate([b, d, sb.ravel(), hb])
+    pt = mcpt_mod.PathTracer(0)
+    got = pt.debug_quot(aa, bb)
+    with np.errstate(all="ignore"):
+        ref = aa / bb
+    nan = np.isnan(ref)
+    assert np.array_equal(np.isnan(got), nan)
+    assert np.array_equal(got[~nan].view(np.uint32), ref[~nan].view(np.uint32))
+    pt.close()
