@@ -3,7 +3,7 @@
 // INTEGRATION.md): build a BASELINE config scene with the host builder, upload it,
 // run the wavefront iterations until every pixel has its samples, write PNG + PFM.
 //
-//   mcpt_render <config 1-5> [spp] [out_prefix] [--gpu-bvh] [--fixed] [--tiles-per-call]
+//   mcpt_render <config 1-5> [spp] [out_prefix] [--gpu-bvh] [--reference-bvh] [--fixed] [--tiles-per-call]
 //
 // --tiles-per-call uses the reference orchestration (one 256x256 tile per call,
 // wavefront_kernels.cu:377-442 + Film::update_tile_position) instead of batch mode.
@@ -20,7 +20,7 @@ struct Cfg { int w, h, spp, depth; float pos[3], pitch; const char* env; };
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        fprintf(stderr, "usage: %s <config 1-5> [spp] [out_prefix] [--gpu-bvh] [--fixed] [--tiles-per-call]\n", argv[0]);
+        fprintf(stderr, "usage: %s <config 1-5> [spp] [out_prefix] [--gpu-bvh] [--reference-bvh] [--fixed] [--tiles-per-call]\n", argv[0]);
         return 2;
     }
     const Cfg cfgs[6] = {{0, 0, 0, 0, {0, 0, 0}, 0, ""},
@@ -34,9 +34,10 @@ int main(int argc, char** argv) {
     Cfg c = cfgs[id];
     if (argc > 2 && argv[2][0] != '-') c.spp = atoi(argv[2]);
     std::string out = (argc > 3 && argv[3][0] != '-') ? argv[3] : "mcpt_render";
-    bool gpu_bvh = false, fixed = false, per_tile = false;
+    bool gpu_bvh = false, ref_bvh = false, fixed = false, per_tile = false;
     for (int i = 2; i < argc; i++) {
         if (!strcmp(argv[i], "--gpu-bvh")) gpu_bvh = true;
+        if (!strcmp(argv[i], "--reference-bvh")) ref_bvh = true;
         if (!strcmp(argv[i], "--fixed")) fixed = true;
         if (!strcmp(argv[i], "--tiles-per-call")) per_tile = true;
     }
@@ -44,7 +45,9 @@ int main(int argc, char** argv) {
 
     // Scene::load + BVHAccel + EnvironmentLight (host builder)
     mcpt_scene* s = mcpt_scene_new();
-    if (!s || mcpt_scene_make_proxy(s, id, assets) || mcpt_scene_build(s, 8)) {
+    // host BVH: binned 3-axis SAH (default) or BVHAccel's builder; films are identical either way
+    mcpt_bvh_params bp = {MCPT_BVH_SAH3, 8, 128, 0.5f, 1.0f};
+    if (!s || mcpt_scene_make_proxy(s, id, assets) || (ref_bvh ? mcpt_scene_build(s, 8) : mcpt_scene_build_ex(s, &bp))) {
         fprintf(stderr, "scene: %s\n", mcpt_last_error(nullptr));
         return 1;
     }

@@ -82,6 +82,9 @@ typedef struct mcpt_scene_desc {
     const float *env_marginal_y;  /* env_h */
     const float *env_conds_y;     /* env_h*env_w */
     const float *env_pdf;         /* env_h*env_w */
+    const int32_t *tri_id;        /* optional ntri original triangle ids (NULL = array position): the
+                                     exact-t tie-break key and the id the trace API reports, so
+                                     neither depends on the order a BVH builder stored triangles in */
 } mcpt_scene_desc;
 
 /* dCamera (Camera.h:34-46): column-major m[c][r] = m[c*4+r]. */
@@ -190,6 +193,22 @@ int mcpt_scene_add_dir_light(mcpt_scene *s, const float *dir, const float *rgb, 
 int mcpt_scene_transform(mcpt_scene *s, const float *xform16);   /* bake a transform into all meshes */
 int mcpt_scene_make_proxy(mcpt_scene *s, int32_t config_id, const char *asset_dir); /* SURVEY.md 8d proxies */
 int mcpt_scene_build(mcpt_scene *s, int32_t max_prims_in_node);  /* SAH BVH (BVH.cu:84-333) + env tables */
+/* BVH builder choice.  Topology is not a parity contract (hits are tree-independent: conservative
+ * culling + (t, scene index) ties), so any builder gives identical films.
+ *   MCPT_BVH_REFERENCE: BVHAccel's SAH (BVH.cu:84-333) -- 12 buckets on the largest centroid axis,
+ *     cost .125 + (n0 A0 + n1 A1) / A; what mcpt_scene_build runs.
+ *   MCPT_BVH_SAH3: binned SAH over all three axes (buckets per axis), cost
+ *     trav_cost + isect_cost (n0 A0 + n1 A1) / A against a leaf cost isect_cost n. */
+#define MCPT_BVH_REFERENCE 0
+#define MCPT_BVH_SAH3 1
+typedef struct mcpt_bvh_params {
+    int32_t builder;      /* MCPT_BVH_* */
+    int32_t max_prims;    /* 1..8 triangles per leaf */
+    int32_t buckets;      /* SAH3: bins per axis (2..256) */
+    float trav_cost;      /* SAH3: cost of a node visit, relative to ... */
+    float isect_cost;     /* ... a triangle test */
+} mcpt_bvh_params;
+int mcpt_scene_build_ex(mcpt_scene *s, const mcpt_bvh_params *p); /* BVH + env tables */
 int mcpt_scene_get_desc(const mcpt_scene *s, mcpt_scene_desc *out); /* pointers owned by s */
 int mcpt_scene_bvh_depth(const mcpt_scene *s);
 int mcpt_camera_make(const mcpt_camera_params *p, mcpt_camera *out);

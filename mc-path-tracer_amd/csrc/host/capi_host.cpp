@@ -95,6 +95,13 @@ int mcpt_scene_build(mcpt_scene* s, int32_t max_prims_in_node) {
     return rc ? fail(s, rc, err) : MCPT_OK;
 }
 
+int mcpt_scene_build_ex(mcpt_scene* s, const mcpt_bvh_params* p) {
+    if (!s || !p) return fail(s, MCPT_E_INVALID, "null argument");
+    std::string err;
+    int rc = s->s.build(*p, err);
+    return rc ? fail(s, rc, err) : MCPT_OK;
+}
+
 int mcpt_scene_get_desc(const mcpt_scene* s, mcpt_scene_desc* out) {
     if (!s || !out) return MCPT_E_INVALID;
     if (!s->s.built) return fail(const_cast<mcpt_scene*>(s), MCPT_E_INVALID, "scene not built");

@@ -33,6 +33,7 @@ struct Scene {
     int bvh_depth = 0;
     std::vector<float> f_v0, f_v1, f_v2, f_n0, f_n1, f_n2;
     std::vector<int32_t> f_mat;
+    std::vector<int32_t> f_id;  // original triangle index of each BVH-ordered slot
     std::vector<float> node_bmin, node_bmax;
     std::vector<int32_t> node_offset, node_nprims, node_axis;
     std::string err;
@@ -43,6 +44,7 @@ struct Scene {
     int load_glb(const char* path, const float* xf16, std::string& err);
     int set_env_hdr(const char* path, int mode, std::string& err);
     int build(int max_prims, std::string& err);
+    int build(const mcpt_bvh_params& p, std::string& err);
     void desc(mcpt_scene_desc* d) const;
 };
 

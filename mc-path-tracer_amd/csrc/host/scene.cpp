@@ -573,6 +573,10 @@ struct Builder {
     std::vector<int> ordered;
     int max_prims;
     int max_depth = 0;
+    // mode 1 (MCPT_BVH_SAH3): binned SAH over all three axes with prefix/suffix sweeps,
+    // cost ct + ci (n0 A0 + n1 A1) / A against leaf cost ci n
+    int mode = 0, nb = 32;
+    double ct = 1.0, ci = 1.0;
     Builder(std::vector<PrimInfo>& i, int mp) : info(i), max_prims(mp) {}
 
     int leaf(int start, int end, const Bounds& b) {
@@ -582,8 +586,91 @@ struct Builder {
         nodes.push_back(n);
         return (int)nodes.size() - 1;
     }
+    int median_split(int start, int end, int dim) {
+        const int mid = (start + end) / 2;
+        std::nth_element(info.begin() + start, info.begin() + mid, info.begin() + end,
+                         [dim](const PrimInfo& a, const PrimInfo& c) {
+                             return comp(a.c, dim) < comp(c.c, dim) || (comp(a.c, dim) == comp(c.c, dim) && a.prim < c.prim);
+                         });
+        return mid;
+    }
+    int inner(int start, int mid, int end, int depth, int dim) {
+        int me = (int)nodes.size();
+        nodes.push_back(BuildNode());
+        int c0 = build(start, mid, depth + 1);
+        int c1 = build(mid, end, depth + 1);
+        nodes[me].child[0] = c0;
+        nodes[me].child[1] = c1;
+        nodes[me].axis = dim;
+        nodes[me].b = nodes[c0].b;
+        nodes[me].b.add(nodes[c1].b);
+        nodes[me].n = 0;
+        return me;
+    }
+    int build_sah3(int start, int end, int depth) {
+        Bounds b;
+        for (int i = start; i < end; i++) b.add(info[i].b);
+        const int np = end - start;
+        if (np == 1) return leaf(start, end, b);
+        Bounds cb;
+        for (int i = start; i < end; i++) cb.add(info[i].c);
+        const double A = b.area();
+        double best = 1e300;
+        int bdim = -1, bsplit = 0;
+        std::vector<int> cnt(nb);
+        std::vector<Bounds> bb(nb), right(nb);
+        for (int dim = 0; dim < 3; dim++) {
+            const float lo = comp(cb.mn, dim), hi = comp(cb.mx, dim);
+            if (!(hi > lo)) continue;
+            std::fill(cnt.begin(), cnt.end(), 0);
+            std::fill(bb.begin(), bb.end(), Bounds());
+            const double scale = (double)nb / ((double)hi - (double)lo);
+            for (int i = start; i < end; i++) {
+                int k = (int)(((double)comp(info[i].c, dim) - lo) * scale);
+                k = k < 0 ? 0 : (k >= nb ? nb - 1 : k);
+                cnt[k]++;
+                bb[k].add(info[i].b);
+            }
+            Bounds acc;
+            int rc = 0;
+            std::vector<int> rcnt(nb);
+            for (int k = nb - 1; k > 0; k--) {
+                acc.add(bb[k]);
+                rc += cnt[k];
+                right[k] = acc;
+                rcnt[k] = rc;
+            }
+            Bounds left;
+            int lc = 0;
+            for (int k = 0; k < nb - 1; k++) {
+                left.add(bb[k]);
+                lc += cnt[k];
+                const int r = rcnt[k + 1];
+                if (lc == 0 || r == 0) continue;
+                const double cost = ct + ci * ((double)lc * left.area() + (double)r * right[k + 1].area()) / A;
+                if (cost < best) { best = cost; bdim = dim; bsplit = k; }
+            }
+        }
+        if (bdim < 0) {  // all centroids coincide (or one bin): leaf, or an index split to bound leaf size
+            if (np <= max_prims) return leaf(start, end, b);
+            const int dim = b.max_extent();
+            return inner(start, median_split(start, end, dim), end, depth, dim);
+        }
+        if (np <= max_prims && ci * np <= best) return leaf(start, end, b);
+        const float lo = comp(cb.mn, bdim), hi = comp(cb.mx, bdim);
+        const double scale = (double)nb / ((double)hi - (double)lo);
+        auto it = std::partition(info.begin() + start, info.begin() + end, [&](const PrimInfo& p) {
+            int k = (int)(((double)comp(p.c, bdim) - lo) * scale);
+            k = k < 0 ? 0 : (k >= nb ? nb - 1 : k);
+            return k <= bsplit;
+        });
+        int mid = (int)(it - info.begin());
+        if (mid == start || mid == end) mid = median_split(start, end, bdim);
+        return inner(start, mid, end, depth, bdim);
+    }
     int build(int start, int end, int depth) {
         max_depth = std::max(max_depth, depth);
+        if (mode == 1) return build_sah3(start, end, depth);
         Bounds b;
         for (int i = start; i < end; i++) b.add(info[i].b);
         int np = end - start;
@@ -653,7 +740,20 @@ struct Builder {
 };
 
 int Scene::build(int max_prims, std::string& err) {
+    mcpt_bvh_params p{};
+    p.builder = MCPT_BVH_REFERENCE;
+    p.max_prims = max_prims;
+    return build(p, err);
+}
+
+int Scene::build(const mcpt_bvh_params& prm, std::string& err) {
+    const int max_prims = prm.max_prims;
     if (max_prims < 1 || max_prims > 8) { err = "max_prims must be 1..8"; return MCPT_E_INVALID; }
+    if (prm.builder != MCPT_BVH_REFERENCE && prm.builder != MCPT_BVH_SAH3) { err = "unknown BVH builder"; return MCPT_E_INVALID; }
+    if (prm.builder == MCPT_BVH_SAH3 && (prm.buckets < 2 || prm.buckets > 256 || !(prm.trav_cost >= 0.f) || !(prm.isect_cost > 0.f))) {
+        err = "SAH3 needs 2..256 buckets, trav_cost >= 0, isect_cost > 0";
+        return MCPT_E_INVALID;
+    }
     size_t T = tris.size();
     std::vector<PrimInfo> info(T);
     for (size_t i = 0; i < T; i++) {  // g_init_BVH_triangle_info (mesh_initialization_kernels.cu:63-83)
@@ -662,6 +762,12 @@ int Scene::build(int max_prims, std::string& err) {
         info[i].c = info[i].b.mn * 0.5f + info[i].b.mx * 0.5f;
     }
     Builder bld(info, max_prims);
+    if (prm.builder == MCPT_BVH_SAH3) {
+        bld.mode = 1;
+        bld.nb = prm.buckets;
+        bld.ct = prm.trav_cost;
+        bld.ci = prm.isect_cost;
+    }
     node_bmin.clear(); node_bmax.clear(); node_offset.clear(); node_nprims.clear(); node_axis.clear();
     bvh_depth = 0;
     if (T > 0) {
@@ -691,8 +797,10 @@ int Scene::build(int max_prims, std::string& err) {
     f_v0.resize(3 * N); f_v1.resize(3 * N); f_v2.resize(3 * N);
     f_n0.resize(3 * N); f_n1.resize(3 * N); f_n2.resize(3 * N);
     f_mat.resize(N);
+    f_id.resize(N);
     for (size_t i = 0; i < N; i++) {
-        const Tri& t = tris[bld.ordered.empty() ? i : (size_t)bld.ordered[i]];
+        f_id[i] = bld.ordered.empty() ? (int32_t)i : bld.ordered[i];
+        const Tri& t = tris[(size_t)f_id[i]];
         const V3* P = t.p;
         const V3* Nn = t.n;
         float* dst[6] = {&f_v0[3 * i], &f_v1[3 * i], &f_v2[3 * i], &f_n0[3 * i], &f_n1[3 * i], &f_n2[3 * i]};
@@ -725,6 +833,7 @@ void Scene::desc(mcpt_scene_desc* d) const {
     d->env_marginal_y = env_marginal_y.empty() ? nullptr : env_marginal_y.data();
     d->env_conds_y = env_conds_y.empty() ? nullptr : env_conds_y.data();
     d->env_pdf = env_pdf.empty() ? nullptr : env_pdf.data();
+    d->tri_id = f_id.empty() ? nullptr : f_id.data();
 }
 
 // ---------------------------------------------------------------------------

@@ -834,12 +834,15 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 float t, u, v;
                 bool done = false;
                 if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) &&
-                    !(t < 0.f)) {
+                    !(t < 0.f) &&
+                    (kind ? t < K_HUGE
+                          : (t < best ||
+                             (t == best && tri >= 0 && __float_as_int(w2.y) < __float_as_int(sc.tri[3 * tri + 2].y))))) {
                     if (kind) {
-                        if (t < K_HUGE) { tri = id; done = true; }  // occluded (tmax 1e32)
-                    } else if (t < best ||
-                               (t == best && __float_as_int(w2.y) < __float_as_int(sc.tri[3 * tri + 2].y))) {
-                        // exact-t ties go to the lower scene index (tri record .y of the
+                        tri = id;  // occluded (tmax 1e32)
+                        done = true;
+                    } else {
+                        // exact-t ties go to the lower triangle id (tri record .y of the
                         // third float4), whatever order the BVH build stored triangles in
                         best = t;
                         tri = id;

@@ -51,7 +51,7 @@ constexpr int kNodeF4 = kNodeWidth == 4 ? 8 : 4;  // float4 per node
 
 struct DevScene {
     const float4* nodes;    // BVH nodes (kNodeWidth children each, kNodeF4 x float4)
-    const float4* tri;      // 3 x float4: (v0.xyz, e1.x) (e1.yz, e2.xy) (e2.z, -, -, -)
+    const float4* tri;      // 3 x float4: (v0.xyz, e1.x) (e1.yz, e2.xy) (e2.z, id, -, -); id = tri_id bits
     const float4* tri_sh;   // 3 x float4: (n0.xyz, n1.x) (n1.yz, n2.xy) (n2.z, mat, -, -)
     float root_mn[3], root_mx[3];
     int root_ref;           // >= 0 pair node, < 0 leaf (0x80000000 | (count-1)<<24 | offset)

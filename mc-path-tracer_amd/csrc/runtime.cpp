@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -256,10 +257,49 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             if (d->offset[i] < 0 || d->offset[i] + d->nprims[i] > d->ntri) return set_err(c, MCPT_E_INVALID, "bad leaf range");
         }
     }
-    auto ref_of = [&](int j) -> int {
-        if (d->nprims[j] == 0) return pair_of[j];
-        return (int)(0x80000000u | ((uint32_t)(d->nprims[j] - 1) << 24) | (uint32_t)d->offset[j]);
+    // A leaf with several triangles becomes a small subtree of pair nodes whose leaves
+    // hold one triangle each, boxed by its own bounds (the vertex union,
+    // g_init_BVH_triangle_info).  A triangle then counts only if the line passes the
+    // leaf box and its own box -- BVHAccel's one-triangle-leaf semantics -- so results
+    // do not depend on how a builder grouped triangles (Moller-Trumbore alone can
+    // accept a grazing line just outside a triangle's box).  The oracle applies the
+    // same own-box test to multi-triangle leaves.
+    std::vector<float4> xn;  // expansion pairs, appended after the desc's pairs
+    auto tri_box = [&](int t0, int n, float mn[3], float mx[3]) {
+        for (int k = 0; k < 3; k++) { mn[k] = 3.402823466e+38f; mx[k] = -3.402823466e+38f; }
+        for (int t = t0; t < t0 + n; t++)
+            for (const float* v : {d->v0 + 3 * (size_t)t, d->v1 + 3 * (size_t)t, d->v2 + 3 * (size_t)t})
+                for (int k = 0; k < 3; k++) { mn[k] = std::fmin(mn[k], v[k]); mx[k] = std::fmax(mx[k], v[k]); }
     };
+    std::function<int(int, int)> expand = [&](int t0, int n) -> int {
+        if (n == 1) return (int)(0x80000000u | (uint32_t)t0);
+        const int m = n / 2;
+        const int me = npair + (int)(xn.size() / 4);
+        xn.resize(xn.size() + 4);
+        const int r0 = expand(t0, m), r1 = expand(t0 + m, n - m);
+        float a0[3], b0[3], a1[3], b1[3];
+        tri_box(t0, m, a0, b0);
+        tri_box(t0 + m, n - m, a1, b1);
+        float4* q = &xn[(size_t)(me - npair) * 4];
+        q[0] = make_float4(a0[0], a1[0], b0[0], b1[0]);
+        q[1] = make_float4(a0[1], a1[1], b0[1], b1[1]);
+        q[2] = make_float4(a0[2], a1[2], b0[2], b1[2]);
+        float fr0, fr1;
+        memcpy(&fr0, &r0, 4);
+        memcpy(&fr1, &r1, 4);
+        q[3] = make_float4(fr0, fr1, 0.f, 0.f);
+        return me;
+    };
+    std::vector<int> leaf_ref(N, 0);
+    int xdepth = 0;  // extra levels under a desc leaf
+    for (int i = 0; i < N; i++) {
+        if (d->nprims[i] == 0) continue;
+        leaf_ref[i] = expand(d->offset[i], d->nprims[i]);
+        int lv = 0;
+        while ((1 << lv) < d->nprims[i]) lv++;
+        xdepth = std::max(xdepth, lv);
+    }
+    auto ref_of = [&](int j) -> int { return d->nprims[j] == 0 ? pair_of[j] : leaf_ref[j]; };
     std::vector<float4> pn((size_t)npair * 4);
     for (int i = 0; i < N; i++) {
         if (d->nprims[i] != 0) continue;
@@ -278,6 +318,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         memcpy(&fax, &ax, 4);
         q[3] = make_float4(fr0, fr1, fax, 0.f);
     }
+    pn.insert(pn.end(), xn.begin(), xn.end());
     // depth of the tree = bound on stack pushes
     int depth = 0;
     if (N > 0) {
@@ -289,6 +330,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             if (d->nprims[n] == 0) { st.push_back({n + 1, dd + 1}); st.push_back({d->offset[n], dd + 1}); }
         }
     }
+    depth += xdepth;
     if (depth > kMaxStack) return set_err(c, MCPT_E_INVALID, "BVH deeper than the 64-entry traversal stack");
     c->pair_depth = depth;
     std::vector<float4> tri((size_t)d->ntri * 3), sh((size_t)d->ntri * 3);
@@ -297,8 +339,9 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         mcpt::V3 e1 = p1 - p0, e2 = p2 - p0;  // Triangle.cu:13-14
         tri[3 * i + 0] = make_float4(p0.x, p0.y, p0.z, e1.x);
         tri[3 * i + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+        const int32_t id = d->tri_id ? d->tri_id[i] : i;
         float fi;
-        memcpy(&fi, &i, 4);  // scene index: the traversal's tie-break key and the API's triangle id
+        memcpy(&fi, &id, 4);  // triangle id: the traversal's tie-break key and the API's triangle id
         tri[3 * i + 2] = make_float4(e2.z, fi, 0.f, 0.f);
         mcpt::V3 n0 = mcpt::ld3(d->n0, i), n1 = mcpt::ld3(d->n1, i), n2 = mcpt::ld3(d->n2, i);
         float fm;

@@ -621,25 +621,55 @@ static int box_hit(const or_scene *sc, int n, const ray_t *ray, v3 inv, const in
 
 typedef struct { uint64_t nodes, tris; } trav_stats;
 
+/* DEVIATION (tree independence): in a leaf with several triangles (and in the brute-force mode)
+ * a triangle's hit counts only if the line also passes its own bounding box (the vertex union,
+ * g_init_BVH_triangle_info, mesh_initialization_kernels.cu:63-83) under the same slab test --
+ * exactly the leaf test of BVHAccel's one-triangle leaves, so results do not depend on how a
+ * builder grouped triangles. */
+static int own_box_hit(const or_scene *sc, int id, const ray_t *ray, v3 inv, const int neg[3]) {
+    const float *a = sc->v0 + 3 * (int64_t)id, *b = sc->v1 + 3 * (int64_t)id, *c = sc->v2 + 3 * (int64_t)id;
+    float mn[3], mx[3];
+    for (int k = 0; k < 3; k++) {
+        mn[k] = fminf(fminf(a[k], b[k]), c[k]);
+        mx[k] = fmaxf(fmaxf(a[k], b[k]), c[k]);
+    }
+    float bx0 = neg[0] ? mx[0] : mn[0], bx1 = neg[0] ? mn[0] : mx[0];
+    float by0 = neg[1] ? mx[1] : mn[1], by1 = neg[1] ? mn[1] : mx[1];
+    float bz0 = neg[2] ? mx[2] : mn[2], bz1 = neg[2] ? mn[2] : mx[2];
+    float tmin = (bx0 - ray->o.x) * inv.x;
+    float tmax = (bx1 - ray->o.x) * inv.x;
+    float tymin = (by0 - ray->o.y) * inv.y;
+    float tymax = (by1 - ray->o.y) * inv.y;
+    if ((tmin > tymax) || (tymin > tmax)) return 0;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = (bz0 - ray->o.z) * inv.z;
+    float tzmax = (bz1 - ray->o.z) * inv.z;
+    if ((tmin > tzmax) || (tzmin > tmax)) return 0;
+    return 1;
+}
+static int tri_key(const or_scene *sc, int id) { return sc->tri_id ? sc->tri_id[id] : id; }
+
 /* intersect() (Triangle.cu:144-203).  Returns winning triangle or -1 and its t.
- * DEVIATION: exact-t ties go to the lower triangle index (order independent). */
+ * DEVIATION: exact-t ties go to the lower triangle id (order independent). */
 static int closest_hit(const or_scene *sc, const ray_t *ray, int traversal, float *tbest, trav_stats *st) {
     float tmin = K_HUGE;
     int best = -1;
+    v3 inv = V(1.f / ray->d.x, 1.f / ray->d.y, 1.f / ray->d.z);
+    int neg[3] = {inv.x < 0, inv.y < 0, inv.z < 0};
     if (traversal == 1) {
         for (int id = 0; id < sc->ntri; id++) {
             float u, v, t;
             st->tris++;
             if (tri_intersect(sc, id, ray, &u, &v, &t) && !(t < 0.f)) {
-                if (t < tmin || (t == tmin && id < best)) { tmin = t; best = id; }
+                if ((t < tmin || (t == tmin && best >= 0 && tri_key(sc, id) < tri_key(sc, best))) &&
+                    own_box_hit(sc, id, ray, inv, neg)) { tmin = t; best = id; }
             }
         }
         *tbest = tmin;
         return best;
     }
     if (sc->nnodes <= 0) { *tbest = tmin; return -1; }
-    v3 inv = V(1.f / ray->d.x, 1.f / ray->d.y, 1.f / ray->d.z);
-    int neg[3] = {inv.x < 0, inv.y < 0, inv.z < 0};
     int stack[128];
     int sp = 0, cur = 0;
     for (;;) {
@@ -652,7 +682,8 @@ static int closest_hit(const or_scene *sc, const ray_t *ray, int traversal, floa
                     float u, v, t;
                     st->tris++;
                     if (tri_intersect(sc, id, ray, &u, &v, &t) && !(t < 0.f)) {
-                        if (t < tmin || (t == tmin && id < best)) { tmin = t; best = id; }
+                        if ((t < tmin || (t == tmin && best >= 0 && tri_key(sc, id) < tri_key(sc, best))) &&
+                            (np == 1 || own_box_hit(sc, id, ray, inv, neg))) { tmin = t; best = id; }
                     }
                 }
                 if (sp == 0) break;
@@ -672,17 +703,18 @@ static int closest_hit(const or_scene *sc, const ray_t *ray, int traversal, floa
 
 /* intersect_shadows (Triangle.cu:204-243) with tmin = K_HUGE (Light.cu:12-16). */
 static int any_hit(const or_scene *sc, const ray_t *ray, int traversal, trav_stats *st) {
+    v3 inv = V(1 / ray->d.x, 1 / ray->d.y, 1 / ray->d.z);
+    int neg[3] = {inv.x < 0, inv.y < 0, inv.z < 0};
     if (traversal == 1) {
         for (int id = 0; id < sc->ntri; id++) {
             float u, v, t;
             st->tris++;
-            if (tri_intersect(sc, id, ray, &u, &v, &t) && !(t < 0.f) && t < K_HUGE) return 1;
+            if (tri_intersect(sc, id, ray, &u, &v, &t) && !(t < 0.f) && t < K_HUGE && own_box_hit(sc, id, ray, inv, neg))
+                return 1;
         }
         return 0;
     }
     if (sc->nnodes <= 0) return 0;
-    v3 inv = V(1 / ray->d.x, 1 / ray->d.y, 1 / ray->d.z);
-    int neg[3] = {inv.x < 0, inv.y < 0, inv.z < 0};
     int stack[128];
     int sp = 0, cur = 0;
     for (;;) {
@@ -694,7 +726,9 @@ static int any_hit(const or_scene *sc, const ray_t *ray, int traversal, trav_sta
                     int id = sc->offset[cur] + i;
                     float u, v, t;
                     st->tris++;
-                    if (tri_intersect(sc, id, ray, &u, &v, &t) && !(t < 0.f) && t < K_HUGE) return 1;
+                    if (tri_intersect(sc, id, ray, &u, &v, &t) && !(t < 0.f) && t < K_HUGE &&
+                        (np == 1 || own_box_hit(sc, id, ray, inv, neg)))
+                        return 1;
                 }
                 if (sp == 0) break;
                 cur = stack[--sp];
@@ -751,7 +785,7 @@ void or_trace_closest(const or_scene *sc, int32_t n, const float *ro, const floa
         pos_t[4 * i + 2] = is.position.z; pos_t[4 * i + 3] = is.t;
         nrm_mat[4 * i + 0] = is.normal.x; nrm_mat[4 * i + 1] = is.normal.y;
         nrm_mat[4 * i + 2] = is.normal.z; nrm_mat[4 * i + 3] = (float)is.mat;
-        tri[i] = id;
+        tri[i] = id >= 0 ? tri_key(sc, id) : -1;
     }
 }
 void or_trace_any(const or_scene *sc, int32_t n, const float *ro, const float *rd, int32_t traversal,

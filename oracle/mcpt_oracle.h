@@ -52,6 +52,7 @@ typedef struct or_scene {
     const float *env_marginal_y;    /* env_h                              */
     const float *env_conds_y;       /* env_h*env_w                        */
     const float *env_pdf;           /* env_h*env_w                        */
+    const int32_t *tri_id;          /* optional ntri triangle ids (tie key, reported id); NULL = index */
 } or_scene;
 
 typedef struct or_camera {

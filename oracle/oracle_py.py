@@ -25,7 +25,7 @@ class OrScene(C.Structure):
                 ("axis", _i), ("nmat", C.c_int32), ("mat_params", _f), ("ndir", C.c_int32), ("dir_params", _f),
                 ("env_mode", C.c_int32), ("env_color", C.c_float * 3), ("env_ls", C.c_float),
                 ("env_w", C.c_int32), ("env_h", C.c_int32), ("env_tex", _f), ("env_marginal_y", _f),
-                ("env_conds_y", _f), ("env_pdf", _f)]
+                ("env_conds_y", _f), ("env_pdf", _f), ("tri_id", _i)]
 
 
 class OrCamera(C.Structure):
@@ -112,6 +112,7 @@ def scene_struct(a: dict) -> OrScene:
     tex = np.asarray(a["env_tex"])
     s.env_h, s.env_w = (tex.shape[0], tex.shape[1]) if tex.size else (0, 0)
     s.env_tex, s.env_marginal_y, s.env_conds_y, s.env_pdf = (f(k) for k in ("env_tex", "env_marginal_y", "env_conds_y", "env_pdf"))
+    s.tri_id = i("tri_id") if "tri_id" in a and len(a["tri_id"]) else None
     s._keep = keep
     return s
 

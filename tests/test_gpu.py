@@ -435,3 +435,33 @@ def test_device_division_is_ieee(mcpt_mod):
     assert np.array_equal(np.isnan(got), nan)
     assert np.array_equal(got[~nan].view(np.uint32), ref[~nan].view(np.uint32))
     pt.close()
+
+
+def test_sah3_tree_same_results(mcpt_mod, oracle, scene_c2):
+    """The GPU on an SAH3 tree (multi-triangle leaves) == the oracle on the reference builder's
+    tree: vertex-grazing rays and a config-2 film band."""
+    from test_oracle import grazing_rays
+
+    a0 = mcpt_mod.build_config_scene(2, builder="reference").arrays()
+    s1 = mcpt_mod.build_config_scene(2, builder="sah3", buckets=16, trav_cost=2.0, isect_cost=1.0, max_prims=8)
+    assert s1.arrays()["nprims"].max() > 1
+    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=2, max_depth=5))
+    pt.upload_scene(s1)
+    ro, rd = grazing_rays(a0, 200000, 2)
+    gp, gn, gt = pt.trace_closest(ro, rd)
+    op_, on, ot = oracle.trace_closest(a0, ro, rd)
+    assert np.array_equal(gt, ot)
+    assert np.array_equal(gp.view(np.uint32), op_.view(np.uint32))
+    assert np.array_equal(gn.view(np.uint32), on.view(np.uint32))
+    assert np.array_equal(pt.trace_any(ro, rd), oracle.trace_any(a0, ro, rd))
+    rc = mcpt_mod.CONFIGS[2]
+    W, H = 160, 90
+    cam = mcpt_mod.config_camera(rc, W, H)
+    pt.set_camera(cam)
+    pt.resize(W, H)
+    pt.render()
+    Ld, smp = pt.film()
+    rL, rs, _ = oracle.render(a0, cam, W, H, 2, 5)
+    assert np.array_equal(smp, rs)
+    assert np.array_equal(Ld.view(np.uint32), np.asarray(rL).reshape(Ld.shape).view(np.uint32))
+    pt.close()

@@ -16,7 +16,7 @@ sys.path[:0] = [os.path.join(REPO, "mc-path-tracer_amd"), os.path.join(REPO, "or
 import mcpt  # noqa: E402
 import oracle_py as op  # noqa: E402
 
-OUT = os.path.join(REPO, "tests", "golden")
+OUT = os.environ.get("GOLDEN_OUT", os.path.join(REPO, "tests", "golden"))
 
 
 def rays(n, seed, box=3.0):
@@ -55,7 +55,7 @@ def main():
     # trace fixtures: 256 rays per scene, closest + any
     for name, arr in (("c1", a1), ("cube", ac)):
         ro, rd = rays(256, 7)
-        pt, nm, tri = op.trace_closest(arr, ro, rd)
+        pt, nm, tri = op.trace_closest(arr, ro, rd)  # tri: triangle ids (scene order, any BVH)
         vis = op.trace_any(arr, ro, rd)
         np.savez_compressed(os.path.join(OUT, f"trace_{name}_256.npz"), ro=ro, rd=rd, pos_t=pt, nrm_mat=nm, tri=tri, vis=vis)
     print("golden fixtures written to", OUT)
