@@ -7,7 +7,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 STEP=${1:-all}
 if [[ $STEP == all || $STEP == test ]]; then
-  timeout -k 10 900 python -m pytest tests/ -q -m gpu -x > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests/ -v -m gpu -x --timeout 300 --timeout-method thread> $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
   tail -3 $OUT/pytest_gpu.log
 fi
 if [[ $STEP == all || $STEP == bench ]]; then
