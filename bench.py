@@ -7,9 +7,10 @@ wavefront_kernels.cu:377-442: logic+generate+material -> extend -> shadow) over 
 rank owns; paths are in steady state after the warmup.  value = (extension + shadow + BRDF
 visibility rays of all ranks) / (max over ranks of the timed wall time).
 
-Multi-GPU: one process per GPU (torch.distributed.run), weak scaling: the frame is 1920 x 1080*N
-and 256x256 tiles are dealt to ranks by (tx + ty) mod N, so every rank owns ~1 frame of 1080p
-pixels.  No collective runs inside the timed region (tiles are independent); the RCCL gather of
+Multi-GPU: one process per GPU (torch.distributed.run), weak scaling: the film is 1920 x 1080*N
+pixels of the same 16:9 view (the config-2 camera; N-fold vertical supersampling), and 256x256
+tiles are dealt to ranks by (tx + ty) mod N, so every rank owns ~one 1080p frame of pixels with
+the same image content (sky / geometry mix) as the 1-GPU run.  No collective runs inside the timed region (tiles are independent); the RCCL gather of
 the film is a separate, untimed step (mcpt/parallel.py).
 """
 from __future__ import annotations
@@ -94,11 +95,19 @@ def main():
         import torch
 
     dist = None
+    # MCPT_BENCH_BACKEND=gloo + MCPT_BENCH_SHARE_GPU=1: rehearse the N-rank path on a 1-GPU box
+    # (every rank on device local % ndev, host-side collectives); the driver's runs use RCCL.
+    backend = os.environ.get("MCPT_BENCH_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
 
+        if os.environ.get("MCPT_BENCH_SHARE_GPU") == "1":
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     import numpy as np
 
     import mcpt
@@ -106,7 +115,7 @@ def main():
     rc = mcpt.CONFIGS[args.config]
     W, H = rc.width, rc.height * world
     scene = mcpt.build_config_scene(args.config)
-    cam = mcpt.config_camera(rc, W, H)
+    cam = mcpt.config_camera(rc, rc.width, rc.height)  # the 1080p view at any N (see docstring)
     pt = mcpt.PathTracer(local, mcpt.default_config(spp=rc.spp, max_depth=rc.max_depth))
     pt.upload_scene(scene)
     pt.set_camera(cam)
@@ -129,7 +138,7 @@ def main():
 
     rays = st.rays
     if dist:
-        v = torch.tensor([dt, float(rays)], dtype=torch.float64, device="cuda")
+        v = torch.tensor([dt, float(rays)], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         mx = v.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(v, op=dist.ReduceOp.SUM)

@@ -354,11 +354,16 @@ struct EnvView {
     const float* pdf;         // h*w
     // Optional search guides (device only, built at upload when the CDFs are
     // sorted): guide_m[k] = upper_bound(marginal_y, h, k / kEnvGuide), k = 0..kEnvGuide,
-    // and the same per conditional row at guide_c[y * (kEnvGuide + 1) + k].
-    const int* guide_m;
-    const int* guide_c;
+    // and the same per conditional row at guide_c[y * (kEnvGuide + 1) + k].  16-bit
+    // entries (tables up to 65535 wide/high): 256 x 1025 x 2 B = 512 KiB for a 512x256 map.
+    const uint16_t* guide_m;
+    const uint16_t* guide_c;
 };
-constexpr int kEnvGuide = 64;
+// Bins per guide table.  Each bin is equally likely (val uniform), and a bin holds W / G
+// CDF entries on average, so G = 1024 leaves ~0.5 (conditional rows, W = 512) and
+// ~0.25 (marginal, H = 256) bisection steps per search: the dependent-load chain of
+// env_dir is the guide fetch plus at most a step or two.
+constexpr int kEnvGuide = 1024;
 
 MCPT_HD int upper_bound(const float* list, int size, float val) {  // Helpers.cu:15-30
     int middle, left = 0, right = size;
@@ -374,10 +379,11 @@ MCPT_HD int upper_bound(const float* list, int size, float val) {  // Helpers.cu
 // precomputed: for val in [k/G, (k+1)/G) (exact bin: G is a power of two) the
 // answer lies in [guide[k], guide[k+1]] by monotonicity, and the same bisection
 // restricted to that range returns it.  val in [0, 1) (rand_float).
-MCPT_HD int upper_bound_guided(const float* list, const int* guide, float val) {
+template <class G>
+MCPT_HD int upper_bound_guided(const float* list, const G* guide, float val) {
     int k = (int)(val * (float)kEnvGuide);
     k = k < 0 ? 0 : (k > kEnvGuide - 1 ? kEnvGuide - 1 : k);
-    int left = guide[k], right = guide[k + 1];
+    int left = (int)guide[k], right = (int)guide[k + 1];
     while (left < right) {
         const int middle = (right - left) / 2 + left;
         if (val >= list[middle]) left = middle + 1;

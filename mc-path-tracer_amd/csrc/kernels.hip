@@ -212,6 +212,25 @@ __device__ inline void hit_record(const DevScene& sc, V3 o, V3 d, int tri, V3& p
 // Per path the arithmetic is the reference's, so which thread evaluates a path
 // does not change any result.
 // ---------------------------------------------------------------------------
+// Optional section profile of k_shade (diagnostics build, -DMCPT_SHADE_PROF): per
+// wave, the s_memtime cycles between section marks, summed per block in LDS and
+// folded into 64 shards of g_trace_prof (read back with mcpt_debug_trace_profile).
+#ifdef MCPT_SHADE_PROF
+__device__ unsigned long long g_trace_prof[64 * 12];
+__shared__ unsigned long long s_sprof[kBlock / 64][12];
+#define SPROF_T0() unsigned long long _sp_t = __builtin_readcyclecounter()
+#define SPROF(i)                                                                             \
+    do {                                                                                     \
+        const unsigned long long _n = __builtin_readcyclecounter();                          \
+        if ((threadIdx.x & 63) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1))           \
+            s_sprof[threadIdx.x >> 6][i] += _n - _sp_t;                                      \
+        _sp_t = _n;                                                                          \
+    } while (0)
+#else
+#define SPROF_T0() ((void)0)
+#define SPROF(i) ((void)0)
+#endif
+
 struct MatOut {
     bool want_ext, want_l, want_b, trivial_ext, vis_ray;
     uint32_t trivial_any;
@@ -228,6 +247,7 @@ template <bool FIXED>
 __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t samples, uint32_t len, V3 beta_store) {
     const DevScene& sc = a.scene;
     MatOut mo{false, false, false, false, false, 0u};
+    SPROF_T0();
     const Rng r{rng_key(a.seed, pid, samples), len};
     const V3 ro = xyz(a.p.ray_o[pid]), rdir = xyz(a.p.ray_d[pid]);
     V3 pos, n;
@@ -241,6 +261,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     if (light_id == 0) ldir = env_dir<FIXED>(sc.env, r);
     else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
     const V3 so_l = pos + n * 0.01f, sd_l = ldir;
+    SPROF(3);
     const Mat m = load_mat(sc.mats + 8 * mat);
     const bool delta = light_id > 0;
     V3 f_l = brdf_f(m, n, ldir, wo);
@@ -254,6 +275,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
     uint32_t nf = 0;
     if (wL > 0.f && pdfl_x > 0.f) nf |= F_CONDL;
+    SPROF(4);
     V3 cB = v3(0.f, 0.f, 0.f);
     V3 so_b = v3(0, 0, 0), sd_b = v3(0, 0, 0);
     if (!delta) {
@@ -274,12 +296,14 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
         mo.want_b = true;
         mo.vis_ray = true;
     }
+    SPROF(5);
     V3 wi_s = (r(SL_CONT_LOBE) < 0.5f) ? spec_get_wi<FIXED>(m, n, wo, r, SL_CONT_E0)
                                         : diff_get_wi<FIXED>(n, r, SL_CONT_E0);
     float pdf_s = brdf_pdf(m, n, wi_s, wo);
     V3 f_s = brdf_f(m, n, wi_s, wo);
     if ((f_s.x == 0.f && f_s.y == 0.f && f_s.z == 0.f) || pdf_s == 0.f) nf |= F_FZERO;
     V3 rr = f_s / pdf_s;
+    SPROF(6);
     const V3 new_o = pos + n * 0.001f;  // :358
     const V3 new_d = wi_s;
     a.p.beta[pid] = f4(beta_store, rr.x);
@@ -312,6 +336,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
             a.p.sray_d[2 * pid + 1] = f4(sd_b, 0.f);
         }
     }
+    SPROF(7);
     return mo;
 }
 
@@ -322,16 +347,18 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
 #endif
 template <bool FIXED>
 __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
-    __shared__ uint32_t s_pid[kBlock];      // pid | len << 24 of the block's continuing paths
-    __shared__ uint32_t s_samples[kBlock];
-    __shared__ float s_beta[3][kBlock];
-    __shared__ uint32_t s_wave_cnt[kBlock / 64];
     const DevScene& sc = a.scene;
     const int tile_px = a.tile_w * a.tile_h;
     const int bpt = (tile_px + kBlock - 1) / kBlock;
     const int tile = blockIdx.x / bpt;
     const int li = (blockIdx.x - tile * bpt) * kBlock + threadIdx.x;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+#ifdef MCPT_SHADE_PROF
+    const int wave = threadIdx.x >> 6;
+    if (threadIdx.x < kBlock / 64 * 12) s_sprof[threadIdx.x / 12][threadIdx.x % 12] = 0;
+    __syncthreads();
+#endif
+    SPROF_T0();
     bool valid = tile < a.ntiles && li < tile_px;
     uint32_t pid = 0;
     int x = 0, y = 0;
@@ -347,17 +374,27 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     uint32_t cont_len = 0, cont_samples = 0;
     V3 beta_store = v3(0.f, 0.f, 0.f);
     if (valid) {
+        // Every load the logic may need is issued up front, in one round: the
+        // per-path state unconditionally, the len-dependent streams (ray_d for a
+        // primary miss, the MIS terms and visibility for len > 1) at pid when needed
+        // and at a shared dummy index 0 otherwise (no extra bandwidth).
         const uint32_t fl = a.p.flags[pid];
         uint32_t samples = a.p.samples[pid];
+        const int32_t htri = a.p.hit_tri[pid];
+        const float4 b4 = a.p.beta[pid];
+        const float4 ld4 = a.p.Ld[pid];
+        const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
+        const bool need_rd = len == 1 && htri < 0;
+        const bool need_nee = len <= (uint32_t)a.max_depth && len > 1;
+        const float4 rd = a.p.ray_d[need_rd ? pid : 0u];
+        const float4 n0 = a.p.nee0[need_nee ? pid : 0u], n1 = a.p.nee1[need_nee ? pid : 0u];
+        const uchar2 vv = reinterpret_cast<const uchar2*>(a.p.vis)[need_nee ? pid : 0u];
         bool dead = (fl & F_DEAD) != 0;
         const uint32_t spp = (uint32_t)a.spp;
         if (!dead && samples < spp) {  // wavefront_kernels.cu:124
-            const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
             const Rng r{rng_key(a.seed, pid, samples), len};
-            const bool found = a.p.hit_tri[pid] >= 0;
-            float4 b4 = a.p.beta[pid];
+            const bool found = htri >= 0;
             const V3 B = xyz(b4);
-            float4 ld4 = a.p.Ld[pid];
             V3 film = xyz(ld4);
             bool terminate = false;
             beta_store = B;
@@ -365,15 +402,13 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
                 if (found) {
                     film = film + v3(0.f, 0.f, 0.f) * B;
                 } else {
-                    float4 rd = a.p.ray_d[pid];
                     const int nbg = FIXED ? 1 : sc.nlights;  // reference adds it once per light (A.4)
                     for (int i = 0; i < nbg; i++) film = film + env_L(sc.env, xyz(rd)) * B;
                 }
             }
             if (len > (uint32_t)a.max_depth || !found) terminate = true;  // :142-146
-            if (len <= (uint32_t)a.max_depth && len > 1) {                // :150-197
-                float4 n0 = a.p.nee0[pid], n1 = a.p.nee1[pid];
-                const uint8_t vl = a.p.vis[2 * pid], vb = a.p.vis[2 * pid + 1];
+            if (need_nee) {                                                // :150-197
+                const uint8_t vl = vv.x, vb = vv.y;
                 V3 acc = v3(0.f, 0.f, 0.f);
                 if ((fl & F_CONDL) && vl) acc = acc + xyz(n0);
                 if (fl & F_HASVIS) {
@@ -412,6 +447,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         }
         uint32_t nflags = fl;
         if (dead) nflags = F_DEAD;
+        SPROF(0);
         if (dead && samples < spp) {  // :219-222 + wf_generate (:225-251)
             const Rng r0{rng_key(a.seed, pid, samples), 0u};
             V3 new_o, new_d;
@@ -429,62 +465,104 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         }
         if (!cont && nflags != fl) a.p.flags[pid] = nflags;  // continuing paths: written by material()
     }
-    // ---- phase 2: compact the continuing paths onto the first threads of the block
+    SPROF(1);
+    // ---- pushes: generated extension rays and continuing paths (material queue); one
+    // atomic per block and queue.  A continuing path's updated throughput goes through
+    // p.beta to k_material (which rewrites it with f_s/pdf_s in .w).
+    if (cont) a.p.beta[pid] = f4(beta_store, 0.f);
+    const int shard = blockIdx.x % kShards;
+    uint32_t* sc_ctr = a.cnt->shard[shard];
     {
-        const uint64_t m = __ballot(cont);
-        const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (lane == 0) s_wave_cnt[wave] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t base = 0, ncont = 0;
-#pragma unroll
-        for (int w = 0; w < kBlock / 64; w++) {
-            const uint32_t c = s_wave_cnt[w];
-            base += (w < wave) ? c : 0u;
-            ncont += c;
-        }
-        if (cont) {
-            const uint32_t i = base + pre;
-            s_pid[i] = pid | (cont_len << 24);
-            s_samples[i] = cont_samples;
-            s_beta[0][i] = beta_store.x;
-            s_beta[1][i] = beta_store.y;
-            s_beta[2][i] = beta_store.z;
-        }
-        __syncthreads();
-        MatOut mo{false, false, false, false, false, 0u};
-        uint32_t mpid = 0;
-        if (threadIdx.x < ncont) {
-            const uint32_t e = s_pid[threadIdx.x];
-            mpid = e & 0xffffffu;
-            mo = material<FIXED>(a, mpid, s_samples[threadIdx.x], e >> 24,
-                          v3(s_beta[0][threadIdx.x], s_beta[1][threadIdx.x], s_beta[2][threadIdx.x]));
-        }
-        // ---- phase 3: queue pushes (one atomic per block and queue)
-        const int shard = blockIdx.x % kShards;
-        uint32_t* sc_ctr = a.cnt->shard[shard];
-        bool want[4] = {gen_ext, mo.want_ext, mo.want_l, mo.want_b};
-        uint32_t* ctr[4] = {sc_ctr + C_EXT, sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
-        uint32_t slot[4], total[4];
-        block_push<4>(want, ctr, slot, total);
+        bool want[2] = {gen_ext, cont};
+        uint32_t* ctr[2] = {sc_ctr + C_EXT, sc_ctr + C_MAT};
+        uint32_t slot[2], total[2];
+        block_push<2>(want, ctr, slot, total);
         if (gen_ext) a.ext_q[shard * a.ext_cap + slot[0]] = pid;
-        if (mo.want_ext) a.ext_q[shard * a.ext_cap + slot[1]] = mpid;
-        if (mo.want_l) a.any_q[shard * a.any_cap + slot[2]] = 2 * mpid;
-        if (mo.want_b) a.any_q[shard * a.any_cap + slot[3]] = 2 * mpid + 1;
-        // ray statistics: queued + resolved-in-place rays of each kind (per-wave reduce)
-        uint32_t n_ext = (gen_ext || gen_trivial ? 1u : 0u) + (mo.want_ext || mo.trivial_ext ? 1u : 0u);
-        uint32_t n_any = (mo.want_l ? 1u : 0u) + (mo.want_b ? 1u : 0u) + mo.trivial_any;
-        uint32_t n_vis = mo.vis_ray ? 1u : 0u;
-        for (int off = 32; off > 0; off >>= 1) {
-            n_ext += __shfl_xor(n_ext, off);
-            n_any += __shfl_xor(n_any, off);
-            n_vis += __shfl_xor(n_vis, off);
-        }
-        if (lane == 0) {
-            if (n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
-            if (n_any) atomicAdd(sc_ctr + C_ANY_RAYS, n_any);
-            if (n_vis) atomicAdd(sc_ctr + C_VIS, n_vis);
+        if (cont) a.mat_q[shard * a.ext_cap + slot[1]] = pid;
+    }
+    uint32_t n_ext = (gen_ext || gen_trivial) ? 1u : 0u;  // queued + resolved-in-place rays
+    for (int off = 32; off > 0; off >>= 1) n_ext += __shfl_xor(n_ext, off);
+    if (lane == 0 && n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
+    (void)cont_len;
+    (void)cont_samples;
+#ifdef MCPT_SHADE_PROF
+    {
+        unsigned long long _n = __builtin_readcyclecounter();
+        _sp_t = _n - _sp_t;  // pushes + statistics
+        if (lane == 0) { s_sprof[wave][2] += _sp_t; s_sprof[wave][11] += 1; }
+        __syncthreads();
+        if (threadIdx.x < 12) {
+            unsigned long long v = 0;
+            for (int w = 0; w < kBlock / 64; w++) v += s_sprof[w][threadIdx.x];
+            atomicAdd(&g_trace_prof[(blockIdx.x % 64) * 12 + threadIdx.x], v);
         }
     }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// k_material: light choice + wf_mat_mix (wavefront_kernels.cu:207-215, 295-375) for
+// the paths k_shade found continuing, dense over the material queue: 256 paths per
+// block and trip, so every wave of a block has the same (heavy) work and the block
+// pushes meet at the barrier together.  Block b serves shard b mod kShards, chunks
+// b / kShards, + gridDim.x / kShards, ... of it (grid from the occupancy calculator).
+// ---------------------------------------------------------------------------
+template <bool FIXED>
+__global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_material(ShadeArgs a) {
+    const uint32_t shard = blockIdx.x % kShards, w_in = blockIdx.x / kShards, bps = gridDim.x / kShards;
+    uint32_t* sc_ctr = a.cnt->shard[shard];
+    const uint32_t n = sc_ctr[C_MAT];
+    const int lane = threadIdx.x & 63;
+#ifdef MCPT_SHADE_PROF
+    if (threadIdx.x < kBlock / 64 * 12) s_sprof[threadIdx.x / 12][threadIdx.x % 12] = 0;
+    __syncthreads();
+    unsigned long long _t_mat = __builtin_readcyclecounter();
+#endif
+    uint32_t n_ext = 0, n_any = 0, n_vis = 0;
+    for (uint32_t base = w_in * kBlock; base < n; base += bps * kBlock) {  // block-uniform trip count
+        const uint32_t i = base + threadIdx.x;
+        MatOut mo{false, false, false, false, false, 0u};
+        uint32_t mpid = 0;
+        if (i < n) {
+            mpid = a.mat_q[shard * a.ext_cap + i];
+            const uint32_t fl = a.p.flags[mpid];
+            const float4 b4 = a.p.beta[mpid];
+            mo = material<FIXED>(a, mpid, a.p.samples[mpid], (fl >> F_LEN_SHIFT) & 0xffu, xyz(b4));
+        }
+        bool want[3] = {mo.want_ext, mo.want_l, mo.want_b};
+        uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
+        uint32_t slot[3], total[3];
+        block_push<3>(want, ctr, slot, total);
+        if (mo.want_ext) a.ext_q[shard * a.ext_cap + slot[0]] = mpid;
+        if (mo.want_l) a.any_q[shard * a.any_cap + slot[1]] = 2 * mpid;
+        if (mo.want_b) a.any_q[shard * a.any_cap + slot[2]] = 2 * mpid + 1;
+        n_ext += (mo.want_ext || mo.trivial_ext) ? 1u : 0u;  // queued + resolved-in-place rays
+        n_any += (mo.want_l ? 1u : 0u) + (mo.want_b ? 1u : 0u) + mo.trivial_any;
+        n_vis += mo.vis_ray ? 1u : 0u;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        n_ext += __shfl_xor(n_ext, off);
+        n_any += __shfl_xor(n_any, off);
+        n_vis += __shfl_xor(n_vis, off);
+    }
+    if (lane == 0) {
+        if (n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
+        if (n_any) atomicAdd(sc_ctr + C_ANY_RAYS, n_any);
+        if (n_vis) atomicAdd(sc_ctr + C_VIS, n_vis);
+    }
+#ifdef MCPT_SHADE_PROF
+    {
+        const int wave = threadIdx.x >> 6;
+        const unsigned long long _n = __builtin_readcyclecounter();
+        if (lane == 0) { s_sprof[wave][8] += _n - _t_mat; s_sprof[wave][10] += 1; }
+        __syncthreads();
+        if (threadIdx.x < 12) {
+            unsigned long long v = 0;
+            for (int w = 0; w < kBlock / 64; w++) v += s_sprof[w][threadIdx.x];
+            atomicAdd(&g_trace_prof[(blockIdx.x % 64) * 12 + threadIdx.x], v);
+        }
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -932,6 +1010,7 @@ __global__ void k_accumulate(CounterBlock* c) {  // fold per-iteration shard cou
     uint32_t er = c->shard[t][C_EXT_RAYS], ar = c->shard[t][C_ANY_RAYS];
     c->shard[t][C_EXT_RAYS] = 0;
     c->shard[t][C_ANY_RAYS] = 0;
+    c->shard[t][C_MAT] = 0;
     for (int off = 32; off > 0; off >>= 1) {
         er += __shfl_xor(er, off);
         ar += __shfl_xor(ar, off);
@@ -965,9 +1044,29 @@ __global__ void k_pack(PackArgs a) {  // tile-set pixels -> packed 16 B/px (for 
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+// Material grid: resident blocks (occupancy calculator x CUs) rounded down to a multiple of
+// the shard count (at least one block per shard).
+template <bool FIXED>
+static uint32_t material_blocks() {
+    static uint32_t b = [] {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_material<FIXED>, kBlock, 0);
+        if (cus <= 0) cus = 256;
+        if (per_cu <= 0) per_cu = 4;
+        return (uint32_t)std::max(1, cus * per_cu / kShards) * (uint32_t)kShards;
+    }();
+    return b;
+}
 void launch_shade(const ShadeArgs& a, int nblocks, bool fixed_mode, hipStream_t s) {
-    if (fixed_mode) hipLaunchKernelGGL(k_shade<true>, dim3(nblocks), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL(k_shade<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
+    if (fixed_mode) {
+        hipLaunchKernelGGL(k_shade<true>, dim3(nblocks), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(k_material<true>, dim3(material_blocks<true>()), dim3(kBlock), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_shade<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(k_material<false>, dim3(material_blocks<false>()), dim3(kBlock), 0, s, a);
+    }
 }
 // Persistent grid: resident waves per CU from the occupancy calculator
 // (MCPT_TRACE_WAVES overrides), rounded to a multiple of the shard count.
@@ -1012,7 +1111,16 @@ void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStre
 }
 
 int trace_profile(unsigned long long* out, int reset) {  // diagnostics build only
-#ifdef MCPT_TRACE_PROF
+#if defined(MCPT_SHADE_PROF)
+    static unsigned long long v[64 * 12];
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_trace_prof), sizeof(v)) != hipSuccess) return -1;
+    for (int i = 0; i < 12; i++) { out[i] = 0; for (int s = 0; s < 64; s++) out[i] += v[s * 12 + i]; }
+    if (reset) {
+        static unsigned long long z[64 * 12] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_trace_prof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 12;
+#elif defined(MCPT_TRACE_PROF)
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace_prof), sizeof(g_trace_prof)) != hipSuccess) return -1;
     if (reset) {
         unsigned long long z[12] = {};

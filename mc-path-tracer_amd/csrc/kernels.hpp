@@ -73,9 +73,9 @@ struct DevPaths {
 // roughly 90 atomics per microsecond, which is what ~24K pushes and ~100K
 // statistics adds per iteration would otherwise cost.
 constexpr int kShards = 64;
-enum : int { C_EXT = 0, C_ANY = 1, C_VIS = 2, C_STATS = 3, C_EXT_RAYS = 9, C_ANY_RAYS = 10, C_WORDS = 32 };  // C_STATS..+5
+enum : int { C_EXT = 0, C_ANY = 1, C_VIS = 2, C_STATS = 3, C_EXT_RAYS = 9, C_ANY_RAYS = 10, C_MAT = 11, C_WORDS = 32 };  // C_STATS..+5
 struct CounterBlock {
-    uint32_t shard[kShards][C_WORDS];  // [0] ext pushes [1] any-hit pushes [2] vis rays [3..8] traversal stats [9,10] rays
+    uint32_t shard[kShards][C_WORDS];  // [0] ext pushes [1] any-hit pushes [2] vis rays [3..8] traversal stats [9,10] rays [11] material pushes
     uint32_t last_ext, last_live, pad[30];
     uint32_t last_ext_shard[kShards];  // per-shard extension pushes of the last iteration
     unsigned long long tot_ext, tot_any, tot_vis, pad2;
@@ -90,7 +90,7 @@ struct ShadeArgs {
     int ntiles, tile_w, tile_h, W, H;
     int spp, max_depth, rr_depth;
     uint64_t seed;
-    uint32_t *ext_q, *any_q;
+    uint32_t *ext_q, *any_q, *mat_q;  // mat_q: continuing paths, k_shade -> k_material (ext_cap per shard)
     uint32_t ext_cap, any_cap;  // per-shard queue capacity
     CounterBlock* cnt;
 };

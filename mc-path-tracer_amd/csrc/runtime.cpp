@@ -51,7 +51,7 @@ struct mcpt_ctx {
     size_t P = 0;
     std::vector<void*> film_bufs;
     DevPaths p{};
-    uint32_t *ext_q = nullptr, *any_q = nullptr;
+    uint32_t *ext_q = nullptr, *any_q = nullptr, *mat_q = nullptr;
     uint32_t ext_cap = 0, any_cap = 0;  // per-shard capacities
     size_t queue_alloc = 0;             // entries allocated for ext_q (any_q holds twice)
     CounterBlock* cnt = nullptr;
@@ -149,6 +149,7 @@ void mcpt_destroy(mcpt_ctx* c) {
     if (c->tiles) (void)hipFree(c->tiles);
     if (c->ext_q) (void)hipFree(c->ext_q);
     if (c->any_q) (void)hipFree(c->any_q);
+    if (c->mat_q) (void)hipFree(c->mat_q);
     for (auto e : c->events) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -440,16 +441,17 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         bool ok = sorted(d->env_marginal_y, d->env_h);
         for (int y = 0; ok && y < d->env_h; y++) ok = sorted(d->env_conds_y + (size_t)y * d->env_w, d->env_w);
         s.env.guide_m = s.env.guide_c = nullptr;
-        if (ok) {
+        if (ok && d->env_w <= 65535 && d->env_h <= 65535) {
             const int G = mcpt::kEnvGuide;
-            std::vector<int> gm(G + 1), gc((size_t)d->env_h * (G + 1));
+            std::vector<uint16_t> gm(G + 1), gc((size_t)d->env_h * (G + 1));
             for (int k = 0; k <= G; k++) {
                 const float val = (float)k / (float)G;
-                gm[k] = mcpt::upper_bound(d->env_marginal_y, d->env_h, val);
+                gm[k] = (uint16_t)mcpt::upper_bound(d->env_marginal_y, d->env_h, val);
                 for (int y = 0; y < d->env_h; y++)
-                    gc[(size_t)y * (G + 1) + k] = mcpt::upper_bound(d->env_conds_y + (size_t)y * d->env_w, d->env_w, val);
+                    gc[(size_t)y * (G + 1) + k] =
+                        (uint16_t)mcpt::upper_bound(d->env_conds_y + (size_t)y * d->env_w, d->env_w, val);
             }
-            int *dgm, *dgc;
+            uint16_t *dgm, *dgc;
             if ((rc = dupload(c, c->scene_bufs, &dgm, gm.data(), gm.size()))) return rc;
             if ((rc = dupload(c, c->scene_bufs, &dgc, gc.data(), gc.size()))) return rc;
             s.env.guide_m = dgm;
@@ -490,10 +492,12 @@ static int set_tiles_internal(mcpt_ctx* c, const std::vector<int2>& t) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (c->ext_q) (void)hipFree(c->ext_q);
         if (c->any_q) (void)hipFree(c->any_q);
-        c->ext_q = c->any_q = nullptr;
+        if (c->mat_q) (void)hipFree(c->mat_q);
+        c->ext_q = c->any_q = c->mat_q = nullptr;
         c->queue_alloc = 0;
         if (hipMalloc(&c->ext_q, need * sizeof(uint32_t)) != hipSuccess ||
-            hipMalloc(&c->any_q, 2 * need * sizeof(uint32_t)) != hipSuccess)
+            hipMalloc(&c->any_q, 2 * need * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&c->mat_q, need * sizeof(uint32_t)) != hipSuccess)
             return set_err(c, MCPT_E_NOMEM, "queue allocation failed");
         c->queue_alloc = need;
     }
@@ -547,7 +551,10 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
         (rc = dalloc(c, c->film_bufs, &p.flags, P)) || (rc = dalloc(c, c->film_bufs, &p.samples, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.vis, 2 * P)))
         return rc;
-    c->ext_q = c->any_q = nullptr;
+    for (uint32_t** q : {&c->ext_q, &c->any_q, &c->mat_q}) {  // re-sized for the new tile set below
+        if (*q) (void)hipFree(*q);
+        *q = nullptr;
+    }
     c->queue_alloc = 0;
     HIPCHK(c, hipMemset(p.hit_tri, 0xff, P * sizeof(int32_t)));
     HIPCHK(c, hipMemset(p.vis, 0, 2 * P));
@@ -606,6 +613,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     sa.seed = c->cfg.seed;
     sa.ext_q = c->ext_q;
     sa.any_q = c->any_q;
+    sa.mat_q = c->mat_q;
     sa.ext_cap = c->ext_cap;
     sa.any_cap = c->any_cap;
     sa.cnt = c->cnt;

@@ -67,6 +67,9 @@ def gather_film(pt, rank, world, tile=256):
     _check(lib().mcpt_film_pack_tiles(pt.h, None, C.byref(n)), pt.h)
     local = torch.empty((n.value, 4), dtype=torch.float32, device="cuda")
     _check(lib().mcpt_film_pack_tiles(pt.h, C.c_void_p(local.data_ptr()), C.byref(n)), pt.h)
+    if dist.get_backend() != "nccl":  # gloo rehearsal: host-side collective
+        torch.cuda.synchronize()
+        local = local.cpu()
     parts = gather_packed(local, rank, world, dist)
     if rank != 0:
         return None
