@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=12, help="spp of the full-frame CPU-oracle sample")
     ap.add_argument("--gather", action="store_true", help="RCCL-gather the film after timing (N>1)")
+    ap.add_argument("--no-full-frame", action="store_true", help="skip the untimed-by-value full 256-spp frame")
     return ap.parse_args()
 
 
@@ -137,12 +138,29 @@ def main():
     dt = time.perf_counter() - t0
 
     rays = st.rays
+    # The literal workload once through, outside `value`: clear the film and render every
+    # pixel the rank owns to spp completion (startup and tail iterations included).
+    full = None
+    if not args.no_full_frame:
+        pt.clear()
+        if torch:
+            torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        fs = pt.render()
+        dt_full = time.perf_counter() - t1
+        full = [dt_full, float(fs.rays), float(fs.iterations)]
     if dist:
         v = torch.tensor([dt, float(rays)], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         mx = v.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(v, op=dist.ReduceOp.SUM)
         dt_all, rays_all = float(mx[0]), float(v[1])
+        if full:
+            f = torch.tensor(full, dtype=torch.float64, device=v.device)
+            fmax = f.clone()
+            dist.all_reduce(fmax, op=dist.ReduceOp.MAX)
+            dist.all_reduce(f, op=dist.ReduceOp.SUM)
+            full = [float(fmax[0]), float(f[1]), float(fmax[2])]
     else:
         dt_all, rays_all = dt, float(rays)
 
@@ -223,6 +241,11 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
     }
+    if full:
+        out["full_frame"] = {"seconds": round(full[0], 4), "rays": int(full[1]), "iterations": int(full[2]),
+                             "mray_s": round(full[1] / full[0] / 1e6, 2),
+                             "what": f"film cleared, every pixel rendered to {rc.spp} spp (max over ranks; host "
+                                     "syncs every 32 iterations, startup and tail included)"}
     print(json.dumps(out), flush=True)
     pt.close()
     if dist:

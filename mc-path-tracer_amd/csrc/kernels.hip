@@ -345,6 +345,11 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
 #else
 #define MCPT_SHADE_ATTR
 #endif
+#ifdef MCPT_MAT_WPE
+#define MCPT_MAT_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_MAT_WPE, MCPT_MAT_WPE)))
+#else
+#define MCPT_MAT_ATTR
+#endif
 template <bool FIXED>
 __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     const DevScene& sc = a.scene;
@@ -508,7 +513,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
 // b / kShards, + gridDim.x / kShards, ... of it (grid from the occupancy calculator).
 // ---------------------------------------------------------------------------
 template <bool FIXED>
-__global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_material(ShadeArgs a) {
+__global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) {
     const uint32_t shard = blockIdx.x % kShards, w_in = blockIdx.x / kShards, bps = gridDim.x / kShards;
     uint32_t* sc_ctr = a.cnt->shard[shard];
     const uint32_t n = sc_ctr[C_MAT];
@@ -634,7 +639,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         const TraceSet& ts = a.set[k];
-        n[k] = ts.count_ptr ? ts.count_ptr[shard * C_WORDS] : ts.count;
+        n[k] = __builtin_amdgcn_readfirstlane(ts.count_ptr ? ts.count_ptr[shard * C_WORDS] : ts.count);  // uniform
         const uint32_t nchunks = (n[k] + 63) >> 6;
         L[k] = w_in < nchunks ? ((nchunks - w_in + wps - 1) / wps) << 6 : 0u;  // this wave's share of set k
     }
@@ -1081,6 +1086,10 @@ static uint32_t persistent_waves() {
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace, kTraceBlock, 0);
+        // At most 7 waves per SIMD: on config 2 the launch takes 0.406 / 0.368 / 0.354 /
+        // 0.329 / 0.382 ms at 16 / 20 / 24 / 28 / 32 waves per CU (more resident rays
+        // thrash the per-CU L1 with unrelated node fetches past 28).
+        per_cu = std::min(per_cu, 28);
         if (const char* e = getenv("MCPT_TRACE_WAVES")) per_cu = atoi(e);
         if (cus <= 0) cus = 256;
         if (per_cu <= 0) per_cu = 16;

@@ -1,6 +1,7 @@
 """Summarise tools/pmc_trace.sh output: per kernel, counters averaged per dispatch."""
 import csv, glob, sys, collections
 def kname(k):
+    if 'k_material' in k: return 'material'
     if 'k_shade' in k: return 'shade'
     if 'k_trace' not in k: return None
     return ('any' if 'true' in k else 'closest') + ('_p' if 'trace_p' in k else '')
