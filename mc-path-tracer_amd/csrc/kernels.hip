@@ -255,34 +255,68 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     float t_hit;
     hit_record(sc, ro, rdir, a.p.hit_tri[pid], pos, n, mat, t_hit);
     const V3 wo = -rdir;
+    const Mat m = load_mat(sc.mats + 8 * mat);
+    SPROF(3);
+    // The three parts of wf_mat_mix draw from disjoint RNG slots and share only the hit
+    // record, so they are evaluated in the order that lets each store its results at
+    // once (short register live ranges): the continuation first (:353-358, its ratio
+    // f_s/pdf_s rides in the .w slots of beta/nee0/nee1), then the light sample
+    // (:316-329), then the BRDF sample (:331-343).
+    uint32_t nf = 0;
+    V3 rr;
+    {
+        V3 wi_s = (r(SL_CONT_LOBE) < 0.5f) ? spec_get_wi<FIXED>(m, n, wo, r, SL_CONT_E0)
+                                            : diff_get_wi<FIXED>(n, r, SL_CONT_E0);
+        float pdf_s = brdf_pdf(m, n, wi_s, wo);
+        V3 f_s = brdf_f(m, n, wi_s, wo);
+        if ((f_s.x == 0.f && f_s.y == 0.f && f_s.z == 0.f) || pdf_s == 0.f) nf |= F_FZERO;
+        rr = f_s / pdf_s;
+        const V3 new_o = pos + n * 0.001f;  // :358
+        a.p.beta[pid] = f4(beta_store, rr.x);
+        a.p.ray_o[pid] = f4(new_o, 0.f);
+        a.p.ray_d[pid] = f4(wi_s, 0.f);
+        mo.want_ext = true;
+        if (ray_misses_scene(sc, new_o, wi_s)) {  // resolved here: isect stays "not found"
+            a.p.hit_tri[pid] = -1;
+            mo.want_ext = false;
+            mo.trivial_ext = true;
+        }
+    }
+    SPROF(4);
     int l_id = (int)(r(SL_LIGHT) * (float)(sc.nlights - 0) + (float)0);
     const int light_id = (l_id == sc.nlights) ? 0 : l_id;
-    V3 ldir;
-    if (light_id == 0) ldir = env_dir<FIXED>(sc.env, r);
-    else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
-    const V3 so_l = pos + n * 0.01f, sd_l = ldir;
-    SPROF(3);
-    const Mat m = load_mat(sc.mats + 8 * mat);
     const bool delta = light_id > 0;
-    V3 f_l = brdf_f(m, n, ldir, wo);
-    V3 Li_l;
-    float pdfl_x;
-    light_L_pdf<FIXED>(sc, light_id, ldir, Li_l, pdfl_x);
     const float sel = FIXED ? 1.f / (float)sc.nlights : 1.f;  // light-selection pdf
-    if (FIXED) pdfl_x = pdfl_x * sel;
-    float pdfb_y = !delta ? brdf_pdf(m, n, ldir, wo) : (FIXED ? 0.f : 1.f);
-    float wL = power_heuristic(pdfl_x, pdfb_y);
-    V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
-    uint32_t nf = 0;
-    if (wL > 0.f && pdfl_x > 0.f) nf |= F_CONDL;
-    SPROF(4);
+    {
+        V3 ldir;
+        if (light_id == 0) ldir = env_dir<FIXED>(sc.env, r);
+        else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
+        V3 f_l = brdf_f(m, n, ldir, wo);
+        V3 Li_l;
+        float pdfl_x;
+        light_L_pdf<FIXED>(sc, light_id, ldir, Li_l, pdfl_x);
+        if (FIXED) pdfl_x = pdfl_x * sel;
+        float pdfb_y = !delta ? brdf_pdf(m, n, ldir, wo) : (FIXED ? 0.f : 1.f);
+        float wL = power_heuristic(pdfl_x, pdfb_y);
+        V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
+        if (wL > 0.f && pdfl_x > 0.f) nf |= F_CONDL;
+        a.p.nee0[pid] = f4(cL, rr.y);
+        const V3 so_l = pos + n * 0.01f;
+        if (ray_misses_scene(sc, so_l, ldir)) {
+            a.p.vis[2 * pid] = 1;
+            mo.trivial_any++;
+        } else {
+            a.p.sray_o[2 * pid] = f4(so_l, 0.f);
+            a.p.sray_d[2 * pid] = f4(ldir, 0.f);
+            mo.want_l = true;
+        }
+    }
+    SPROF(5);
     V3 cB = v3(0.f, 0.f, 0.f);
-    V3 so_b = v3(0, 0, 0), sd_b = v3(0, 0, 0);
     if (!delta) {
         V3 wi_b = (r(SL_MAT_LOBE) < 0.5f) ? spec_get_wi<FIXED>(m, n, wo, r, SL_MAT_E0)
                                            : diff_get_wi<FIXED>(n, r, SL_MAT_E0);
-        so_b = pos + wi_b * 0.001f;
-        sd_b = wi_b;
+        const V3 so_b = pos + wi_b * 0.001f;
         V3 f_b = brdf_f(m, n, wi_b, wo);
         V3 Li_b;
         float pdfl_y;
@@ -293,49 +327,19 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
         cB = ((f_b * Li_b) * wB) / pdfb_x;
         if (wB > 0.f && pdfb_x > 0.f) nf |= F_CONDB;
         nf |= F_HASVIS;
-        mo.want_b = true;
         mo.vis_ray = true;
-    }
-    SPROF(5);
-    V3 wi_s = (r(SL_CONT_LOBE) < 0.5f) ? spec_get_wi<FIXED>(m, n, wo, r, SL_CONT_E0)
-                                        : diff_get_wi<FIXED>(n, r, SL_CONT_E0);
-    float pdf_s = brdf_pdf(m, n, wi_s, wo);
-    V3 f_s = brdf_f(m, n, wi_s, wo);
-    if ((f_s.x == 0.f && f_s.y == 0.f && f_s.z == 0.f) || pdf_s == 0.f) nf |= F_FZERO;
-    V3 rr = f_s / pdf_s;
-    SPROF(6);
-    const V3 new_o = pos + n * 0.001f;  // :358
-    const V3 new_d = wi_s;
-    a.p.beta[pid] = f4(beta_store, rr.x);
-    a.p.nee0[pid] = f4(cL, rr.y);
-    a.p.nee1[pid] = f4(cB, rr.z);
-    a.p.flags[pid] = nf | ((len + 1) << F_LEN_SHIFT);  // extend increments len (:270)
-    a.p.ray_o[pid] = f4(new_o, 0.f);
-    a.p.ray_d[pid] = f4(new_d, 0.f);
-    mo.want_ext = true;
-    if (ray_misses_scene(sc, new_o, new_d)) {  // resolved here: isect stays "not found"
-        a.p.hit_tri[pid] = -1;
-        mo.want_ext = false;
-        mo.trivial_ext = true;
-    }
-    if (ray_misses_scene(sc, so_l, sd_l)) {
-        a.p.vis[2 * pid] = 1;
-        mo.trivial_any++;
-    } else {
-        a.p.sray_o[2 * pid] = f4(so_l, 0.f);
-        a.p.sray_d[2 * pid] = f4(sd_l, 0.f);
-        mo.want_l = true;
-    }
-    if (mo.want_b) {
-        if (ray_misses_scene(sc, so_b, sd_b)) {
+        if (ray_misses_scene(sc, so_b, wi_b)) {
             a.p.vis[2 * pid + 1] = 1;
-            mo.want_b = false;
             mo.trivial_any++;
         } else {
             a.p.sray_o[2 * pid + 1] = f4(so_b, 0.f);
-            a.p.sray_d[2 * pid + 1] = f4(sd_b, 0.f);
+            a.p.sray_d[2 * pid + 1] = f4(wi_b, 0.f);
+            mo.want_b = true;
         }
     }
+    a.p.nee1[pid] = f4(cB, rr.z);
+    a.p.flags[pid] = nf | ((len + 1) << F_LEN_SHIFT);  // extend increments len (:270)
+    SPROF(6);
     SPROF(7);
     return mo;
 }
