@@ -55,18 +55,18 @@ def tiles_for(rank, world, W, H, tile):
 
 
 def pmc_traffic(kernel_prefix):
-    """Per-launch HBM bytes for a kernel from the committed rocprofv3 PMC summary, if present."""
+    """Per-iteration HBM bytes of a stage from the committed rocprofv3 PMC summary, if present:
+    the sum over the stage's kernels (each launched once per iteration) of their bytes per launch."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json")))
     if not files:
         return None
     try:
         d = json.load(open(files[-1]))
-        for k, v in d.get("kernels", {}).items():
-            if any(k.startswith(p) or k.startswith("void " + p) for p in kernel_prefix):
-                return v.get("hbm_bytes_per_launch")
+        got = [v.get("hbm_bytes_per_launch") for k, v in d.get("kernels", {}).items()
+               if any(k.startswith(p) or k.startswith("void " + p) for p in kernel_prefix)]
+        return int(sum(got)) if got and None not in got else None
     except Exception:
         return None
-    return None
 
 
 def cpu_baseline(scene_arrays, cam, W, H, spp, max_depth):
@@ -183,7 +183,7 @@ def main():
     # dominant kernel by summed HIP-event time over the timed region (same stream as the kernels);
     # k_trace traces the extension (closest-hit) and any-hit rays of an iteration in one launch
     kern = {"k_trace": st.ms_extend + st.ms_shadow, "k_shade": st.ms_shade}
-    names = {"k_trace": ("mcpt_dev::k_trace(",), "k_shade": ("mcpt_dev::k_shade(", "mcpt_dev::k_shade<")}
+    names = {"k_trace": ("mcpt_dev::k_trace(",), "k_shade": ("mcpt_dev::k_shade<", "mcpt_dev::k_material<")}
     dom = max(kern, key=kern.get)
     byts = b_ext + b_any if dom == "k_trace" else b_shd
     state = (B_EXT_STATE * st.extend_rays + B_ANY_STATE * (st.shadow_rays + st.vis_rays)) if dom == "k_trace" else b_shd
