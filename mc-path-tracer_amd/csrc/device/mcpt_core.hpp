@@ -597,6 +597,57 @@ MCPT_HD float brdf_pdf(const Mat& m, V3 n, V3 wi, V3 wo) {  // (diff + spec) * 0
     return (diff_get_pdf() + spec_get_pdf(m, n, wi, wo)) * 0.5f;
 }
 
+// Lobe-merged sampler: spec_get_wi (spec) or diff_get_wi (!spec) with their common tail
+// -- the phi rotation, the gram_schmidt frame and the frame transform -- written once, so
+// a wave whose lanes picked different lobes runs that tail once instead of in both
+// branches.  Per lane the operations are exactly those of the function it selects
+// (2.f * PI_F == TWO_PI_F; the diffuse "theta" terms are sqrt(1 - e0^2) and e0).
+template <bool FIXED = false>
+MCPT_HD V3 brdf_sample_wi(const Mat& m, V3 N, V3 wo, const Rng& r, uint32_t s0, bool spec) {
+    float e0 = r(s0 + 0);
+    float e1 = r(s0 + 1);
+    float st, ct;
+    if (spec) {
+        float rr = m.rough;
+        float a2 = ((rr * rr) * rr) * rr;
+        float theta = dacos(__builtin_sqrtf((1.f - e0) / (e0 * (a2 - 1.f) + 1.f)));
+        dsincos(theta, st, ct);
+    } else {
+        st = __builtin_sqrtf(1.f - e0 * e0);
+        ct = e0;
+    }
+    float phi = TWO_PI_F * e1;
+    float sp, cp;
+    dsincos(phi, sp, cp);
+    float x = st * cp;
+    float z = st * sp;
+    V3 T = gram_schmidt<FIXED>(N, r, s0 + 2);
+    V3 B = normalize(cross(N, T));
+    V3 v = normalize((T * x + N * ct) + B * z);
+    if (spec) v = normalize(reflect(-wo, v));
+    return v;
+}
+// brdf_f and brdf_pdf of one direction with their shared terms evaluated once: the half
+// vector, f0, D, F and n.wi (same operations and values as the separate calls).
+MCPT_HD void brdf_f_pdf(const Mat& m, V3 n, V3 wi, V3 wo, V3& f, float& pdf) {
+    V3 wh = normalize(wo + wi);
+    V3 f0 = mix(m.fresnel, m.base, m.metal);
+    float n_dot_wi = fmx(dot(n, wi), BRDF_EPS);
+    float n_dot_wo = fmx(dot(n, wo), BRDF_EPS);
+    float D = ndf_ggx_tr(n, wh, m.rough);
+    float G = g1_schlick_ggx(wi, n, m.rough) * g1_schlick_ggx(wo, n, m.rough);
+    V3 F = fresnel_schlick(f0, wh, wo);
+    V3 L = (F * (D * G)) * n_dot_wi;
+    V3 fs = L / fmx((4.f * n_dot_wo) * n_dot_wi, BRDF_EPS);    // spec_get_f
+    V3 kD = (v3(1.f, 1.f, 1.f) - F) * (1.f - m.metal);
+    V3 fd = ((kD * m.base) * n_dot_wi) * ONE_PI_F;            // diff_get_f
+    f = fs + fd;
+    float wh_dot_n = fmx(dot(wh, n), BRDF_EPS);
+    float wo_dot_wh = fmx(dot(wo, wh), BRDF_EPS);
+    float ps = (D * wh_dot_n) / fmx(4.f * wo_dot_wh, BRDF_EPS);  // spec_get_pdf
+    pdf = (diff_get_pdf() + ps) * 0.5f;
+}
+
 // ---------------------------------------------------------------------------
 // Camera (Camera.cu:18-45, Sample.cu:129-149).
 // ---------------------------------------------------------------------------

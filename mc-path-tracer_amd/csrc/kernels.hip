@@ -265,10 +265,10 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     uint32_t nf = 0;
     V3 rr;
     {
-        V3 wi_s = (r(SL_CONT_LOBE) < 0.5f) ? spec_get_wi<FIXED>(m, n, wo, r, SL_CONT_E0)
-                                            : diff_get_wi<FIXED>(n, r, SL_CONT_E0);
-        float pdf_s = brdf_pdf(m, n, wi_s, wo);
-        V3 f_s = brdf_f(m, n, wi_s, wo);
+        V3 wi_s = brdf_sample_wi<FIXED>(m, n, wo, r, SL_CONT_E0, r(SL_CONT_LOBE) < 0.5f);  // spec : diff
+        float pdf_s;
+        V3 f_s;
+        brdf_f_pdf(m, n, wi_s, wo, f_s, pdf_s);
         if ((f_s.x == 0.f && f_s.y == 0.f && f_s.z == 0.f) || pdf_s == 0.f) nf |= F_FZERO;
         rr = f_s / pdf_s;
         const V3 new_o = pos + n * 0.001f;  // :358
@@ -291,12 +291,14 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
         V3 ldir;
         if (light_id == 0) ldir = env_dir<FIXED>(sc.env, r);
         else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
-        V3 f_l = brdf_f(m, n, ldir, wo);
+        V3 f_l;
+        float pdf_bl;
+        brdf_f_pdf(m, n, ldir, wo, f_l, pdf_bl);
         V3 Li_l;
         float pdfl_x;
         light_L_pdf<FIXED>(sc, light_id, ldir, Li_l, pdfl_x);
         if (FIXED) pdfl_x = pdfl_x * sel;
-        float pdfb_y = !delta ? brdf_pdf(m, n, ldir, wo) : (FIXED ? 0.f : 1.f);
+        float pdfb_y = !delta ? pdf_bl : (FIXED ? 0.f : 1.f);
         float wL = power_heuristic(pdfl_x, pdfb_y);
         V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
         if (wL > 0.f && pdfl_x > 0.f) nf |= F_CONDL;
@@ -314,15 +316,15 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     SPROF(5);
     V3 cB = v3(0.f, 0.f, 0.f);
     if (!delta) {
-        V3 wi_b = (r(SL_MAT_LOBE) < 0.5f) ? spec_get_wi<FIXED>(m, n, wo, r, SL_MAT_E0)
-                                           : diff_get_wi<FIXED>(n, r, SL_MAT_E0);
+        V3 wi_b = brdf_sample_wi<FIXED>(m, n, wo, r, SL_MAT_E0, r(SL_MAT_LOBE) < 0.5f);  // spec : diff
         const V3 so_b = pos + wi_b * 0.001f;
-        V3 f_b = brdf_f(m, n, wi_b, wo);
+        V3 f_b;
+        float pdfb_x;
+        brdf_f_pdf(m, n, wi_b, wo, f_b, pdfb_x);
         V3 Li_b;
         float pdfl_y;
         light_L_pdf<FIXED>(sc, light_id, wi_b, Li_b, pdfl_y);
         if (FIXED) pdfl_y = pdfl_y * sel;
-        float pdfb_x = brdf_pdf(m, n, wi_b, wo);
         float wB = power_heuristic(pdfb_x, pdfl_y);
         cB = ((f_b * Li_b) * wB) / pdfb_x;
         if (wB > 0.f && pdfb_x > 0.f) nf |= F_CONDB;
