@@ -635,22 +635,72 @@ constexpr int kNodeSteps = MCPT_NODE_STEPS;
 #else
 #define MCPT_TRACE_ATTR
 #endif
+#ifdef MCPT_WAVE_TIMES
+__device__ unsigned long long g_wave_t[4 * 16384];  // per wave: s_memrealtime (100 MHz, chip-wide) at entry and
+                                                     // exit, partition, time its partition ran dry for it
+#endif
 __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs a) {
+#ifdef MCPT_WAVE_TIMES
+    if (threadIdx.x == 0 && blockIdx.x < 16384) g_wave_t[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
     __shared__ int2 stk[kLdsStack][kTraceBlock];
     const int lane = threadIdx.x;
-    const uint32_t nsh = (uint32_t)a.nshards;
-    const uint32_t wps = gridDim.x / nsh;  // waves per shard (host: gridDim.x % nsh == 0)
-    const uint32_t shard = blockIdx.x % nsh, w_in = blockIdx.x / nsh;
-    uint32_t n[2], L[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const TraceSet& ts = a.set[k];
-        n[k] = __builtin_amdgcn_readfirstlane(ts.count_ptr ? ts.count_ptr[shard * C_WORDS] : ts.count);  // uniform
-        const uint32_t nchunks = (n[k] + 63) >> 6;
-        L[k] = w_in < nchunks ? ((nchunks - w_in + wps - 1) / wps) << 6 : 0u;  // this wave's share of set k
+    // ---- work distribution.  The chip's L2 is per XCD (not coherent with the others
+    // inside a launch), so the queue shards are split into one partition per XCD
+    // (shard s -> partition s mod nparts) and the waves running on an XCD hand out the
+    // 64-ray chunks of its partition with an atomic counter in that XCD's L2
+    // (workgroup-scope atomics are performed in the L2 the XCD's CUs share; the
+    // partition is chosen by the hardware XCC id, so every atomic on a counter runs in
+    // the same L2).  A static split left the waves of a launch finishing anywhere
+    // between 52 % and 100 % of its duration (tools/wave_times.py).
+    const uint32_t nsh = (uint32_t)a.nshards, nparts = a.nparts;
+    uint32_t part = 0;
+    if (nparts > 1) {
+        uint32_t xcc;
+        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        part = (xcc & 15u) % nparts;
     }
-    const uint32_t Ltot = L[0] + L[1];
-    if (Ltot == 0) return;
+    // Partition entries: its shards part, part + nparts, ... (spart of them) of set 0,
+    // then the same shards of set 1 (at most 2 * 64 entries: one per lane and half),
+    // read as one sequence of rays.  pre(e) = first position of entry e (exclusive prefix;
+    // entries past the last and pre(128)
+    // give the total), kept in LDS (s_pre): the kernel has to stay at <= 64 VGPRs for 7
+    // waves per SIMD (gfx950 allocates VGPRs in blocks of 16 here: 65..80 -> 6 waves).
+    // Rays are handed out exactly as lanes fall idle (an atomic add of the idle count):
+    // a wave reserves no rays ahead, so when the partition runs dry each wave only
+    // finishes its lanes.
+    __shared__ uint32_t s_pre[129];
+    const uint32_t spart = nsh > part ? (nsh - part + nparts - 1) / nparts : 0u;
+    uint32_t T;  // rays in the partition
+    {
+        uint32_t ne[2], inc[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t e = (uint32_t)lane + 64u * h;
+            const bool k1 = e >= spart;
+            const uint32_t j = k1 ? e - spart : e;
+            ne[h] = 0;
+            if (e < 2 * spart) {
+                const TraceSet& ts = k1 ? a.set[1] : a.set[0];
+                const uint32_t sh = part + j * nparts;
+                ne[h] = ts.count_ptr ? ts.count_ptr[sh * C_WORDS] : (sh == 0 ? ts.count : 0u);
+            }
+            inc[h] = ne[h];
+            for (int off = 1; off < 64; off <<= 1) {  // inclusive scan over the lanes
+                const uint32_t v = __shfl_up(inc[h], off);
+                if (lane >= off) inc[h] += v;
+            }
+        }
+        const uint32_t t0 = __shfl(inc[0], 63);
+        T = __builtin_amdgcn_readfirstlane(t0 + __shfl(inc[1], 63));
+        s_pre[lane] = inc[0] - ne[0];
+        s_pre[64 + lane] = t0 + inc[1] - ne[1];
+        if (lane == 0) s_pre[128] = T;
+        __syncthreads();
+    }
+    if (T == 0) return;
+    uint32_t* const grab = a.grab + part * C_WORDS;
+    bool more = true;  // the partition may still hold rays
     const DevScene& sc = a.scene;
 
     // per-lane work counters per set (wave-reduced at exit); per-ray step counts only in
@@ -664,7 +714,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #define RAY_STEP_NODE() ((void)0)
 #define RAY_STEP_TRI() ((void)0)
 #endif
-    uint32_t next = 0;  // wave-uniform position in the sequence
     bool act = false;
     int kind = 0;  // 0 closest, 1 any
     uint32_t rid = 0;
@@ -715,25 +764,34 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #endif
     for (;;) {
         PROF_ADD(0, 1);
-        // ---- refill idle lanes from the wave's sequence
+        // ---- refill idle lanes with the partition's next rays
         const uint64_t idle = __ballot(!act);
         const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (next < Ltot && (nidle >= a.refill_min || nidle == 64u)) {
+        if (more && (nidle >= a.refill_min || nidle == 64u)) {
+            uint32_t p0 = 0;
+            if (lane == 0) p0 = __hip_atomic_fetch_add(grab, nidle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p0 = __builtin_amdgcn_readfirstlane(p0);
+            if (p0 + nidle >= T) more = false;  // the rest of the partition is taken
+            const uint32_t q = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+            const uint32_t pos = p0 + q;  // meaningful on idle lanes
+            // entry of the first position: the last e with pre(e) <= p0 (a non-empty one)
+            const uint32_t e0 = p0 < T ? (uint32_t)__popcll(__ballot(s_pre[lane] <= p0)) +
+                                             (uint32_t)__popcll(__ballot(s_pre[64 + lane] <= p0)) - 1u
+                                       : 0u;
             if (!act) {
-                const uint32_t q = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                uint32_t s = next + q;
-                kind = s >= L[0];
-                const uint32_t nk = kind ? n[1] : n[0];
-                if (kind) s -= L[0];
-                const uint32_t k = (w_in + (s >> 6) * wps) * 64u + (s & 63u);
-                if (s < (kind ? L[1] : L[0]) && k < nk) {
+                if (pos < T) {
+                    uint32_t my_e = e0;
+                    while (pos >= s_pre[my_e + 1]) my_e++;  // the grab spans entries (rarely a step)
+                    const uint32_t my_pre = s_pre[my_e];
+                    kind = my_e >= spart;
+                    const uint32_t sh = part + (kind ? my_e - spart : my_e) * nparts;
+                    const uint32_t qslot = sh * (kind ? a.set[1].shard_cap : a.set[0].shard_cap) + (pos - my_pre);
                     // select the set's fields with ternaries: indexing a.set[kind] with a
                     // per-lane kind makes hipcc fetch them from kernarg memory per lane
                     const uint32_t* qp = kind ? a.set[1].queue : a.set[0].queue;
                     const float4* rop = kind ? a.set[1].ro : a.set[0].ro;
                     const float4* rdp = kind ? a.set[1].rd : a.set[0].rd;
-                    const uint32_t qslot = shard * (kind ? a.set[1].shard_cap : a.set[0].shard_cap) + k;
 #ifdef MCPT_RAY_STEPS
                     qi = qslot;
 #endif
@@ -773,11 +831,13 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     }
                 }
             }
-            next += nidle;
+#ifdef MCPT_WAVE_TIMES
+            if (!more && lane == 0 && blockIdx.x < 16384) g_wave_t[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
+#endif
             PROF_ADD(1, 1);
         }
         if (__ballot(act) == 0) {
-            if (next >= Ltot) break;
+            if (!more) break;
             continue;
         }
         // ---- node phase: up to kNodeSteps child-pair tests per lane holding an
@@ -958,6 +1018,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #endif
     wave_stats(a.set[0].stats, lane, tot_n0, tot_t0, tot_h0);
     wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);
+#ifdef MCPT_WAVE_TIMES
+    if (threadIdx.x == 0 && blockIdx.x < 16384) {
+        g_wave_t[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        g_wave_t[4 * blockIdx.x + 2] = part;
+    }
+#endif
 }
 
 __global__ void k_hit_record(HitRecordArgs a) {  // stage_run(EXTEND) outputs
@@ -1018,6 +1084,7 @@ __global__ void k_accumulate(CounterBlock* c) {  // fold per-iteration shard cou
 #pragma unroll
     for (int k = 0; k < C_STATS + 6; k++)
         for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    if (t < kMaxParts) c->grab[t][0] = 0;  // k_trace chunk hand-out counters
     uint32_t er = c->shard[t][C_EXT_RAYS], ar = c->shard[t][C_ANY_RAYS];
     c->shard[t][C_EXT_RAYS] = 0;
     c->shard[t][C_ANY_RAYS] = 0;
@@ -1110,6 +1177,13 @@ void launch_trace(const TraceArgs& args, hipStream_t s) {
     static const uint32_t tri_min = env_u32("MCPT_TRI_MIN", 16, 0, 64);
     a.refill_min = refill_min;
     a.tri_min = tri_min;
+    static const uint32_t nparts = [] {  // one work partition per XCD (L2 domain)
+        int dev = 0, nx = 1;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess) nx = 1;
+        return (uint32_t)std::min(kMaxParts, std::max(1, nx));
+    }();
+    a.nparts = nparts;
     const uint32_t nsh = (uint32_t)a.nshards;
     const uint32_t wps = std::max<uint32_t>(1, persistent_waves() / nsh);
     hipLaunchKernelGGL(k_trace, dim3(wps * nsh), dim3(kTraceBlock), 0, s, a);
@@ -1125,6 +1199,17 @@ void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStre
     if (n) hipLaunchKernelGGL(k_quot, dim3((n + 255) / 256), dim3(256), 0, s, a, b, out, n);
 }
 
+int wave_times(unsigned long long* out, int n) {  // diagnostics build only (MCPT_WAVE_TIMES)
+#ifdef MCPT_WAVE_TIMES
+    n = n < 16384 ? n : 16384;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), 4 * n * sizeof(unsigned long long)) != hipSuccess) return -1;
+    return n;
+#else
+    (void)out;
+    (void)n;
+    return 0;
+#endif
+}
 int trace_profile(unsigned long long* out, int reset) {  // diagnostics build only
 #if defined(MCPT_SHADE_PROF)
     static unsigned long long v[64 * 12];

@@ -73,11 +73,13 @@ struct DevPaths {
 // roughly 90 atomics per microsecond, which is what ~24K pushes and ~100K
 // statistics adds per iteration would otherwise cost.
 constexpr int kShards = 64;
+constexpr int kMaxParts = 16;  // k_trace work partitions (one per XCD; MI355X has 8)
 enum : int { C_EXT = 0, C_ANY = 1, C_VIS = 2, C_STATS = 3, C_EXT_RAYS = 9, C_ANY_RAYS = 10, C_MAT = 11, C_WORDS = 32 };  // C_STATS..+5
 struct CounterBlock {
     uint32_t shard[kShards][C_WORDS];  // [0] ext pushes [1] any-hit pushes [2] vis rays [3..8] traversal stats [9,10] rays [11] material pushes
     uint32_t last_ext, last_live, pad[30];
     uint32_t last_ext_shard[kShards];  // per-shard extension pushes of the last iteration
+    uint32_t grab[kMaxParts][C_WORDS];  // k_trace chunk hand-out, one counter line per XCD partition
     unsigned long long tot_ext, tot_any, tot_vis, pad2;
     unsigned long long tot_stats[6];
 };
@@ -115,6 +117,8 @@ struct TraceArgs {
     uint8_t* vis;               // any-hit output: 1 = unoccluded
     uint32_t refill_min;        // refill when at least this many lanes are idle (set by launch_trace)
     uint32_t tri_min;           // run the triangle phase when this many lanes hold a leaf (set by launch_trace)
+    uint32_t nparts;            // work partitions = XCDs of the device (set by launch_trace)
+    uint32_t* grab;             // nparts chunk counters, C_WORDS apart, zero at launch (k_accumulate resets)
 };
 
 struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; int32_t* scene_tri; uint32_t n; };
@@ -136,6 +140,7 @@ struct LbvhOutput {
 };
 int build_lbvh(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
 int trace_profile(unsigned long long* out, int reset);
+int wave_times(unsigned long long* out, int n);
 void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStream_t s);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);

@@ -643,6 +643,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     v.prefiltered = 1;
     ta.hit_tri = c->p.hit_tri;
     ta.vis = c->p.vis;
+    ta.grab = &c->cnt->grab[0][0];  // reset by k_accumulate below
     launch_trace(ta, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
     launch_accumulate(c->cnt, c->stream);
@@ -783,9 +784,11 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
         if ((rc = dalloc(c, c->tmp_bufs, &steps, n))) return rc;
         ts.ray_steps = steps;
     }
+    ta.grab = &c->cnt->grab[0][0];
     HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
     launch_trace(ta, c->stream);
     HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->cnt->grab, 0, sizeof(c->cnt->grab), c->stream));  // hand-out counters back to 0
     if (stage == MCPT_STAGE_EXTEND) {
         HitRecordArgs ha{c->scene, dro, drd, ht, hp, hn, ht, n};  // ht: positions in, scene indices out
         launch_hit_record(ha, c->stream);
@@ -934,5 +937,13 @@ int mcpt_debug_trace_profile(mcpt_ctx* c, uint64_t* out8, int reset) {  // out8:
     int n = trace_profile(v, reset);
     for (int i = 0; i < 12; i++) out8[i] = v[i];
     return n;
+}
+// Diagnostics builds (-DMCPT_WAVE_TIMES) only, not part of mcpt.h: entry / exit s_memrealtime (100 MHz)
+// stamps of the last k_trace launch's first n waves (out: 4n words: entry, exit, partition,
+// time the partition ran dry); returns n or 0.
+int mcpt_debug_wave_times(mcpt_ctx* c, uint64_t* out, int n) {
+    if (!c || !out || n < 0) return MCPT_E_INVALID;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return wave_times(reinterpret_cast<unsigned long long*>(out), n);
 }
 }
