@@ -4,7 +4,10 @@ Workload (BASELINE.json configs[1]): 1920x1080, 256 spp, depth 5, MIS on, env im
 Cornell-box + 5 spheres proxy for the missing scene_show_off_spheres.glb lit by
 night_free_Env.hdr.  A *step* is one wavefront iteration (the reference's wavefront_pathtrace,
 wavefront_kernels.cu:377-442: logic+generate+material -> extend -> shadow) over every pixel the
-rank owns; paths are in steady state after the warmup.  value = (extension + shadow + BRDF
+rank owns; paths are in steady state after the warmup.  Three paths are in flight per pixel
+(mcpt_set_path_slots: slot k renders samples k, k+3, ...; same per-sample results, films equal to
+fp32 summation order -- tests/test_gpu.py::test_path_slots_*): 6.2 M paths per iteration amortise
+each launch's ramp-up and drain (+15 % over one path per pixel, measured).  value = (extension + shadow + BRDF
 visibility rays of all ranks) / (max over ranks of the timed wall time).
 
 Multi-GPU: one process per GPU (torch.distributed.run), weak scaling: the film is 1920 x 1080*N
@@ -46,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-spp", type=int, default=12, help="spp of the full-frame CPU-oracle sample")
     ap.add_argument("--gather", action="store_true", help="RCCL-gather the film after timing (N>1)")
     ap.add_argument("--no-full-frame", action="store_true", help="skip the untimed-by-value full 256-spp frame")
+    ap.add_argument("--slots", type=int, default=int(os.environ.get("MCPT_BENCH_SLOTS", "3")),
+                    help="paths in flight per pixel (mcpt_set_path_slots)")
     return ap.parse_args()
 
 
@@ -120,6 +125,7 @@ def main():
     pt = mcpt.PathTracer(local, mcpt.default_config(spp=rc.spp, max_depth=rc.max_depth))
     pt.upload_scene(scene)
     pt.set_camera(cam)
+    pt.set_path_slots(args.slots)
     pt.resize(W, H)
     my_tiles = tiles_for(rank, world, W, H, 256)
     pt.set_tiles(my_tiles)
@@ -230,11 +236,12 @@ def main():
                         f"night_free_Env.hdr env IS, {rc.width}x{rc.height} per GPU, {rc.spp} spp, depth {rc.max_depth}, MIS",
             "frame": [W, H],
             "tiles": "256x256, rank = (tx+ty) mod N",
-            "step": "one wavefront iteration (shade+extend+shadow) over the rank's pixels, steady state",
+            "step": "one wavefront iteration (shade+extend+shadow) over the rank's pixels x path slots, steady state",
             "rays_per_step": int(rays_all / K),
             "rays_per_step_rank0": {"extend": round(st.extend_rays / K), "shadow": round(st.shadow_rays / K),
                                     "visibility": round(st.vis_rays / K)},
             "parallelism": f"tiles{world}",
+            "path_slots": args.slots,
             "device": pt.device_name,
         },
         "stage_ms_per_step": {k: round(v / K, 4) for k, v in kern.items()},

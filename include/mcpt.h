@@ -149,6 +149,13 @@ int mcpt_scene_upload_gpu_bvh(mcpt_ctx *ctx, const mcpt_scene_desc *desc);
 int mcpt_camera_set(mcpt_ctx *ctx, const mcpt_camera *cam);
 int mcpt_film_resize(mcpt_ctx *ctx, uint32_t w, uint32_t h, uint32_t tile_w, uint32_t tile_h);
 int mcpt_film_clear(mcpt_ctx *ctx);                                          /* == clear_dfilm */
+/* Paths in flight per pixel (default 1, the reference's one path per pixel,
+ * wavefront_kernels.cu:108,114).  With S > 1, path slot k of a pixel renders its samples
+ * k, k + S, k + 2S, ... into its own accumulator and the film readers sum the slots in
+ * slot order: the same per-sample contributions, summed in another order (films agree to
+ * float rounding, samples exactly).  More rays per iteration amortise each launch's ramp
+ * and drain.  Re-allocates the path state (the film is cleared). */
+int mcpt_set_path_slots(mcpt_ctx *ctx, uint32_t slots);
 int mcpt_set_tiles(mcpt_ctx *ctx, const uint32_t *tile_xy, uint32_t ntiles); /* batch tile set; NULL = all */
 int mcpt_wavefront_step(mcpt_ctx *ctx, uint32_t tile_x, uint32_t tile_y, mcpt_stage_stats *st); /* one iteration, one tile */
 int mcpt_iterate(mcpt_ctx *ctx, uint32_t iterations, mcpt_stage_stats *st);  /* batch iterations over the tile set */

@@ -248,7 +248,10 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     const DevScene& sc = a.scene;
     MatOut mo{false, false, false, false, false, 0u};
     SPROF_T0();
-    const Rng r{rng_key(a.seed, pid, samples), len};
+    // path slot -> (pixel, sample index): slot k of a pixel runs samples k, k + S, k + 2S, ...
+    const uint32_t npix = (uint32_t)a.W * (uint32_t)a.H;
+    const uint32_t slot = a.slots > 1 ? pid / npix : 0u;
+    const Rng r{rng_key(a.seed, pid - slot * npix, slot + (uint32_t)a.slots * samples), len};
     const V3 ro = xyz(a.p.ray_o[pid]), rdir = xyz(a.p.ray_d[pid]);
     V3 pos, n;
     int mat;
@@ -361,8 +364,12 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     const DevScene& sc = a.scene;
     const int tile_px = a.tile_w * a.tile_h;
     const int bpt = (tile_px + kBlock - 1) / kBlock;
-    const int tile = blockIdx.x / bpt;
-    const int li = (blockIdx.x - tile * bpt) * kBlock + threadIdx.x;
+    // path slots: blocks [k * ntiles * bpt, (k + 1) * ntiles * bpt) run slot k of every pixel
+    const int per_slot = a.ntiles * bpt;
+    const int slot = a.slots > 1 ? (int)blockIdx.x / per_slot : 0;
+    const int bs = (int)blockIdx.x - slot * per_slot;
+    const int tile = bs / bpt;
+    const int li = (bs - tile * bpt) * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63;
 #ifdef MCPT_SHADE_PROF
     const int wave = threadIdx.x >> 6;
@@ -371,14 +378,15 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
 #endif
     SPROF_T0();
     bool valid = tile < a.ntiles && li < tile_px;
-    uint32_t pid = 0;
+    uint32_t pid = 0, pix = 0;  // path id (slot * pixels + pixel) and pixel id
     int x = 0, y = 0;
     if (valid) {
         int2 t = a.tiles[tile];
         x = t.x * a.tile_w + li % a.tile_w;
         y = t.y * a.tile_h + li / a.tile_w;
         valid = x < a.W - 1 && y < a.H - 1;  // last column and row never rendered (wavefront_kernels.cu:110)
-        pid = (uint32_t)y * (uint32_t)a.W + (uint32_t)x;
+        pix = (uint32_t)y * (uint32_t)a.W + (uint32_t)x;
+        pid = (uint32_t)slot * ((uint32_t)a.W * (uint32_t)a.H) + pix;
     }
     // ---- phase 1: logic + generate (one thread per pixel)
     bool gen_ext = false, gen_trivial = false, cont = false;
@@ -402,8 +410,10 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         const uchar2 vv = reinterpret_cast<const uchar2*>(a.p.vis)[need_nee ? pid : 0u];
         bool dead = (fl & F_DEAD) != 0;
         const uint32_t spp = (uint32_t)a.spp;
-        if (!dead && samples < spp) {  // wavefront_kernels.cu:124
-            const Rng r{rng_key(a.seed, pid, samples), len};
+        // this slot's sample index (slot k runs samples k, k + S, ...; S = 1: the count itself)
+        uint32_t sidx = (uint32_t)slot + (uint32_t)a.slots * samples;
+        if (!dead && sidx < spp) {  // wavefront_kernels.cu:124
+            const Rng r{rng_key(a.seed, pix, sidx), len};
             const bool found = htri >= 0;
             const V3 B = xyz(b4);
             V3 film = xyz(ld4);
@@ -449,6 +459,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             if (terminate) {  // :199-204
                 dead = true;
                 samples++;
+                sidx += (uint32_t)a.slots;
                 a.p.samples[pid] = samples;
             } else {
                 cont = true;
@@ -459,8 +470,8 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         uint32_t nflags = fl;
         if (dead) nflags = F_DEAD;
         SPROF(0);
-        if (dead && samples < spp) {  // :219-222 + wf_generate (:225-251)
-            const Rng r0{rng_key(a.seed, pid, samples), 0u};
+        if (dead && sidx < spp) {  // :219-222 + wf_generate (:225-251)
+            const Rng r0{rng_key(a.seed, pix, sidx), 0u};
             V3 new_o, new_d;
             gen_ray(a.cam, a.W, a.H, x, y, r0, new_o, new_d);
             a.p.beta[pid] = make_float4(1.f, 1.f, 1.f, 0.f);
@@ -1053,6 +1064,20 @@ __global__ void k_clear(ClearArgs a) {  // g_clear_dfilm (wavefront_kernels.cu:5
     a.Ld[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+__global__ void k_resolve(ResolveArgs a) {  // film = sum of the path slots' accumulators, in slot order
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    float4 L = a.Ld[i];
+    uint32_t n = a.samples[i];
+    for (int k = 1; k < a.slots; k++) {
+        const float4 l = a.Ld[(size_t)k * a.n + i];
+        L = make_float4(L.x + l.x, L.y + l.y, L.z + l.z, 0.f);
+        n += a.samples[(size_t)k * a.n + i];
+    }
+    a.out_Ld[i] = L;
+    a.out_samples[i] = n;
+}
+
 __global__ void k_tonemap(TonemapArgs a) {  // draw_to_surface (wavefront_kernels.cu:6-40)
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
@@ -1238,6 +1263,9 @@ void launch_clear(const ClearArgs& a, hipStream_t s) {
 }
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_hit_record, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+}
+void launch_resolve(const ResolveArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_resolve, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 void launch_tonemap(const TonemapArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_tonemap, dim3((a.n + 255) / 256), dim3(256), 0, s, a);

@@ -91,6 +91,7 @@ struct ShadeArgs {
     const int2* tiles;
     int ntiles, tile_w, tile_h, W, H;
     int spp, max_depth, rr_depth;
+    int slots;  // path slots per pixel (paths in flight per pixel; slot k runs samples k, k + slots, ...)
     uint64_t seed;
     uint32_t *ext_q, *any_q, *mat_q;  // mat_q: continuing paths, k_shade -> k_material (ext_cap per shard)
     uint32_t ext_cap, any_cap;  // per-shard queue capacity
@@ -123,6 +124,7 @@ struct TraceArgs {
 
 struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; int32_t* scene_tri; uint32_t n; };
 struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n; };
+struct ResolveArgs { const float4* Ld; const uint32_t* samples; float4* out_Ld; uint32_t* out_samples; uint32_t n; int slots; };
 struct TonemapArgs { const float4* Ld; const uint32_t* samples; uchar4* out; float exposure; uint32_t n; };
 struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* out; };
 
@@ -144,6 +146,7 @@ int wave_times(unsigned long long* out, int n);
 void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStream_t s);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);
+void launch_resolve(const ResolveArgs& a, hipStream_t s);
 void launch_accumulate(CounterBlock* c, hipStream_t s);
 void launch_pack(const PackArgs& a, hipStream_t s);
 

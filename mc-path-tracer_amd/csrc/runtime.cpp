@@ -48,7 +48,10 @@ struct mcpt_ctx {
     bool film_stale = false;
     // film + paths
     uint32_t W = 0, H = 0, tile_w = 256, tile_h = 256;
-    size_t P = 0;
+    size_t P = 0;      // pixels (W * H)
+    uint32_t slots = 1;  // path slots per pixel (mcpt_set_path_slots); path state holds slots * P paths
+    float4* film_Ld = nullptr;     // slots > 1: resolved film (sum of the slot accumulators)
+    uint32_t* film_samples = nullptr;
     std::vector<void*> film_bufs;
     DevPaths p{};
     uint32_t *ext_q = nullptr, *any_q = nullptr, *mat_q = nullptr;
@@ -484,7 +487,7 @@ int mcpt_camera_set(mcpt_ctx* c, const mcpt_camera* cam) {
 static int set_tiles_internal(mcpt_ctx* c, const std::vector<int2>& t) {
     // per-shard queue capacity: shard = k_shade block mod kShards
     const uint32_t bpt = (c->tile_w * c->tile_h + kBlock - 1) / kBlock;
-    const uint32_t nblocks = (uint32_t)t.size() * bpt;
+    const uint32_t nblocks = (uint32_t)t.size() * bpt * c->slots;
     c->ext_cap = std::max<uint32_t>(1, (nblocks + kShards - 1) / kShards) * kBlock;
     c->any_cap = 2 * c->ext_cap;
     const size_t need = (size_t)kShards * c->ext_cap;
@@ -523,7 +526,7 @@ static std::vector<int2> all_tiles(const mcpt_ctx* c) {
 int mcpt_film_clear(mcpt_ctx* c) {
     if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
     HIPCHK(c, hipSetDevice(c->device));
-    ClearArgs a{c->p.flags, c->p.samples, c->p.Ld, (uint32_t)c->P};
+    ClearArgs a{c->p.flags, c->p.samples, c->p.Ld, (uint32_t)(c->P * c->slots)};
     launch_clear(a, c->stream);
     HIPCHK(c, hipGetLastError());
     c->film_stale = false;
@@ -540,7 +543,8 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
     free_list(c->film_bufs);
     c->P = 0;
     c->W = w; c->H = h; c->tile_w = tw; c->tile_h = th;
-    size_t P = (size_t)w * h;
+    const size_t npix = (size_t)w * h, P = npix * c->slots;  // P: paths
+    if (P >= (1ull << 31)) return set_err(c, MCPT_E_INVALID, "film too large for the path slots");
     DevPaths p{};
     int rc;
     if ((rc = dalloc(c, c->film_bufs, &p.ray_o, P)) || (rc = dalloc(c, c->film_bufs, &p.ray_d, P)) ||
@@ -551,6 +555,11 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
         (rc = dalloc(c, c->film_bufs, &p.flags, P)) || (rc = dalloc(c, c->film_bufs, &p.samples, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.vis, 2 * P)))
         return rc;
+    c->film_Ld = nullptr;
+    c->film_samples = nullptr;
+    if (c->slots > 1 && ((rc = dalloc(c, c->film_bufs, &c->film_Ld, npix)) ||
+                         (rc = dalloc(c, c->film_bufs, &c->film_samples, npix))))
+        return rc;
     for (uint32_t** q : {&c->ext_q, &c->any_q, &c->mat_q}) {  // re-sized for the new tile set below
         if (*q) (void)hipFree(*q);
         *q = nullptr;
@@ -559,7 +568,7 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
     HIPCHK(c, hipMemset(p.hit_tri, 0xff, P * sizeof(int32_t)));
     HIPCHK(c, hipMemset(p.vis, 0, 2 * P));
     c->p = p;
-    c->P = P;
+    c->P = npix;
     int rc2 = set_tiles_internal(c, all_tiles(c));
     if (rc2) return rc2;
     return mcpt_film_clear(c);
@@ -611,6 +620,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     sa.max_depth = c->cfg.max_depth;
     sa.rr_depth = c->cfg.rr_depth;
     sa.seed = c->cfg.seed;
+    sa.slots = (int)c->slots;
     sa.ext_q = c->ext_q;
     sa.any_q = c->any_q;
     sa.mat_q = c->mat_q;
@@ -619,7 +629,8 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     sa.cnt = c->cnt;
     int bpt = (int)((c->tile_w * c->tile_h + kBlock - 1) / kBlock);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 0), c->stream));
-    if (sa.ntiles > 0) launch_shade(sa, sa.ntiles * bpt, (c->cfg.flags & MCPT_FLAG_FIXED) != 0, c->stream);
+    if (sa.ntiles > 0)
+        launch_shade(sa, sa.ntiles * bpt * (int)c->slots, (c->cfg.flags & MCPT_FLAG_FIXED) != 0, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 1), c->stream));
     // extension (closest hit) and any-hit rays in one persistent launch
     TraceArgs ta{};
@@ -819,24 +830,55 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
     return MCPT_OK;
 }
 
+// The film (dFilm.Ld / samples): the path state's accumulators with one slot per pixel,
+// else their per-pixel sum in slot order (k_resolve) -- enqueued on the context stream.
+static int film_view(mcpt_ctx* c, const float4** Ld, const uint32_t** samples) {
+    if (c->slots <= 1) {
+        *Ld = c->p.Ld;
+        *samples = c->p.samples;
+        return MCPT_OK;
+    }
+    ResolveArgs a{c->p.Ld, c->p.samples, c->film_Ld, c->film_samples, (uint32_t)c->P, (int)c->slots};
+    launch_resolve(a, c->stream);
+    HIPCHK(c, hipGetLastError());
+    *Ld = c->film_Ld;
+    *samples = c->film_samples;
+    return MCPT_OK;
+}
+
+int mcpt_set_path_slots(mcpt_ctx* c, uint32_t slots) {
+    if (!c || slots < 1 || slots > 64) return set_err(c, MCPT_E_INVALID, "path slots must be 1..64");
+    if (slots == c->slots) return MCPT_OK;
+    c->slots = slots;
+    return c->P ? mcpt_film_resize(c, c->W, c->H, c->tile_w, c->tile_h) : MCPT_OK;
+}
+
 int mcpt_film_read(mcpt_ctx* c, float* Ld, uint32_t* samples) {
     if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
     HIPCHK(c, hipSetDevice(c->device));
+    const float4* fL;
+    const uint32_t* fs;
+    int rc = film_view(c, &fL, &fs);
+    if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (Ld) {
         std::vector<float4> tmp(c->P);
-        HIPCHK(c, hipMemcpy(tmp.data(), c->p.Ld, c->P * sizeof(float4), hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(tmp.data(), fL, c->P * sizeof(float4), hipMemcpyDeviceToHost));
         for (size_t i = 0; i < c->P; i++) { Ld[3 * i] = tmp[i].x; Ld[3 * i + 1] = tmp[i].y; Ld[3 * i + 2] = tmp[i].z; }
     }
-    if (samples) HIPCHK(c, hipMemcpy(samples, c->p.samples, c->P * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (samples) HIPCHK(c, hipMemcpy(samples, fs, c->P * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return MCPT_OK;
 }
 
 int mcpt_film_read_device(mcpt_ctx* c, void* dLd, void* dsamples) {
     if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
     HIPCHK(c, hipSetDevice(c->device));
-    if (dLd) HIPCHK(c, hipMemcpyAsync(dLd, c->p.Ld, c->P * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
-    if (dsamples) HIPCHK(c, hipMemcpyAsync(dsamples, c->p.samples, c->P * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    const float4* fL;
+    const uint32_t* fs;
+    int rc = film_view(c, &fL, &fs);
+    if (rc) return rc;
+    if (dLd) HIPCHK(c, hipMemcpyAsync(dLd, fL, c->P * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+    if (dsamples) HIPCHK(c, hipMemcpyAsync(dsamples, fs, c->P * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return MCPT_OK;
 }
@@ -847,7 +889,11 @@ int mcpt_film_pack_tiles(mcpt_ctx* c, void* d_out, uint32_t* npix) {
     if (npix) *npix = n;
     if (!d_out) return MCPT_OK;
     HIPCHK(c, hipSetDevice(c->device));
-    PackArgs a{c->p.Ld, c->p.samples, c->tiles, (int)c->tiles_h.size(), (int)c->tile_w, (int)c->tile_h, (int)c->W, (int)c->H, (float4*)d_out};
+    const float4* fL;
+    const uint32_t* fs;
+    int rc = film_view(c, &fL, &fs);
+    if (rc) return rc;
+    PackArgs a{fL, fs, c->tiles, (int)c->tiles_h.size(), (int)c->tile_w, (int)c->tile_h, (int)c->W, (int)c->H, (float4*)d_out};
     if (n) launch_pack(a, c->stream);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -865,9 +911,13 @@ int mcpt_film_size(const mcpt_ctx* c, uint32_t* w, uint32_t* h) {
 int mcpt_film_tonemap_rgba8(mcpt_ctx* c, float exposure, uint8_t* out) {
     if (!c || !c->P || !out) return set_err(c, MCPT_E_INVALID, "bad argument");
     HIPCHK(c, hipSetDevice(c->device));
+    const float4* fL;
+    const uint32_t* fs;
+    int rc = film_view(c, &fL, &fs);
+    if (rc) return rc;
     uchar4* d = nullptr;
     HIPCHK(c, hipMalloc(&d, c->P * sizeof(uchar4)));
-    TonemapArgs a{c->p.Ld, c->p.samples, d, exposure, (uint32_t)c->P};
+    TonemapArgs a{fL, fs, d, exposure, (uint32_t)c->P};
     launch_tonemap(a, c->stream);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -896,9 +946,10 @@ int mcpt_debug_queue_rays(mcpt_ctx* c, int which, float* ro, float* rd, uint32_t
     for (int sh = 0; sh < kShards; sh++)
         for (uint32_t k = 0; k < cb.last_ext_shard[sh] && q.size() < n; k++) q.push_back(all[(size_t)sh * c->ext_cap + k]);
     n = (uint32_t)q.size();
-    std::vector<float4> o(c->P), d(c->P);
-    HIPCHK(c, hipMemcpy(o.data(), c->p.ray_o, c->P * sizeof(float4), hipMemcpyDeviceToHost));
-    HIPCHK(c, hipMemcpy(d.data(), c->p.ray_d, c->P * sizeof(float4), hipMemcpyDeviceToHost));
+    const size_t np = c->P * c->slots;
+    std::vector<float4> o(np), d(np);
+    HIPCHK(c, hipMemcpy(o.data(), c->p.ray_o, np * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(d.data(), c->p.ray_d, np * sizeof(float4), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < n; i++) {
         float4 a = o[q[i]], b = d[q[i]];
         ro[3 * i] = a.x; ro[3 * i + 1] = a.y; ro[3 * i + 2] = a.z;

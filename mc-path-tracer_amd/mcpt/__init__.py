@@ -89,6 +89,7 @@ ABI = {
     "mcpt_film_resize": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "mcpt_film_clear": (C.c_int, [C.c_void_p]),
     "mcpt_set_tiles": (C.c_int, [C.c_void_p, _u, C.c_uint32]),
+    "mcpt_set_path_slots": (C.c_int, [C.c_void_p, C.c_uint32]),
     "mcpt_wavefront_step": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(StageStats)]),
     "mcpt_iterate": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(StageStats)]),
     "mcpt_render": (C.c_int, [C.c_void_p, C.POINTER(StageStats)]),
@@ -370,6 +371,10 @@ class PathTracer:
 
     def clear(self):
         self._ck(lib().mcpt_film_clear(self.h))
+
+    def set_path_slots(self, slots):
+        """Paths in flight per pixel (mcpt_set_path_slots); re-allocates and clears the film."""
+        self._ck(lib().mcpt_set_path_slots(self.h, slots))
 
     def set_tiles(self, tiles=None):
         if tiles is None:

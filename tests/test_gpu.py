@@ -219,6 +219,64 @@ def test_tile_partition_invariance(mcpt_mod, scene_c2):
         p.close()
 
 
+@pytest.mark.parametrize("slots", [2, 4])
+def test_path_slots_config1_parity(mcpt_mod, oracle, scene_c1, slots):
+    """mcpt_set_path_slots: S paths in flight per pixel, slot k running samples k, k+S, ... with the
+    same per-sample RNG keys, so every sample contributes exactly what it does with one path per
+    pixel; only the summation order of the film differs.  BASELINE config 1 in full against the
+    oracle: sample counts and ray counts exact, radiance within the north star's 1e-4."""
+    rc = mcpt_mod.CONFIGS[1]
+    cam = mcpt_mod.config_camera(rc)
+    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=rc.spp, max_depth=rc.max_depth))
+    pt.upload_scene(scene_c1[0])
+    pt.set_camera(cam)
+    pt.set_path_slots(slots)  # before resize: allocated once
+    pt.resize(rc.width, rc.height)
+    st = pt.render()
+    Ld, smp = pt.film()
+    rL, rs, cnt = oracle.render(scene_c1[1], cam, rc.width, rc.height, rc.spp, rc.max_depth)
+    assert np.array_equal(smp, rs)
+    ok, nbad = film_close(Ld, rL)
+    assert ok, f"{nbad} radiance values differ"
+    assert (st.extend_rays, st.shadow_rays, st.vis_rays) == (cnt["extend_rays"], cnt["shadow_rays"], cnt["vis_rays"])
+    assert st.iterations < 7 * rc.spp  # slots run their samples concurrently
+    # the readers (tonemap, device read) see the resolved film
+    with np.errstate(invalid="ignore", divide="ignore"):
+        c = (Ld / smp[..., None].astype(np.float32)) * np.float32(1.0)
+        v = np.float32(255) * (c / (c + np.float32(1.0)))
+    want = np.where(np.isfinite(v) & (v >= 0), v, 0).astype(np.uint32).astype(np.uint8)
+    assert np.array_equal(pt.tonemap(1.0)[..., :3], want)
+    pt.close()
+
+
+def test_path_slots_ragged_and_resize(mcpt_mod, oracle, scene_c2):
+    """Slots with spp not a multiple of S (slot 2 of 3 runs one sample fewer), slots changed after
+    resize (re-allocates, clears), and spp=1 with 4 slots bit-identical to one slot."""
+    rc = mcpt_mod.CONFIGS[2]
+    W, H = 160, 90
+    cam = mcpt_mod.config_camera(rc, W, H)
+    pt = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 4, rc.max_depth)
+    pt.render()
+    pt.set_path_slots(3)
+    assert pt.film()[1].max() == 0  # cleared by the re-allocation
+    pt.render()
+    Ld, smp = pt.film()
+    rL, rs, _ = oracle.render(scene_c2[1], cam, W, H, 4, rc.max_depth)
+    assert np.array_equal(smp, rs)
+    assert film_close(Ld, rL)[0]
+    one = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 1, rc.max_depth)
+    one.render()
+    four = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 1, rc.max_depth)
+    four.set_path_slots(4)
+    four.render()
+    (a, sa), (b, sb) = one.film(), four.film()
+    assert np.array_equal(sa, sb) and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    with pytest.raises(mcpt_mod.McptError):
+        pt.set_path_slots(0)
+    for p in (pt, one, four):
+        p.close()
+
+
 def test_tonemap_matches_draw_to_surface(mcpt_mod, scene_c1):
     cam = mcpt_mod.config_camera(mcpt_mod.CONFIGS[1], 64, 64)
     pt = make_pt(mcpt_mod, scene_c1[0], cam, 64, 64, 2, 3)
