@@ -244,7 +244,8 @@ struct MatOut {
 // (A.6), delta lights get MIS weight 1 (pdf_brdf.y = 0 instead of 1, A.7), textbook
 // Gram-Schmidt (A.9), env sampling/pdf on matched, clamped cells (A.11).
 template <bool FIXED>
-__device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t samples, uint32_t len, V3 beta_store) {
+__device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t samples, uint32_t len, V3 beta_store,
+                                 int32_t htri) {
     const DevScene& sc = a.scene;
     MatOut mo{false, false, false, false, false, 0u};
     SPROF_T0();
@@ -256,7 +257,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     V3 pos, n;
     int mat;
     float t_hit;
-    hit_record(sc, ro, rdir, a.p.hit_tri[pid], pos, n, mat, t_hit);
+    hit_record(sc, ro, rdir, htri, pos, n, mat, t_hit);
     const V3 wo = -rdir;
     const Mat m = load_mat(sc.mats + 8 * mat);
     SPROF(3);
@@ -391,6 +392,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     // ---- phase 1: logic + generate (one thread per pixel)
     bool gen_ext = false, gen_trivial = false, cont = false;
     uint32_t cont_len = 0, cont_samples = 0;
+    int32_t cont_htri = -1;
     V3 beta_store = v3(0.f, 0.f, 0.f);
     if (valid) {
         // Every load the logic may need is issued up front, in one round: the
@@ -465,6 +467,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
                 cont = true;
                 cont_len = len;
                 cont_samples = samples;
+                cont_htri = htri;
             }
         }
         uint32_t nflags = fl;
@@ -489,9 +492,8 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     }
     SPROF(1);
     // ---- pushes: generated extension rays and continuing paths (material queue); one
-    // atomic per block and queue.  A continuing path's updated throughput goes through
-    // p.beta to k_material (which rewrites it with f_s/pdf_s in .w).
-    if (cont) a.p.beta[pid] = f4(beta_store, 0.f);
+    // atomic per block and queue.  A continuing path's record and updated throughput go
+    // to k_material densely (it writes p.beta with f_s/pdf_s in .w).
     const int shard = blockIdx.x % kShards;
     uint32_t* sc_ctr = a.cnt->shard[shard];
     {
@@ -500,13 +502,15 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         uint32_t slot[2], total[2];
         block_push<2>(want, ctr, slot, total);
         if (gen_ext) a.ext_q[shard * a.ext_cap + slot[0]] = pid;
-        if (cont) a.mat_q[shard * a.ext_cap + slot[1]] = pid;
+        if (cont) {
+            const uint32_t qi = shard * a.ext_cap + slot[1];
+            a.mat_rec[qi] = make_uint4(pid, cont_len, cont_samples, (uint32_t)cont_htri);
+            a.mat_beta[qi] = f4(beta_store, 0.f);
+        }
     }
     uint32_t n_ext = (gen_ext || gen_trivial) ? 1u : 0u;  // queued + resolved-in-place rays
     for (int off = 32; off > 0; off >>= 1) n_ext += __shfl_xor(n_ext, off);
     if (lane == 0 && n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
-    (void)cont_len;
-    (void)cont_samples;
 #ifdef MCPT_SHADE_PROF
     {
         unsigned long long _n = __builtin_readcyclecounter();
@@ -546,10 +550,10 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
         MatOut mo{false, false, false, false, false, 0u};
         uint32_t mpid = 0;
         if (i < n) {
-            mpid = a.mat_q[shard * a.ext_cap + i];
-            const uint32_t fl = a.p.flags[mpid];
-            const float4 b4 = a.p.beta[mpid];
-            mo = material<FIXED>(a, mpid, a.p.samples[mpid], (fl >> F_LEN_SHIFT) & 0xffu, xyz(b4));
+            const uint4 q = a.mat_rec[shard * a.ext_cap + i];  // {pid, len, samples, hit_tri}
+            const float4 b4 = a.mat_beta[shard * a.ext_cap + i];
+            mpid = q.x;
+            mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w);
         }
         bool want[3] = {mo.want_ext, mo.want_l, mo.want_b};
         uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};

@@ -93,7 +93,12 @@ struct ShadeArgs {
     int spp, max_depth, rr_depth;
     int slots;  // path slots per pixel (paths in flight per pixel; slot k runs samples k, k + slots, ...)
     uint64_t seed;
-    uint32_t *ext_q, *any_q, *mat_q;  // mat_q: continuing paths, k_shade -> k_material (ext_cap per shard)
+    uint32_t *ext_q, *any_q;
+    // material queue (continuing paths, k_shade -> k_material, ext_cap per shard): dense records
+    // {pid, len, samples, hit_tri} + the updated throughput, so k_material reads its per-path
+    // inputs from k_shade's coalesced loads instead of gathering them again at pid
+    uint4* mat_rec;
+    float4* mat_beta;
     uint32_t ext_cap, any_cap;  // per-shard queue capacity
     CounterBlock* cnt;
 };

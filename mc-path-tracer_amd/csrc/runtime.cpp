@@ -500,7 +500,7 @@ static int set_tiles_internal(mcpt_ctx* c, const std::vector<int2>& t) {
         c->queue_alloc = 0;
         if (hipMalloc(&c->ext_q, need * sizeof(uint32_t)) != hipSuccess ||
             hipMalloc(&c->any_q, 2 * need * sizeof(uint32_t)) != hipSuccess ||
-            hipMalloc(&c->mat_q, need * sizeof(uint32_t)) != hipSuccess)
+            hipMalloc(&c->mat_q, need * 8 * sizeof(uint32_t)) != hipSuccess)  // MatRec + beta per slot
             return set_err(c, MCPT_E_NOMEM, "queue allocation failed");
         c->queue_alloc = need;
     }
@@ -623,7 +623,8 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     sa.slots = (int)c->slots;
     sa.ext_q = c->ext_q;
     sa.any_q = c->any_q;
-    sa.mat_q = c->mat_q;
+    sa.mat_rec = reinterpret_cast<uint4*>(c->mat_q);
+    sa.mat_beta = reinterpret_cast<float4*>(c->mat_q) + (size_t)kShards * c->ext_cap;
     sa.ext_cap = c->ext_cap;
     sa.any_cap = c->any_cap;
     sa.cnt = c->cnt;

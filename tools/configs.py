@@ -19,6 +19,8 @@ ap.add_argument("--configs", default="1,2,3,4,5")
 ap.add_argument("--warmup", type=int, default=20)
 ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--out", default=None)
+ap.add_argument("--slots", default="auto", help="paths per pixel: auto = ~6.2 M paths in flight, capped at spp and 16")
+ap.add_argument("--full", default="1", help="configs also rendered as a whole frame to spp completion")
 args = ap.parse_args()
 res = []
 for c in [int(x) for x in args.configs.split(",")]:
@@ -30,6 +32,9 @@ for c in [int(x) for x in args.configs.split(",")]:
     pt = mcpt.PathTracer(0, mcpt.default_config(spp=rc.spp, max_depth=rc.max_depth))
     pt.upload_scene(scene)
     pt.set_camera(mcpt.config_camera(rc))
+    P = rc.width * rc.height
+    S = max(1, min(rc.spp, 16, round(6.2e6 / P))) if args.slots == "auto" else int(args.slots)
+    pt.set_path_slots(S)
     pt.resize(rc.width, rc.height)
     pt.iterate(args.warmup)
     t1 = time.time()
@@ -43,7 +48,14 @@ for c in [int(x) for x in args.configs.split(",")]:
          "rays_per_iter": {"extend": st.extend_rays // args.iters, "shadow": st.shadow_rays // args.iters,
                            "vis": st.vis_rays // args.iters},
          "ext_nodes_per_ray": round(st.ext_nodes / max(1, st.extend_rays), 2),
-         "any_nodes_per_ray": round(st.any_nodes / max(1, st.shadow_rays + st.vis_rays), 2)}
+         "any_nodes_per_ray": round(st.any_nodes / max(1, st.shadow_rays + st.vis_rays), 2), "path_slots": S}
+    if str(c) in args.full.split(","):
+        pt.clear()
+        t2 = time.time()
+        fs = pt.render()
+        dtf = time.time() - t2
+        r["full_frame"] = {"seconds": round(dtf, 4), "iterations": fs.iterations,
+                           "mray_s": round((fs.extend_rays + fs.shadow_rays + fs.vis_rays) / dtf / 1e6, 1)}
     print(json.dumps(r), flush=True)
     res.append(r)
     pt.close()
