@@ -208,6 +208,11 @@ def main():
                         "ext_tri_tests": round(st.ext_tests / max(1, st.extend_rays), 2),
                         "any_pair_nodes": round(st.any_nodes / max(1, st.shadow_rays + st.vis_rays), 2),
                         "any_tri_tests": round(st.any_tests / max(1, st.shadow_rays + st.vis_rays), 2)}}
+    # measured HBM ceiling on this device (hand-written dwordx4 copy) beside the spec peak
+    copy = pt.hbm_copy_gbps(1 << 30, 20)
+    roof["measured_copy_GBps"] = round(copy, 1)
+    if traffic is not None:
+        roof["traffic_GBps"] = round(traffic / (avg_ms * 1e-3) / 1e9, 1)
     # whole-pipeline form: all logical bytes of both kernels over their summed time
     t_pipe = (st.ms_extend + st.ms_shadow + st.ms_shade) * 1e-3
     roof["pipeline_frac"] = round((b_ext + b_any + b_shd) / t_pipe / HBM_PEAK, 4)

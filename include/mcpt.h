@@ -187,6 +187,9 @@ int mcpt_debug_trace_profile(mcpt_ctx *ctx, uint64_t *out12, int reset);
 /* diagnostics: the kernels' shared-denominator division (mcpt::quot3, mcpt_core.hpp) on the
  * device for n host pairs: out[i] = a[i] / b[i] as the kernels compute it (must equal IEEE fp32). */
 int mcpt_debug_quot(mcpt_ctx *ctx, const float *a, const float *b, uint32_t n, float *out);
+/* Measured HBM ceiling for the roofline: a hand-written dwordx4 copy of `bytes`
+ * between two device buffers, `iters` launches timed with HIP events; *gbps = (read + write) bytes / s. */
+int mcpt_debug_hbm_copy(mcpt_ctx *ctx, uint64_t bytes, uint32_t iters, double *gbps);
 
 /* ---- host scene builder (Scene.cu:24-470, EnvironmentLight.cu:329-452, BVH.cu) ---- */
 mcpt_scene *mcpt_scene_new(void);

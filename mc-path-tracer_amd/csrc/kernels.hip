@@ -1228,6 +1228,18 @@ void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStre
     if (n) hipLaunchKernelGGL(k_quot, dim3((n + 255) / 256), dim3(256), 0, s, a, b, out, n);
 }
 
+// HBM copy ceiling (mcpt_debug_hbm_copy; SURVEY.md 8(d) "re-measure a STREAM-copy ceiling"): one
+// dwordx4 per lane, one pass (a block per 256 float4).  tools/hbm/copy_sweep.hip measured the
+// variants: one-pass grids reach 6.25-6.39 TB/s on 1-4 GiB, persistent grid-stride loops
+// 4.5-5.0 TB/s whatever the unroll or cache policy.
+__global__ __launch_bounds__(256) void k_copy(const float4* __restrict__ src, float4* __restrict__ dst, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+void launch_copy(const float4* src, float4* dst, size_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_copy, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, n);
+}
+
 int wave_times(unsigned long long* out, int n) {  // diagnostics build only (MCPT_WAVE_TIMES)
 #ifdef MCPT_WAVE_TIMES
     n = n < 16384 ? n : 16384;

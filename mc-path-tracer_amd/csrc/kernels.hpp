@@ -149,6 +149,7 @@ int build_lbvh(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
 int trace_profile(unsigned long long* out, int reset);
 int wave_times(unsigned long long* out, int n);
 void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStream_t s);
+void launch_copy(const float4* src, float4* dst, size_t n, hipStream_t s);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);
 void launch_resolve(const ResolveArgs& a, hipStream_t s);

@@ -982,6 +982,35 @@ int mcpt_debug_quot(mcpt_ctx* c, const float* a, const float* b, uint32_t n, flo
     return rc;
 }
 
+int mcpt_debug_hbm_copy(mcpt_ctx* c, uint64_t bytes, uint32_t iters, double* gbps) {
+    if (!c || !gbps || bytes < 4096 || iters == 0) return set_err(c, MCPT_E_INVALID, "bad argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t n = (size_t)(bytes / sizeof(float4));
+    float4* d = nullptr;
+    if (hipMalloc(&d, 2 * n * sizeof(float4)) != hipSuccess) return set_err(c, MCPT_E_NOMEM, "copy buffers");
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = MCPT_OK;
+    if (hipMemsetAsync(d, 0, 2 * n * sizeof(float4), c->stream) != hipSuccess ||
+        hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+        rc = set_err(c, MCPT_E_HIP, "copy setup");
+    } else {
+        launch_copy(d, d + n, n, c->stream);  // warm-up
+        (void)hipEventRecord(e0, c->stream);
+        for (uint32_t i = 0; i < iters; i++) launch_copy(i & 1 ? d + n : d, i & 1 ? d : d + n, n, c->stream);
+        (void)hipEventRecord(e1, c->stream);
+        float ms = 0.f;
+        if (hipGetLastError() != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+            hipEventElapsedTime(&ms, e0, e1) != hipSuccess || ms <= 0.f)
+            rc = set_err(c, MCPT_E_HIP, "copy kernel");
+        else
+            *gbps = 2.0 * (double)n * sizeof(float4) * iters / (ms * 1e-3) / 1e9;  // read + write bytes
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(d);
+    return rc;
+}
+
 int mcpt_debug_trace_profile(mcpt_ctx* c, uint64_t* out8, int reset) {  // out8: 12 words
     if (!c || !out8) return MCPT_E_INVALID;
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -112,6 +112,7 @@ ABI = {
     "mcpt_debug_trace_profile": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "mcpt_scene_build_ex": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mcpt_debug_quot": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "mcpt_debug_hbm_copy": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
     "mcpt_scene_new": (C.c_void_p, []),
     "mcpt_scene_free": (None, [C.c_void_p]),
     "mcpt_scene_load_glb": (C.c_int, [C.c_void_p, C.c_char_p, _f]),
@@ -455,6 +456,12 @@ class PathTracer:
         names = ("trips", "refills", "node_lanes", "tri_phases", "tri_lanes", "finish_trips", "idle_lanes",
                  "pop_trips", "pop_lanes", "slow_slab_trips", "finish_lanes", "_11")
         return {k: int(x) for k, x in zip(names, v)} if n > 0 else None
+
+    def hbm_copy_gbps(self, nbytes=1 << 30, iters=20) -> float:
+        """Measured HBM copy ceiling (read + write GB/s) of a hand-written dwordx4 copy kernel."""
+        g = C.c_double(0.0)
+        self._ck(lib().mcpt_debug_hbm_copy(self.h, nbytes, iters, C.byref(g)))
+        return g.value
 
     def debug_quot(self, a, b):
         """a / b as the kernels divide (shared fp64 reciprocal, mcpt_core.hpp quot3)."""

@@ -495,6 +495,16 @@ def test_device_division_is_ieee(mcpt_mod):
     pt.close()
 
 
+def test_hbm_copy_ceiling(mcpt_mod):
+    """mcpt_debug_hbm_copy: the measured copy ceiling the bench reports beside the 8 TB/s spec."""
+    pt = mcpt_mod.PathTracer(0)
+    g = pt.hbm_copy_gbps(256 << 20, 5)
+    assert 1000.0 < g < 8000.0
+    with pytest.raises(mcpt_mod.McptError):
+        pt.hbm_copy_gbps(16, 1)
+    pt.close()
+
+
 def test_sah3_tree_same_results(mcpt_mod, oracle, scene_c2):
     """The GPU on an SAH3 tree (multi-triangle leaves) == the oracle on the reference builder's
     tree: vertex-grazing rays and a config-2 film band."""
