@@ -24,6 +24,7 @@ def run(K):
         pt = mcpt.PathTracer(0, mcpt.default_config(spp=rc.spp, max_depth=rc.max_depth))
         pt.upload_scene(scene)
         pt.set_camera(cam)
+        pt.set_path_slots(int(os.environ.get("SLOTS", "3")))
         pt.resize(W, H)
         pt.set_tiles([(tx, ty) for ty in range(ny) for tx in range(nx) if (tx + ty) % K == k])
         pt.iterate(WARM)
