@@ -19,9 +19,13 @@ ap.add_argument("--configs", default="1,2,3,4,5")
 ap.add_argument("--warmup", type=int, default=20)
 ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--out", default=None)
-ap.add_argument("--slots", default="auto", help="paths per pixel: auto = ~6.2 M paths in flight, capped at spp and 16")
+ap.add_argument("--slots", default="auto", help="paths per pixel; auto = the measured best per config (AUTO_SLOTS)")
 ap.add_argument("--full", default="1", help="configs also rendered as a whole frame to spp completion")
 args = ap.parse_args()
+# Path slots per config, measured (steady state, 1 GPU): C2 1/2/3/4 -> 7248/8095/8340/7520 Mray/s
+# (full frame 0.481/0.419/0.396/0.400 s); C3 2/3 -> 5670/6146; C4 1/2/4 -> 4476/4852/4982;
+# C5 1/2/4 -> 4548/4910/5011; C1 (65K pixels, 16 spp) renders all its samples at once with 16.
+AUTO_SLOTS = {1: 16, 2: 3, 3: 3, 4: 4, 5: 4}
 res = []
 for c in [int(x) for x in args.configs.split(",")]:
     rc = mcpt.CONFIGS[c]
@@ -33,7 +37,7 @@ for c in [int(x) for x in args.configs.split(",")]:
     pt.upload_scene(scene)
     pt.set_camera(mcpt.config_camera(rc))
     P = rc.width * rc.height
-    S = max(1, min(rc.spp, 16, round(6.2e6 / P))) if args.slots == "auto" else int(args.slots)
+    S = AUTO_SLOTS.get(c, 1) if args.slots == "auto" else int(args.slots)
     pt.set_path_slots(S)
     pt.resize(rc.width, rc.height)
     pt.iterate(args.warmup)
@@ -43,7 +47,8 @@ for c in [int(x) for x in args.configs.split(",")]:
     rays = st.extend_rays + st.shadow_rays + st.vis_rays
     r = {"config": c, "W": rc.width, "H": rc.height, "spp": rc.spp, "depth": rc.max_depth,
          "tris": int(len(a["mat"])), "bvh_depth": scene.bvh_depth, "host_build_s": round(t_build, 2),
-         "mray_s": round(rays / (st.ms_total * 1e-3) / 1e6, 1), "mray_s_wall": round(rays / wall / 1e6, 1),
+         "mray_s": round(rays / (st.ms_total * 1e-3) / 1e6, 1) if rays else None,  # None: finished in the warmup
+         "mray_s_wall": round(rays / wall / 1e6, 1) if rays else None,
          "ms_trace": round(st.ms_extend / args.iters, 4), "ms_shade": round(st.ms_shade / args.iters, 4),
          "rays_per_iter": {"extend": st.extend_rays // args.iters, "shadow": st.shadow_rays // args.iters,
                            "vis": st.vis_rays // args.iters},
