@@ -6,7 +6,7 @@ sys.path[:0] = [os.path.join(REPO, "mc-path-tracer_amd")]
 import mcpt
 rc = mcpt.CONFIGS[2]
 pt = mcpt.PathTracer(0, mcpt.default_config(spp=256, max_depth=5))
-pt.upload_scene(mcpt.build_config_scene(2)); pt.set_camera(mcpt.config_camera(rc)); pt.resize(rc.width, rc.height)
+pt.upload_scene(mcpt.build_config_scene(2)); pt.set_camera(mcpt.config_camera(rc)); pt.set_path_slots(int(os.environ.get("SLOTS", "3"))); pt.resize(rc.width, rc.height)
 pt.iterate(30)
 pt.trace_profile(reset=True)
 N = 10
