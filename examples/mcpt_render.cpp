@@ -3,7 +3,7 @@
 // INTEGRATION.md): build a BASELINE config scene with the host builder, upload it,
 // run the wavefront iterations until every pixel has its samples, write PNG + PFM.
 //
-//   mcpt_render <config 1-5> [spp] [out_prefix] [--gpu-bvh] [--reference-bvh] [--fixed] [--tiles-per-call]
+//   mcpt_render <config 1-5> [spp] [out_prefix] [--gpu-bvh] [--reference-bvh] [--fixed] [--tiles-per-call] [--slots S]
 //
 // --tiles-per-call uses the reference orchestration (one 256x256 tile per call,
 // wavefront_kernels.cu:377-442 + Film::update_tile_position) instead of batch mode.
@@ -20,7 +20,7 @@ struct Cfg { int w, h, spp, depth; float pos[3], pitch; const char* env; };
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        fprintf(stderr, "usage: %s <config 1-5> [spp] [out_prefix] [--gpu-bvh] [--reference-bvh] [--fixed] [--tiles-per-call]\n", argv[0]);
+        fprintf(stderr, "usage: %s <config 1-5> [spp] [out_prefix] [--gpu-bvh] [--reference-bvh] [--fixed] [--tiles-per-call] [--slots S]\n", argv[0]);
         return 2;
     }
     const Cfg cfgs[6] = {{0, 0, 0, 0, {0, 0, 0}, 0, ""},
@@ -35,11 +35,13 @@ int main(int argc, char** argv) {
     if (argc > 2 && argv[2][0] != '-') c.spp = atoi(argv[2]);
     std::string out = (argc > 3 && argv[3][0] != '-') ? argv[3] : "mcpt_render";
     bool gpu_bvh = false, ref_bvh = false, fixed = false, per_tile = false;
+    uint32_t slots = 1;
     for (int i = 2; i < argc; i++) {
         if (!strcmp(argv[i], "--gpu-bvh")) gpu_bvh = true;
         if (!strcmp(argv[i], "--reference-bvh")) ref_bvh = true;
         if (!strcmp(argv[i], "--fixed")) fixed = true;
         if (!strcmp(argv[i], "--tiles-per-call")) per_tile = true;
+        if (!strcmp(argv[i], "--slots") && i + 1 < argc) slots = (uint32_t)atoi(argv[++i]);
     }
     const char* assets = getenv("MCPT_ASSETS") ? getenv("MCPT_ASSETS") : "assets";
 
@@ -68,6 +70,7 @@ int main(int argc, char** argv) {
     mcpt_camera cam;
     if (!rc) rc = mcpt_camera_make(&cp, &cam);
     if (!rc) rc = mcpt_camera_set(ctx, &cam);
+    if (!rc) rc = mcpt_set_path_slots(ctx, slots);  // paths in flight per pixel (default 1)
     if (!rc) rc = mcpt_film_resize(ctx, c.w, c.h, 256, 256);
     if (rc) { fprintf(stderr, "setup: %s\n", mcpt_last_error(ctx)); return 1; }
 

@@ -277,6 +277,34 @@ def test_path_slots_ragged_and_resize(mcpt_mod, oracle, scene_c2):
         p.close()
 
 
+def test_path_slots_partition_invariance(mcpt_mod, scene_c2):
+    """With 2 path slots, tile subsets rendered separately (as ranks would) and the reference's
+    one-tile-per-call orchestration give the batch film bit for bit (same slot order per pixel)."""
+    rc = mcpt_mod.CONFIGS[2]
+    W, H, T = 200, 120, 64
+    cam = mcpt_mod.config_camera(rc, W, H)
+    from mcpt import parallel
+
+    pts = [make_pt(mcpt_mod, scene_c2[0], cam, W, H, 3, 5, tile=T) for _ in range(3)]
+    for p in pts:
+        p.set_path_slots(2)
+    full, parts, ref = pts
+    full.render()
+    for r in range(2):
+        parts.set_tiles(parallel.tiles_for_rank(r, 2, W, H, T))
+        parts.render()
+    nx, ny = parallel.tile_grid(W, H, T)
+    for it in range(40 * nx * ny):
+        t = it % (nx * ny)
+        ref.step(t % nx, t // nx)
+    (L0, s0), (L1, s1), (L2, s2) = full.film(), parts.film(), ref.film()
+    assert s0[: H - 1, : W - 1].min() == 3
+    for L, sm in ((L1, s1), (L2, s2)):
+        assert np.array_equal(L0.view(np.uint32), L.view(np.uint32)) and np.array_equal(s0, sm)
+    for p in pts:
+        p.close()
+
+
 def test_tonemap_matches_draw_to_surface(mcpt_mod, scene_c1):
     cam = mcpt_mod.config_camera(mcpt_mod.CONFIGS[1], 64, 64)
     pt = make_pt(mcpt_mod, scene_c1[0], cam, 64, 64, 2, 3)
