@@ -538,6 +538,7 @@ int mcpt_film_clear(mcpt_ctx* c) {
 int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t th) {
     if (!c || w == 0 || h == 0 || tw == 0 || th == 0) return set_err(c, MCPT_E_INVALID, "bad film size");
     if ((uint64_t)w * h >= (1ull << 31)) return set_err(c, MCPT_E_INVALID, "film too large");
+    if ((uint64_t)tw * th > (1ull << 26)) return set_err(c, MCPT_E_INVALID, "tile too large");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     free_list(c->film_bufs);

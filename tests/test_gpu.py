@@ -305,6 +305,37 @@ def test_path_slots_partition_invariance(mcpt_mod, scene_c2):
         p.close()
 
 
+def test_degenerate_and_ragged_films(mcpt_mod, oracle, scene_c1):
+    """Edge cases of the film/tile contract against the oracle: 1x1 and 2x2 films (the last row
+    and column are never rendered, wavefront_kernels.cu:110), spp = 0, ragged non-square tiles,
+    a tile larger than the film, with 1 and 2 path slots; bad sizes are rejected."""
+    rc = mcpt_mod.CONFIGS[1]
+    cases = [(1, 1, 2, 256, 256), (2, 2, 3, 256, 256), (70, 50, 2, 48, 32), (100, 60, 2, 512, 512), (33, 17, 0, 16, 8)]
+    for W, H, spp, tw, th in cases:
+        cam = mcpt_mod.config_camera(rc, W, H)
+        rL, rs, cnt = oracle.render(scene_c1[1], cam, W, H, spp, rc.max_depth)
+        for slots in (1, 2):
+            pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=spp, max_depth=rc.max_depth))
+            pt.upload_scene(scene_c1[0])
+            pt.set_camera(cam)
+            pt.set_path_slots(slots)
+            pt.resize(W, H, tw, th)
+            st = pt.render()
+            Ld, smp = pt.film()
+            assert st.live_paths == 0
+            assert np.array_equal(smp, rs), (W, H, spp, tw, th, slots)
+            assert film_close(Ld, rL)[0], (W, H, spp, tw, th, slots)
+            if slots == 1:
+                assert np.array_equal(Ld.view(np.uint32), np.asarray(rL, np.float32).reshape(Ld.shape).view(np.uint32))
+            assert (st.extend_rays, st.shadow_rays, st.vis_rays) == (cnt["extend_rays"], cnt["shadow_rays"], cnt["vis_rays"])
+            pt.close()
+    pt = mcpt_mod.PathTracer(0)
+    for bad in ((0, 4, 256, 256), (4, 0, 256, 256), (4, 4, 0, 256), (64, 64, 1 << 14, 1 << 14)):
+        with pytest.raises(mcpt_mod.McptError):
+            pt.resize(*bad)
+    pt.close()
+
+
 def test_tonemap_matches_draw_to_surface(mcpt_mod, scene_c1):
     cam = mcpt_mod.config_camera(mcpt_mod.CONFIGS[1], 64, 64)
     pt = make_pt(mcpt_mod, scene_c1[0], cam, 64, 64, 2, 3)
