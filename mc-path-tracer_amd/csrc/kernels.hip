@@ -402,7 +402,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         const uint32_t fl = a.p.flags[pid];
         uint32_t samples = a.p.samples[pid];
         const int32_t htri = a.p.hit_tri[pid];
-        const float4 b4 = a.p.beta[pid];
+        const float4 b4 = a.p.beta[(((fl >> F_LEN_SHIFT) & 0xffu) > 1u) ? pid : 0u];  // len 1: beta is (1,1,1), not loaded
         const float4 ld4 = a.p.Ld[pid];
         const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
         const bool need_rd = len == 1 && htri < 0;
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         if (!dead && sidx < spp) {  // wavefront_kernels.cu:124
             const Rng r{rng_key(a.seed, pix, sidx), len};
             const bool found = htri >= 0;
-            const V3 B = xyz(b4);
+            const V3 B = len == 1 ? v3(1.f, 1.f, 1.f) : xyz(b4);  // wf_generate's beta (:245)
             V3 film = xyz(ld4);
             bool terminate = false;
             beta_store = B;
@@ -457,7 +457,10 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
                     }
                 }
             }
-            a.p.Ld[pid] = f4(film, ld4.w);
+            // film unchanged bit for bit (a zero contribution): the store would rewrite the same bytes
+            if (__float_as_uint(film.x) != __float_as_uint(ld4.x) || __float_as_uint(film.y) != __float_as_uint(ld4.y) ||
+                __float_as_uint(film.z) != __float_as_uint(ld4.z))
+                a.p.Ld[pid] = f4(film, ld4.w);
             if (terminate) {  // :199-204
                 dead = true;
                 samples++;
@@ -477,7 +480,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             const Rng r0{rng_key(a.seed, pix, sidx), 0u};
             V3 new_o, new_d;
             gen_ray(a.cam, a.W, a.H, x, y, r0, new_o, new_d);
-            a.p.beta[pid] = make_float4(1.f, 1.f, 1.f, 0.f);
+            // beta = (1,1,1) (:245) is implied by len 1: k_shade does not load it for len-1 paths
             nflags = 1u << F_LEN_SHIFT;
             a.p.ray_o[pid] = f4(new_o, 0.f);
             a.p.ray_d[pid] = f4(new_d, 0.f);
