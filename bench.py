@@ -208,6 +208,16 @@ def main():
                         "ext_tri_tests": round(st.ext_tests / max(1, st.extend_rays), 2),
                         "any_pair_nodes": round(st.any_nodes / max(1, st.shadow_rays + st.vis_rays), 2),
                         "any_tri_tests": round(st.any_tests / max(1, st.shadow_rays + st.vis_rays), 2)}}
+    # the streaming stages (logic + generate + material: k_shade and k_material) on their own,
+    # by SURVEY 8(d) state bytes and by the committed PMC traffic
+    t_shd = st.ms_shade / K * 1e-3
+    roof["shade_stages"] = {"ms_per_iteration": round(st.ms_shade / K, 4),
+                            "state_bytes_per_iteration": int(b_shd / K),
+                            "state_frac": round(b_shd / K / t_shd / HBM_PEAK, 4)}
+    shd_traffic = pmc_traffic(names["k_shade"])
+    if shd_traffic is not None:
+        roof["shade_stages"]["traffic"] = shd_traffic
+        roof["shade_stages"]["traffic_frac"] = round(shd_traffic / t_shd / HBM_PEAK, 4)
     # measured HBM ceiling on this device (hand-written dwordx4 copy) beside the spec peak
     copy = pt.hbm_copy_gbps(1 << 30, 20)
     roof["measured_copy_GBps"] = round(copy, 1)
