@@ -263,25 +263,38 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     }
     // Sibling-contiguous numbering for trees that stay in L2: the interior children of a
     // node get consecutive pair indices (one 128-B line holds both, so a popped far child is
-    // often already cached), subtrees in depth-first order after them.  Measured against
-    // plain depth-first numbering (parent and first child adjacent): config 2 (4.8 K pairs)
-    // k_trace 0.804 -> 0.782 ms; configs 3-5 (0.1-2 M pairs, beyond L2) 1-2 % slower, so they
-    // keep depth-first.  MCPT_SIBLING_LAYOUT=0/1 forces either.  Layout only: hits unchanged.
+    // often already cached), level by level (layout 2, breadth-first: the hot top levels
+    // share lines) or depth-first by sibling pairs (layout 1).  Measured against plain
+    // depth-first numbering (layout 0: parent next to its first child) on config 2 (4.8 K
+    // pairs): k_trace 0.808 -> 0.786 (1) -> 0.781 ms (2); configs 3-5 (0.1-2 M pairs, beyond
+    // L2) run 1-2 % slower with 1 or 2, so they keep 0.  MCPT_SIBLING_LAYOUT=0/1/2 forces a
+    // layout.  Layout only: hits are unchanged.
     const char* sl_env = getenv("MCPT_SIBLING_LAYOUT");
-    const bool sibling = sl_env ? atoi(sl_env) != 0 : (size_t)npair * 64 <= ((size_t)2 << 20);
-    if (N > 0 && d->nprims[0] == 0 && sibling) {
+    const int layout = sl_env ? atoi(sl_env) : ((size_t)npair * 64 <= ((size_t)2 << 20) ? 2 : 0);
+    if (N > 0 && d->nprims[0] == 0 && layout != 0) {
         std::vector<int> po(pair_of);
         int next = 0;
         po[0] = next++;
-        std::vector<int> st{0};
-        while (!st.empty() && next <= npair) {
-            const int i = st.back();
-            st.pop_back();
+        std::vector<int> st{0};  // layout 1: stack (depth-first by sibling pairs); 2: FIFO (breadth-first)
+        size_t head = 0;
+        while (head < st.size() && next <= npair) {
+            int i;
+            if (layout == 2) {
+                i = st[head++];
+            } else {
+                i = st.back();
+                st.pop_back();
+            }
             const int ch[2] = {i + 1, d->offset[i]};
             for (int k = 0; k < 2; k++)
                 if (d->nprims[ch[k]] == 0) po[ch[k]] = next++;
-            for (int k = 1; k >= 0; k--)
-                if (d->nprims[ch[k]] == 0) st.push_back(ch[k]);
+            if (layout == 2) {
+                for (int k = 0; k < 2; k++)
+                    if (d->nprims[ch[k]] == 0) st.push_back(ch[k]);
+            } else {
+                for (int k = 1; k >= 0; k--)
+                    if (d->nprims[ch[k]] == 0) st.push_back(ch[k]);
+            }
         }
         if (next == npair) pair_of.swap(po);  // every interior node reached once: a permutation
     }
