@@ -863,6 +863,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         if (act) {
 #pragma unroll 1
           for (int it = 0; it < kNodeSteps; it++) {
+#ifdef MCPT_X_ANYWAIT  // experiment: an any-hit lane with a parked leaf waits for its triangle test
+            if (kind != 0 && leaf != kEnd) break;
+#endif
             bool need_pop = false;
             if (ref >= 0) {
               RAY_STEP_NODE();
