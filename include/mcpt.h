@@ -154,8 +154,14 @@ int mcpt_film_clear(mcpt_ctx *ctx);                                          /* 
  * k, k + S, k + 2S, ... into its own accumulator and the film readers sum the slots in
  * slot order: the same per-sample contributions, summed in another order (films agree to
  * float rounding, samples exactly).  More rays per iteration amortise each launch's ramp
- * and drain.  Re-allocates the path state (the film is cleared). */
+ * and drain.  Re-allocates the path state, so a change CLEARS the film.  A rejected count
+ * (W*H*slots >= 2^31, or out of memory) leaves the previous slot count in place. */
 int mcpt_set_path_slots(mcpt_ctx *ctx, uint32_t slots);
+/* Work partitions of the persistent traversal kernel (0 = device default: two per XCD, 16 on
+ * MI355X; at most 64).  Each partition's rays are handed out by one counter; waves start on a
+ * partition of their die and, once it is drained, join the others, so all settings trace every
+ * ray and give identical results -- a tuning knob only (MCPT_TRACE_PARTS sets the default). */
+int mcpt_set_trace_partitions(mcpt_ctx *ctx, uint32_t nparts);
 int mcpt_set_tiles(mcpt_ctx *ctx, const uint32_t *tile_xy, uint32_t ntiles); /* batch tile set; NULL = all */
 int mcpt_wavefront_step(mcpt_ctx *ctx, uint32_t tile_x, uint32_t tile_y, mcpt_stage_stats *st); /* one iteration, one tile */
 int mcpt_iterate(mcpt_ctx *ctx, uint32_t iterations, mcpt_stage_stats *st);  /* batch iterations over the tile set */
@@ -179,6 +185,10 @@ int mcpt_device_name(mcpt_ctx *ctx, char *buf, int32_t len);
 int mcpt_debug_queue_rays(mcpt_ctx *ctx, int which, float *ray_o, float *ray_d, uint32_t *n_inout);
 float mcpt_debug_last_stage_ms(const mcpt_ctx *ctx);
 float mcpt_debug_last_build_ms(const mcpt_ctx *ctx);  /* device time of the last GPU BVH build */
+/* pair-node numbering of the last uploaded tree: 0 depth-first, 1 depth-first by sibling pairs,
+ * 2 breadth-first (default 2 for trees of <= 2 MiB of nodes, else 0; MCPT_SIBLING_LAYOUT=0/1/2
+ * at upload forces one; inputs that are not a tree -- a shared child -- always get 0). */
+int mcpt_debug_node_layout(const mcpt_ctx *ctx);
 /* k_trace loop profile (diagnostics builds with -DMCPT_TRACE_PROF; returns 0 and zeros otherwise):
  * out12 = {loop trips, refills, node lane-steps, triangle phases, triangle lane-steps, trips with a finish,
  * idle lane-trips, trips with a pop, popping lanes, trips with a non-finite-direction slab, finishing lanes, -}

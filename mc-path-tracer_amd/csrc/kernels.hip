@@ -618,6 +618,20 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
 // wave owns.  Stack: kLdsStack entries per lane in LDS ([entry][lane],
 // conflict-free), deeper entries in private scratch.
 // ---------------------------------------------------------------------------
+// Inclusive scan over the 64 lanes of a wave with DPP moves (no ds_bpermute address
+// registers): Hillis-Steele within each 16-lane row (row_shr 1/2/4/8; lanes shifted past
+// their row's start add the 0 'old' operand), then row 15's total into rows 1 and 3
+// (row_bcast:15) and lane 31's into rows 2 and 3 (row_bcast:31).
+__device__ inline uint32_t wave_scan_incl(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
 // Traversal work counters: wave-reduce, one atomic per counter per wave.
 __device__ inline void wave_stats(uint32_t* stats, int lane, uint32_t nodes, uint32_t tests, uint32_t hits) {
     if (!stats) return;
@@ -648,11 +662,13 @@ __device__ unsigned long long g_trace_prof[12];
 #endif
 constexpr int kNodeSteps = MCPT_NODE_STEPS;
 
-#ifdef MCPT_TRACE_WPE
-#define MCPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_TRACE_WPE, MCPT_TRACE_WPE)))
-#else
-#define MCPT_TRACE_ATTR
+// 7 waves per SIMD (<= 72 VGPRs): the persistent grid's measured optimum (launch_geometry).
+// The attribute lets the register allocator park the partition scan's loop-invariant lane
+// addresses in scratch (two spills, reloaded only by the scan) instead of giving up a wave.
+#ifndef MCPT_TRACE_WPE
+#define MCPT_TRACE_WPE 7
 #endif
+#define MCPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_TRACE_WPE, MCPT_TRACE_WPE)))
 #ifdef MCPT_WAVE_TIMES
 __device__ unsigned long long g_wave_t[4 * 16384];  // per wave: s_memrealtime (100 MHz, chip-wide) at entry and
                                                      // exit, partition, time its partition ran dry for it
@@ -663,62 +679,87 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #endif
     __shared__ int2 stk[kLdsStack][kTraceBlock];
     const int lane = threadIdx.x;
-    // ---- work distribution.  The chip's L2 is per XCD (not coherent with the others
-    // inside a launch), so the queue shards are split into one partition per XCD
-    // (shard s -> partition s mod nparts) and the waves running on an XCD hand out the
-    // 64-ray chunks of its partition with an atomic counter in that XCD's L2
-    // (workgroup-scope atomics are performed in the L2 the XCD's CUs share; the
-    // partition is chosen by the hardware XCC id, so every atomic on a counter runs in
-    // the same L2).  A static split left the waves of a launch finishing anywhere
-    // between 52 % and 100 % of its duration (tools/wave_times.py).
+    // ---- work distribution.  The queue shards are split into nparts partitions
+    // (shard s -> partition s mod nparts; by default one per XCD) and each partition's
+    // rays are handed out by one agent-scope atomic counter (gfx950 performs these at
+    // the memory side: the same instruction as a workgroup-scope add, coherent across
+    // XCDs).  A wave starts on the partition of the die it runs on (hardware XCC id:
+    // the counter's line and the partition's rays stay in that die's L2 -- a speed
+    // choice only).  Once that partition is drained and the wave has no ray left, it
+    // reads every partition's counter and joins the first one (after its own, in
+    // rotation) that still holds rays; it exits when all of them read drained.  So
+    // every queued ray is traced whatever the placement of waves on dies (a die with
+    // no waves, more partitions than dies), and k_accumulate checks per launch that
+    // every counter reached its partition's ray count.  A static split left the waves
+    // of a launch finishing anywhere between 52 % and 100 % of its duration
+    // (tools/wave_times.py).
     const uint32_t nsh = (uint32_t)a.nshards, nparts = a.nparts;
-    uint32_t part = 0;
+    uint32_t home = 0;
     if (nparts > 1) {
         uint32_t xcc;
         __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        part = (xcc & 15u) % nparts;
+        // several partitions per die (nparts a multiple of the die count): consecutive
+        // blocks of a die (blocks are dealt round-robin over the dies) alternate between them
+        const uint32_t nd = a.ndies >= 1 && a.ndies <= nparts && nparts % a.ndies == 0 ? a.ndies : nparts;
+        home = (xcc & 15u) % nd + nd * ((blockIdx.x / nd) % (nparts / nd));  // (nd: XCC ids 0..7)
     }
+    // rays per partition (s_tot), for the drained test of the partition scan
+    __shared__ uint32_t s_tot[kMaxParts];
+    if (lane < kMaxParts) s_tot[lane] = 0;
+    __syncthreads();
+    if ((uint32_t)lane < nsh) {
+        uint32_t n = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const TraceSet& ts = a.set[k];
+            n += ts.count_ptr ? ts.count_ptr[lane * C_WORDS] : (lane == 0 ? ts.count : 0u);
+        }
+        if (n) atomicAdd(&s_tot[lane % nparts], n);
+    }
+    __syncthreads();
     // Partition entries: its shards part, part + nparts, ... (spart of them) of set 0,
     // then the same shards of set 1 (at most 2 * 64 entries: one per lane and half),
     // read as one sequence of rays.  pre(e) = first position of entry e (exclusive prefix;
     // entries past the last and pre(128)
-    // give the total), kept in LDS (s_pre): the kernel has to stay at <= 64 VGPRs for 7
-    // waves per SIMD (gfx950 allocates VGPRs in blocks of 16 here: 65..80 -> 6 waves).
+    // give the total), kept in LDS (s_pre): the kernel has to stay at <= 72 VGPRs for 7
+    // waves per SIMD (gfx950 allocates VGPRs in blocks of 8 here: 73..80 -> 6 waves).
     // Rays are handed out exactly as lanes fall idle (an atomic add of the idle count):
     // a wave reserves no rays ahead, so when the partition runs dry each wave only
-    // finishes its lanes.
+    // finishes its lanes.  (The block is one wave: s_pre is rewritten in program order
+    // after its last read.)
     __shared__ uint32_t s_pre[129];
-    const uint32_t spart = nsh > part ? (nsh - part + nparts - 1) / nparts : 0u;
-    uint32_t T;  // rays in the partition
-    {
-        uint32_t ne[2], inc[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
+    uint32_t part = home, spart = 0, T = 0;  // T: rays in the current partition
+    uint32_t* grab = a.grab;
+    bool more = false;  // the current partition may still hold rays
+    // join partition p: its entry prefix into s_pre, its ray count into T
+    auto enter = [&](uint32_t p) {
+        part = __builtin_amdgcn_readfirstlane(p);  // (wave-uniform: keep it, spart and T in SGPRs)
+        spart = __builtin_amdgcn_readfirstlane(nsh > part ? (nsh - part + nparts - 1) / nparts : 0u);
+        // the two halves one after the other: this code sits inside the traversal loop,
+        // where every temporary counts against the VGPR budget of 7 waves per SIMD
+        uint32_t base = 0;
+#pragma unroll 1
+        for (uint32_t h = 0; h < 2; h++) {
             const uint32_t e = (uint32_t)lane + 64u * h;
             const bool k1 = e >= spart;
             const uint32_t j = k1 ? e - spart : e;
-            ne[h] = 0;
+            uint32_t ne = 0;
             if (e < 2 * spart) {
                 const TraceSet& ts = k1 ? a.set[1] : a.set[0];
                 const uint32_t sh = part + j * nparts;
-                ne[h] = ts.count_ptr ? ts.count_ptr[sh * C_WORDS] : (sh == 0 ? ts.count : 0u);
+                ne = ts.count_ptr ? ts.count_ptr[sh * C_WORDS] : (sh == 0 ? ts.count : 0u);
             }
-            inc[h] = ne[h];
-            for (int off = 1; off < 64; off <<= 1) {  // inclusive scan over the lanes
-                const uint32_t v = __shfl_up(inc[h], off);
-                if (lane >= off) inc[h] += v;
-            }
+            const uint32_t inc = wave_scan_incl(ne);
+            s_pre[e] = base + inc - ne;
+            base += __builtin_amdgcn_readlane(inc, 63);
         }
-        const uint32_t t0 = __shfl(inc[0], 63);
-        T = __builtin_amdgcn_readfirstlane(t0 + __shfl(inc[1], 63));
-        s_pre[lane] = inc[0] - ne[0];
-        s_pre[64 + lane] = t0 + inc[1] - ne[1];
+        T = __builtin_amdgcn_readfirstlane(base);
         if (lane == 0) s_pre[128] = T;
         __syncthreads();
-    }
-    if (T == 0) return;
-    uint32_t* const grab = a.grab + part * C_WORDS;
-    bool more = true;  // the partition may still hold rays
+        grab = a.grab + part * C_WORDS;
+        more = T > 0;
+    };
+    enter(home);
     const DevScene& sc = a.scene;
 
     // per-lane work counters per set (wave-reduced at exit); per-ray step counts only in
@@ -732,6 +773,13 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #define RAY_STEP_NODE() ((void)0)
 #define RAY_STEP_TRI() ((void)0)
 #endif
+#ifdef MCPT_TRACE_PROF
+    uint64_t prof[12] = {};  // see mcpt_debug_trace_profile
+#endif
+    uint64_t drained = 0;  // partitions this wave saw run dry (by an atomic: never stale)
+    for (;;) {  // one trip per partition joined
+    // Per-lane ray state is declared per partition trip: when the trip ends no lane holds a
+    // ray, so none of it is live across the partition scan below (VGPR budget).
     bool act = false;
     int kind = 0;  // 0 closest, 1 any
     uint32_t rid = 0;
@@ -777,9 +825,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         else a.hit_tri[rid] = tri;                  // hit record rebuilt by the consumer (hit_record())
         act = false;
     };
-#ifdef MCPT_TRACE_PROF
-    uint64_t prof[12] = {};  // see mcpt_debug_trace_profile
-#endif
     for (;;) {
         PROF_ADD(0, 1);
         // ---- refill idle lanes with the partition's next rays
@@ -787,9 +832,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if (more && (nidle >= a.refill_min || nidle == 64u)) {
             uint32_t p0 = 0;
-            if (lane == 0) p0 = __hip_atomic_fetch_add(grab, nidle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lane == 0) p0 = __hip_atomic_fetch_add(grab, nidle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             p0 = __builtin_amdgcn_readfirstlane(p0);
-            if (p0 + nidle >= T) more = false;  // the rest of the partition is taken
+            if (p0 + nidle >= T) {  // the rest of the partition is taken
+                more = false;
+                drained |= 1ull << part;
+            }
             const uint32_t q = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             const uint32_t pos = p0 + q;  // meaningful on idle lanes
@@ -855,7 +903,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             PROF_ADD(1, 1);
         }
         if (__ballot(act) == 0) {
-            if (!more) break;
+            if (!more) break;  // partition drained, every lane idle
             continue;
         }
         // ---- node phase: up to kNodeSteps child-pair tests per lane holding an
@@ -1033,6 +1081,34 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #endif
         if (act && ref == kEnd && leaf == kEnd) finish();
     }
+#ifdef MCPT_X_NOSTEAL  // experiment: home partition only (round 1's scheme: needs a wave on every die)
+    break;
+#endif
+    // ---- partition scan: read every counter (one lane each) and join the first
+    // partition after the current one that still holds rays.  A stale read (this die's
+    // L2 holding an old copy of a counter line) can only be lower than the true count, so
+    // a partition that reads drained is drained.  One that reads open but is not costs
+    // one atomic, which marks it in `drained`; every other join takes rays.  So the scans
+    // end, with every partition's counter at or past its ray count.
+    {
+        uint32_t g = 0;
+        const bool cand = (uint32_t)lane < nparts && !((drained >> lane) & 1ull);
+        if (cand) g = __hip_atomic_load(a.grab + lane * C_WORDS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t open = __ballot(cand && g < s_tot[lane]);
+        if (open == 0) break;  // every partition drained
+#ifndef MCPT_X_PICK_NEXT
+        // the open partition with the most rays left (lowest index on ties): waves that
+        // run dry spread over the remaining work instead of queueing on one counter
+        const uint32_t rem = min(s_tot[lane] - g, (1u << 25) - 1u);
+        uint32_t key = (open >> lane) & 1ull ? (rem << 6) | (63u - (uint32_t)lane) : 0u;
+        for (int off = 32; off > 0; off >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, off));
+        enter(63u - (__builtin_amdgcn_readfirstlane(key) & 63u));
+#else  // experiment: the first open partition after the current one
+        const uint64_t after = open & ~((2ull << part) - 1ull);  // partitions past the current one
+        enter((uint32_t)__builtin_ctzll(after ? after : open));
+#endif
+    }
+    }
 #ifdef MCPT_TRACE_PROF
     if (lane == 0)
         for (int i = 0; i < 12; i++) atomicAdd(&g_trace_prof[i], (unsigned long long)prof[i]);
@@ -1107,7 +1183,7 @@ __global__ void k_tonemap(TonemapArgs a) {  // draw_to_surface (wavefront_kernel
     a.out[i] = o;
 }
 
-__global__ void k_accumulate(CounterBlock* c) {  // fold per-iteration shard counts into 64-bit totals
+__global__ void k_accumulate(CounterBlock* c, uint32_t nparts) {  // fold per-iteration shard counts into 64-bit totals
     const int t = threadIdx.x;  // one lane per shard
     uint32_t v[C_STATS + 6];
 #pragma unroll
@@ -1116,9 +1192,20 @@ __global__ void k_accumulate(CounterBlock* c) {  // fold per-iteration shard cou
         c->shard[t][k] = 0;
     }
     c->last_ext_shard[t] = v[C_EXT];
+    // drain check of the k_trace launch: every partition's hand-out counter must have
+    // reached the partition's queued rays (shards t = p mod nparts)
+    __shared__ uint32_t s_part[kMaxParts];
+    if (t < kMaxParts) s_part[t] = 0;
+    __syncthreads();
+    atomicAdd(&s_part[t % nparts], v[C_EXT] + v[C_ANY]);
+    __syncthreads();
+    uint32_t g = 0;
+    if (t < kMaxParts) g = c->grab[t][0];
+    const bool short_part = t < (int)nparts && g < s_part[t];
 #pragma unroll
     for (int k = 0; k < C_STATS + 6; k++)
         for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    if (__ballot(short_part) != 0 && t == 0) c->trace_short += 1;
     if (t < kMaxParts) c->grab[t][0] = 0;  // k_trace chunk hand-out counters
     uint32_t er = c->shard[t][C_EXT_RAYS], ar = c->shard[t][C_ANY_RAYS];
     c->shard[t][C_EXT_RAYS] = 0;
@@ -1159,68 +1246,63 @@ __global__ void k_pack(PackArgs a) {  // tile-set pixels -> packed 16 B/px (for 
 // ---------------------------------------------------------------------------
 // Material grid: resident blocks (occupancy calculator x CUs) rounded down to a multiple of
 // the shard count (at least one block per shard).
-template <bool FIXED>
-static uint32_t material_blocks() {
-    static uint32_t b = [] {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_material<FIXED>, kBlock, 0);
-        if (cus <= 0) cus = 256;
-        if (per_cu <= 0) per_cu = 4;
-        return (uint32_t)std::max(1, cus * per_cu / kShards) * (uint32_t)kShards;
-    }();
-    return b;
-}
-void launch_shade(const ShadeArgs& a, int nblocks, bool fixed_mode, hipStream_t s) {
-    if (fixed_mode) {
-        hipLaunchKernelGGL(k_shade<true>, dim3(nblocks), dim3(kBlock), 0, s, a);
-        hipLaunchKernelGGL(k_material<true>, dim3(material_blocks<true>()), dim3(kBlock), 0, s, a);
-    } else {
-        hipLaunchKernelGGL(k_shade<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
-        hipLaunchKernelGGL(k_material<false>, dim3(material_blocks<false>()), dim3(kBlock), 0, s, a);
-    }
-}
-// Persistent grid: resident waves per CU from the occupancy calculator
-// (MCPT_TRACE_WAVES overrides), rounded to a multiple of the shard count.
 static uint32_t env_u32(const char* name, int def, int lo, int hi) {
     const char* e = getenv(name);
     int v = e ? atoi(e) : def;
     return (uint32_t)std::min(hi, std::max(lo, v));
 }
-static uint32_t persistent_waves() {
-    static uint32_t w = [] {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace, kTraceBlock, 0);
-        // At most 7 waves per SIMD: on config 2 the launch takes 0.406 / 0.368 / 0.354 /
-        // 0.329 / 0.382 ms at 16 / 20 / 24 / 28 / 32 waves per CU (more resident rays
-        // thrash the per-CU L1 with unrelated node fetches past 28).
-        per_cu = std::min(per_cu, 28);
-        if (const char* e = getenv("MCPT_TRACE_WAVES")) per_cu = atoi(e);
-        if (cus <= 0) cus = 256;
-        if (per_cu <= 0) per_cu = 16;
-        return (uint32_t)(cus * per_cu);
-    }();
-    return w;
+// Per-device launch geometry, computed once per context (mcpt_create) for the device
+// the context owns.
+//  * k_material: resident blocks (occupancy calculator x CUs) rounded down to a multiple
+//    of the shard count (at least one block per shard).
+//  * k_trace: resident waves per CU from the occupancy calculator, at most 28 (7 per
+//    SIMD): on config 2 the launch takes 0.406 / 0.368 / 0.354 / 0.329 / 0.382 ms at
+//    16 / 20 / 24 / 28 / 32 waves per CU (more resident rays thrash the per-CU L1 with
+//    unrelated node fetches past 28).  MCPT_TRACE_WAVES overrides the waves per CU.
+//  * k_trace partitions: two per XCD, MCPT_TRACE_PARTS overrides.
+int launch_geometry(int dev, LaunchGeom& g) {
+    int cus = 0, nx = 1, per_cu = 0, mat0 = 0, mat1 = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess) nx = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace, kTraceBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat0, k_material<false>, kBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat1, k_material<true>, kBlock, 0) != hipSuccess)
+        return -1;
+    if (cus <= 0) cus = 256;
+    per_cu = std::min(per_cu, 28);
+    if (const char* e = getenv("MCPT_TRACE_WAVES")) per_cu = atoi(e);
+    if (per_cu <= 0) per_cu = 16;
+    g.trace_waves = (uint32_t)(cus * per_cu);
+    g.ndies = (uint32_t)std::max(1, nx);
+    // Two partitions (hand-out counters) per die: one counter per die serialised the
+    // returning atomics (config 2 k_trace 0.82 ms at 8 partitions, 0.767 at 16, 0.766 at
+    // 32, 0.779 at 64; interleaved runs on one box)
+    g.trace_parts = env_u32("MCPT_TRACE_PARTS", std::min(kMaxParts, 2 * std::max(1, nx)), 1, kMaxParts);
+    g.mat_blocks[0] = (uint32_t)std::max(1, cus * std::max(1, mat0) / kShards) * (uint32_t)kShards;
+    g.mat_blocks[1] = (uint32_t)std::max(1, cus * std::max(1, mat1) / kShards) * (uint32_t)kShards;
+    g.refill_min = env_u32("MCPT_REFILL_MIN", 16, 1, 64);
+    g.tri_min = env_u32("MCPT_TRI_MIN", 16, 0, 64);
+    return 0;
 }
-void launch_trace(const TraceArgs& args, hipStream_t s) {
+void launch_shade(const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fixed_mode, hipStream_t s) {
+    if (fixed_mode) {
+        hipLaunchKernelGGL(k_shade<true>, dim3(nblocks), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(k_material<true>, dim3(g.mat_blocks[1]), dim3(kBlock), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_shade<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(k_material<false>, dim3(g.mat_blocks[0]), dim3(kBlock), 0, s, a);
+    }
+}
+// Persistent grid: the device's resident waves rounded to a multiple of the shard count.
+void launch_trace(const TraceArgs& args, const LaunchGeom& g, hipStream_t s) {
     if (args.nshards <= 0) return;
     TraceArgs a = args;
-    static const uint32_t refill_min = env_u32("MCPT_REFILL_MIN", 16, 1, 64);
-    static const uint32_t tri_min = env_u32("MCPT_TRI_MIN", 16, 0, 64);
-    a.refill_min = refill_min;
-    a.tri_min = tri_min;
-    static const uint32_t nparts = [] {  // one work partition per XCD (L2 domain)
-        int dev = 0, nx = 1;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess) nx = 1;
-        return (uint32_t)std::min(kMaxParts, std::max(1, nx));
-    }();
-    a.nparts = nparts;
+    a.refill_min = g.refill_min;
+    a.tri_min = g.tri_min;
+    a.nparts = std::min<uint32_t>(kMaxParts, std::max<uint32_t>(1, g.trace_parts));
+    a.ndies = g.ndies;
     const uint32_t nsh = (uint32_t)a.nshards;
-    const uint32_t wps = std::max<uint32_t>(1, persistent_waves() / nsh);
+    const uint32_t wps = std::max<uint32_t>(1, g.trace_waves / nsh);
     hipLaunchKernelGGL(k_trace, dim3(wps * nsh), dim3(kTraceBlock), 0, s, a);
 }
 __global__ void k_quot(const float* a, const float* b, float* out, uint32_t n) {  // mcpt_debug_quot
@@ -1292,7 +1374,9 @@ void launch_resolve(const ResolveArgs& a, hipStream_t s) {
 void launch_tonemap(const TonemapArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_tonemap, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
-void launch_accumulate(CounterBlock* c, hipStream_t s) { hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(kShards), 0, s, c); }
+void launch_accumulate(CounterBlock* c, uint32_t nparts, hipStream_t s) {
+    hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(kShards), 0, s, c, std::min<uint32_t>(kMaxParts, std::max<uint32_t>(1, nparts)));
+}
 void launch_pack(const PackArgs& a, hipStream_t s) {
     uint32_t n = (uint32_t)(a.ntiles * a.tile_w * a.tile_h);
     hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, s, a);

@@ -73,13 +73,15 @@ struct DevPaths {
 // roughly 90 atomics per microsecond, which is what ~24K pushes and ~100K
 // statistics adds per iteration would otherwise cost.
 constexpr int kShards = 64;
-constexpr int kMaxParts = 16;  // k_trace work partitions (one per XCD; MI355X has 8)
+constexpr int kMaxParts = kShards;  // k_trace work partitions (at most one per queue shard)
 enum : int { C_EXT = 0, C_ANY = 1, C_VIS = 2, C_STATS = 3, C_EXT_RAYS = 9, C_ANY_RAYS = 10, C_MAT = 11, C_WORDS = 32 };  // C_STATS..+5
 struct CounterBlock {
     uint32_t shard[kShards][C_WORDS];  // [0] ext pushes [1] any-hit pushes [2] vis rays [3..8] traversal stats [9,10] rays [11] material pushes
-    uint32_t last_ext, last_live, pad[30];
+    uint32_t last_ext, last_live;
+    uint32_t trace_short;  // k_trace launches that left a partition's rays untraced (k_accumulate; must stay 0)
+    uint32_t pad[29];
     uint32_t last_ext_shard[kShards];  // per-shard extension pushes of the last iteration
-    uint32_t grab[kMaxParts][C_WORDS];  // k_trace chunk hand-out, one counter line per XCD partition
+    uint32_t grab[kMaxParts][C_WORDS];  // k_trace ray hand-out, one counter line per partition
     unsigned long long tot_ext, tot_any, tot_vis, pad2;
     unsigned long long tot_stats[6];
 };
@@ -123,7 +125,8 @@ struct TraceArgs {
     uint8_t* vis;               // any-hit output: 1 = unoccluded
     uint32_t refill_min;        // refill when at least this many lanes are idle (set by launch_trace)
     uint32_t tri_min;           // run the triangle phase when this many lanes hold a leaf (set by launch_trace)
-    uint32_t nparts;            // work partitions = XCDs of the device (set by launch_trace)
+    uint32_t nparts;            // work partitions (default: the device's XCDs; set by launch_trace)
+    uint32_t ndies;             // XCDs of the device (set by launch_trace)
     uint32_t* grab;             // nparts chunk counters, C_WORDS apart, zero at launch (k_accumulate resets)
 };
 
@@ -133,8 +136,18 @@ struct ResolveArgs { const float4* Ld; const uint32_t* samples; float4* out_Ld; 
 struct TonemapArgs { const float4* Ld; const uint32_t* samples; uchar4* out; float exposure; uint32_t n; };
 struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* out; };
 
-void launch_shade(const ShadeArgs& a, int nblocks, bool fixed_mode, hipStream_t s);
-void launch_trace(const TraceArgs& a, hipStream_t s);
+// Launch geometry of one device (mcpt_create): persistent grids from the occupancy
+// calculator and the device's XCD count, with environment overrides for sweeps.
+struct LaunchGeom {
+    uint32_t trace_waves;    // k_trace grid (waves), MCPT_TRACE_WAVES = waves per CU
+    uint32_t trace_parts;    // k_trace work partitions, MCPT_TRACE_PARTS (1..kMaxParts)
+    uint32_t ndies;          // XCDs
+    uint32_t mat_blocks[2];  // k_material grid [reference mode, fixed mode]
+    uint32_t refill_min, tri_min;  // MCPT_REFILL_MIN, MCPT_TRI_MIN
+};
+int launch_geometry(int device, LaunchGeom& g);  // device must be current
+void launch_shade(const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fixed_mode, hipStream_t s);
+void launch_trace(const TraceArgs& a, const LaunchGeom& g, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
 
 // GPU linear BVH (bvh_build.hip).  Inputs: host vertex arrays (3 floats per
@@ -153,7 +166,7 @@ void launch_copy(const float4* src, float4* dst, size_t n, hipStream_t s);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);
 void launch_resolve(const ResolveArgs& a, hipStream_t s);
-void launch_accumulate(CounterBlock* c, hipStream_t s);
+void launch_accumulate(CounterBlock* c, uint32_t nparts, hipStream_t s);
 void launch_pack(const PackArgs& a, hipStream_t s);
 
 }  // namespace mcpt_dev

@@ -33,12 +33,15 @@ struct mcpt_ctx {
     mcpt_config cfg{};
     char devname[256] = {0};
     int num_cu = 0;
+    LaunchGeom geom{};             // persistent grids and k_trace partitions of this device
+    uint32_t trace_parts_default = 1;
     // scene
     std::vector<void*> scene_bufs;
     DevScene scene{};
     bool has_scene = false;
     bool has_scene_before = false;  // set at the start of a re-upload
     int pair_depth = 0;
+    int node_layout = 0;  // pair-node numbering the last upload used (mcpt_debug_node_layout)
     // camera
     mcpt::CamView cam{};
     bool has_cam = false;
@@ -136,6 +139,11 @@ int mcpt_create(int device, const mcpt_config* cfg, mcpt_ctx** out) {
         return set_err(nullptr, MCPT_E_NOMEM, "counter allocation failed");
     }
     (void)hipMemset(c->cnt, 0, sizeof(CounterBlock));
+    if (launch_geometry(device, c->geom) != 0) {
+        mcpt_destroy(c);
+        return set_err(nullptr, MCPT_E_HIP, "occupancy query failed");
+    }
+    c->trace_parts_default = c->geom.trace_parts;
     *out = c;
     return MCPT_OK;
 }
@@ -268,16 +276,25 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     // depth-first numbering (layout 0: parent next to its first child) on config 2 (4.8 K
     // pairs): k_trace 0.808 -> 0.786 (1) -> 0.781 ms (2); configs 3-5 (0.1-2 M pairs, beyond
     // L2) run 1-2 % slower with 1 or 2, so they keep 0.  MCPT_SIBLING_LAYOUT=0/1/2 forces a
-    // layout.  Layout only: hits are unchanged.
+    // layout (other values are ignored).  Layout only: hits are unchanged (tested).
     const char* sl_env = getenv("MCPT_SIBLING_LAYOUT");
-    const int layout = sl_env ? atoi(sl_env) : ((size_t)npair * 64 <= ((size_t)2 << 20) ? 2 : 0);
+    int layout = (size_t)npair * 64 <= ((size_t)2 << 20) ? 2 : 0;
+    if (sl_env && sl_env[0] >= '0' && sl_env[0] <= '2' && sl_env[1] == 0) layout = sl_env[0] - '0';
+    c->node_layout = 0;
     if (N > 0 && d->nprims[0] == 0 && layout != 0) {
+        // Renumber by walking the tree from the root.  The walk must reach every interior
+        // node exactly once (a tree); a shared child (a DAG, which the validation above
+        // accepts and layout 0 traverses correctly) or an unreachable node would give two
+        // nodes one pair index, so such inputs keep layout 0.
         std::vector<int> po(pair_of);
+        std::vector<uint8_t> seen(N, 0);
         int next = 0;
         po[0] = next++;
+        seen[0] = 1;
+        bool tree = true;
         std::vector<int> st{0};  // layout 1: stack (depth-first by sibling pairs); 2: FIFO (breadth-first)
         size_t head = 0;
-        while (head < st.size() && next <= npair) {
+        while (tree && (layout == 2 ? head < st.size() : !st.empty())) {
             int i;
             if (layout == 2) {
                 i = st[head++];
@@ -286,8 +303,12 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
                 st.pop_back();
             }
             const int ch[2] = {i + 1, d->offset[i]};
-            for (int k = 0; k < 2; k++)
-                if (d->nprims[ch[k]] == 0) po[ch[k]] = next++;
+            for (int k = 0; k < 2 && tree; k++) {
+                if (d->nprims[ch[k]] != 0) continue;
+                if (seen[ch[k]]) tree = false;  // reached twice
+                seen[ch[k]] = 1;
+                po[ch[k]] = next++;
+            }
             if (layout == 2) {
                 for (int k = 0; k < 2; k++)
                     if (d->nprims[ch[k]] == 0) st.push_back(ch[k]);
@@ -296,7 +317,10 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
                     if (d->nprims[ch[k]] == 0) st.push_back(ch[k]);
             }
         }
-        if (next == npair) pair_of.swap(po);  // every interior node reached once: a permutation
+        if (tree && next == npair) {  // every interior node reached exactly once: a permutation
+            pair_of.swap(po);
+            c->node_layout = layout;
+        }
     }
     // A leaf with several triangles becomes a small subtree of pair nodes whose leaves
     // hold one triangle each, boxed by its own bounds (the vertex union,
@@ -507,6 +531,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
 int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) { return scene_upload(c, d, false); }
 int mcpt_scene_upload_gpu_bvh(mcpt_ctx* c, const mcpt_scene_desc* d) { return scene_upload(c, d, true); }
 float mcpt_debug_last_build_ms(const mcpt_ctx* c) { return c ? c->last_build_ms : -1.f; }
+int mcpt_debug_node_layout(const mcpt_ctx* c) { return c ? c->node_layout : MCPT_E_INVALID; }
 
 int mcpt_camera_set(mcpt_ctx* c, const mcpt_camera* cam) {
     if (!c || !cam) return set_err(c, MCPT_E_INVALID, "null argument");
@@ -669,7 +694,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     int bpt = (int)((c->tile_w * c->tile_h + kBlock - 1) / kBlock);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 0), c->stream));
     if (sa.ntiles > 0)
-        launch_shade(sa, sa.ntiles * bpt * (int)c->slots, (c->cfg.flags & MCPT_FLAG_FIXED) != 0, c->stream);
+        launch_shade(sa, sa.ntiles * bpt * (int)c->slots, c->geom, (c->cfg.flags & MCPT_FLAG_FIXED) != 0, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 1), c->stream));
     // extension (closest hit) and any-hit rays in one persistent launch
     TraceArgs ta{};
@@ -694,9 +719,9 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     ta.hit_tri = c->p.hit_tri;
     ta.vis = c->p.vis;
     ta.grab = &c->cnt->grab[0][0];  // reset by k_accumulate below
-    launch_trace(ta, c->stream);
+    launch_trace(ta, c->geom, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
-    launch_accumulate(c->cnt, c->stream);
+    launch_accumulate(c->cnt, c->geom.trace_parts, c->stream);
     HIPCHK(c, hipGetLastError());
     return MCPT_OK;
 }
@@ -717,6 +742,9 @@ static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st) {
     HIPCHK(c, hipMemcpyAsync(c->cnt_host, c->cnt, sizeof(CounterBlock), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const CounterBlock& after = *c->cnt_host;
+    if (after.trace_short != before.trace_short)  // k_accumulate's drain check (never expected)
+        return set_err(c, MCPT_E_HIP, "k_trace left queued rays untraced in " +
+                                          std::to_string(after.trace_short - before.trace_short) + " launch(es)");
     if (st) {
         memset(st, 0, sizeof(*st));
         st->extend_rays = after.tot_ext - before.tot_ext;
@@ -836,8 +864,10 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
     }
     ta.grab = &c->cnt->grab[0][0];
     HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
-    launch_trace(ta, c->stream);
+    launch_trace(ta, c->geom, c->stream);
     HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
+    uint32_t grab0 = 0;  // drain check: the one shard is partition 0's
+    HIPCHK(c, hipMemcpyAsync(&c->cnt_host->grab[0][0], &c->cnt->grab[0][0], sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemsetAsync(c->cnt->grab, 0, sizeof(c->cnt->grab), c->stream));  // hand-out counters back to 0
     if (stage == MCPT_STAGE_EXTEND) {
         HitRecordArgs ha{c->scene, dro, drd, ht, hp, hn, ht, n};  // ht: positions in, scene indices out
@@ -846,6 +876,8 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipEventElapsedTime(&c->last_stage_ms, c->events[0], c->events[1]));
+    grab0 = c->cnt_host->grab[0][0];
+    if (grab0 < n) return set_err(c, MCPT_E_HIP, "k_trace left rays untraced");
     if (steps) HIPCHK(c, hipMemcpy(out->steps, steps, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (stage == MCPT_STAGE_EXTEND) {
         std::vector<float4> a(n), b(n);
@@ -888,8 +920,29 @@ static int film_view(mcpt_ctx* c, const float4** Ld, const uint32_t** samples) {
 int mcpt_set_path_slots(mcpt_ctx* c, uint32_t slots) {
     if (!c || slots < 1 || slots > 64) return set_err(c, MCPT_E_INVALID, "path slots must be 1..64");
     if (slots == c->slots) return MCPT_OK;
+    if (!c->P) {
+        c->slots = slots;
+        return MCPT_OK;
+    }
+    // check the new size before touching anything: a rejected count leaves the film as it was
+    if ((uint64_t)c->P * slots >= (1ull << 31)) return set_err(c, MCPT_E_INVALID, "film too large for the path slots");
+    const uint32_t old = c->slots;
     c->slots = slots;
-    return c->P ? mcpt_film_resize(c, c->W, c->H, c->tile_w, c->tile_h) : MCPT_OK;
+    int rc = mcpt_film_resize(c, c->W, c->H, c->tile_w, c->tile_h);  // clears the film
+    if (rc != MCPT_OK) {  // e.g. out of memory: back to the old slot count and its (cleared) film
+        const std::string err = c->err;
+        c->slots = old;
+        (void)mcpt_film_resize(c, c->W, c->H, c->tile_w, c->tile_h);
+        return set_err(c, rc, err);
+    }
+    return MCPT_OK;
+}
+
+int mcpt_set_trace_partitions(mcpt_ctx* c, uint32_t nparts) {
+    if (!c || nparts > (uint32_t)kMaxParts)
+        return set_err(c, MCPT_E_INVALID, "trace partitions must be 0 (device default) .. " + std::to_string(kMaxParts));
+    c->geom.trace_parts = nparts ? nparts : c->trace_parts_default;
+    return MCPT_OK;
 }
 
 int mcpt_film_read(mcpt_ctx* c, float* Ld, uint32_t* samples) {

@@ -90,6 +90,7 @@ ABI = {
     "mcpt_film_clear": (C.c_int, [C.c_void_p]),
     "mcpt_set_tiles": (C.c_int, [C.c_void_p, _u, C.c_uint32]),
     "mcpt_set_path_slots": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "mcpt_set_trace_partitions": (C.c_int, [C.c_void_p, C.c_uint32]),
     "mcpt_wavefront_step": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(StageStats)]),
     "mcpt_iterate": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(StageStats)]),
     "mcpt_render": (C.c_int, [C.c_void_p, C.POINTER(StageStats)]),
@@ -103,6 +104,7 @@ ABI = {
     "mcpt_debug_queue_rays": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _u]),
     "mcpt_debug_last_stage_ms": (C.c_float, [C.c_void_p]),
     "mcpt_debug_last_build_ms": (C.c_float, [C.c_void_p]),
+    "mcpt_debug_node_layout": (C.c_int, [C.c_void_p]),
     "mcpt_scene_upload_gpu_bvh": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mcpt_film_size": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "mcpt_film_write_png": (C.c_int, [C.c_void_p, C.c_float, C.c_char_p]),
@@ -376,6 +378,10 @@ class PathTracer:
     def set_path_slots(self, slots):
         """Paths in flight per pixel (mcpt_set_path_slots); re-allocates and clears the film."""
         self._ck(lib().mcpt_set_path_slots(self.h, slots))
+
+    def set_trace_partitions(self, nparts=0):
+        """k_trace work partitions (mcpt_set_trace_partitions); 0 = one per XCD of the device."""
+        self._ck(lib().mcpt_set_trace_partitions(self.h, nparts))
 
     def set_tiles(self, tiles=None):
         if tiles is None:

@@ -592,3 +592,85 @@ def test_sah3_tree_same_results(mcpt_mod, oracle, scene_c2):
     assert np.array_equal(smp, rs)
     assert np.array_equal(Ld.view(np.uint32), np.asarray(rL).reshape(Ld.shape).view(np.uint32))
     pt.close()
+
+
+@pytest.mark.parametrize("nparts", [1, 3, 12, 64])
+def test_trace_partitions_trace_every_ray(mcpt_mod, oracle, scene_c2, nparts):
+    """k_trace work partitions: waves start on a partition of their die and, once it is drained,
+    join the others, so any partition count traces every queued ray.  12 partitions on 8 dies
+    leaves four with no home waves at all (drained only by joining waves); 3 does not divide the
+    64 shards evenly; 64 is one shard each.  Films, ray counts and the per-launch drain check
+    (k_accumulate) must not change."""
+    rc = mcpt_mod.CONFIGS[2]
+    W, H = 320, 180
+    cam = mcpt_mod.config_camera(rc, W, H)
+    ref = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 3, rc.max_depth)
+    st_ref = ref.render()
+    L_ref, s_ref = ref.film()
+    pt = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 3, rc.max_depth)
+    pt.set_trace_partitions(nparts)
+    st = pt.render()  # raises if a launch left rays untraced
+    L, s = pt.film()
+    assert np.array_equal(s, s_ref) and st.rays == st_ref.rays
+    assert np.array_equal(L.view(np.uint32), L_ref.view(np.uint32))
+    # the single-shard trace API (mcpt_stage_run) under the same partition count
+    ro, rd = random_rays(50000, 9)
+    _, _, gt = pt.trace_closest(ro, rd)
+    assert np.array_equal(gt, oracle.trace_closest(scene_c2[1], ro, rd)[2])
+    assert np.array_equal(pt.trace_any(ro, rd), oracle.trace_any(scene_c2[1], ro, rd))
+    with pytest.raises(mcpt_mod.McptError):
+        pt.set_trace_partitions(65)
+    pt.close()
+    ref.close()
+
+
+def test_node_layouts_same_hits(mcpt_mod, oracle, scene_c2):
+    """Pair-node numberings 0 (depth-first), 1 (sibling pairs, depth-first) and 2 (breadth-first)
+    are layout only: bit-identical hits and visibility; out-of-range MCPT_SIBLING_LAYOUT values
+    are ignored (the size-based default, 2 for config 2's small tree)."""
+    s, a = scene_c2
+    ro, rd = random_rays(100000, 33)
+    ref = None
+    old = os.environ.get("MCPT_SIBLING_LAYOUT")
+    try:
+        for layout in ("0", "1", "2", "3", "x"):
+            os.environ["MCPT_SIBLING_LAYOUT"] = layout
+            pt = mcpt_mod.PathTracer(0)
+            pt.upload_scene(s)
+            got = mcpt_mod.lib().mcpt_debug_node_layout(pt.h)
+            assert got == (int(layout) if layout in "012" else 2)
+            p, n, t = pt.trace_closest(ro, rd)
+            v = pt.trace_any(ro, rd)
+            if ref is None:
+                ref = (p, n, t, v)
+                assert np.array_equal(t, oracle.trace_closest(a, ro, rd)[2])
+            else:
+                assert np.array_equal(t, ref[2]) and np.array_equal(v, ref[3])
+                assert np.array_equal(p.view(np.uint32), ref[0].view(np.uint32))
+                assert np.array_equal(n.view(np.uint32), ref[1].view(np.uint32))
+            pt.close()
+    finally:
+        if old is None:
+            os.environ.pop("MCPT_SIBLING_LAYOUT", None)
+        else:
+            os.environ["MCPT_SIBLING_LAYOUT"] = old
+
+
+def test_path_slots_rejected_count_keeps_film(mcpt_mod, scene_c1):
+    """mcpt_set_path_slots checks W*H*slots < 2^31 before touching the film: a rejected count
+    leaves the slot count and the accumulated film in place; an accepted one clears it."""
+    W, H = 8192, 4096  # 2^25 pixels: 64 slots would be 2^31 paths
+    cam = mcpt_mod.config_camera(mcpt_mod.CONFIGS[1], W, H)
+    pt = make_pt(mcpt_mod, scene_c1[0], cam, W, H, 1, 1)
+    pt.set_tiles([(0, 0)])
+    pt.iterate(3)
+    Ld0, s0 = pt.film()
+    assert s0[:256, :256].sum() > 0
+    with pytest.raises(mcpt_mod.McptError):
+        pt.set_path_slots(64)  # rejected up front
+    Ld1, s1 = pt.film()
+    assert np.array_equal(s1, s0) and np.array_equal(Ld1.view(np.uint32), Ld0.view(np.uint32))
+    pt.set_path_slots(2)
+    _, s2 = pt.film()
+    assert s2.sum() == 0  # accepted change: film cleared
+    pt.close()
