@@ -29,6 +29,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "mc-path-tracer_amd"))
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+L2_PEAK = 34.5e12  # aggregate L2 bandwidth over the 8 XCDs (MI355X_MICROARCH.md, L2 section)
 # SURVEY.md 8(d) algorithmic bytes per unit of work
 B_EXT_STATE = 65      # extend: queue 4 + ray 24 + len 4 read, len/found/pos/n/mat 33 written
 B_ANY_STATE = 33      # shadow: queue 4 + ray 24 + light id 4 read, visible 1 written
@@ -59,19 +60,50 @@ def tiles_for(rank, world, W, H, tile):
     return [(tx, ty) for ty in range(ny) for tx in range(nx) if (tx + ty) % world == rank]
 
 
-def pmc_traffic(kernel_prefix):
-    """Per-iteration HBM bytes of a stage from the committed rocprofv3 PMC summary, if present:
-    the sum over the stage's kernels (each launched once per iteration) of their bytes per launch."""
+KERNEL_SOURCES = ("mc-path-tracer_amd/csrc/kernels.hip", "mc-path-tracer_amd/csrc/kernels.hpp",
+                  "mc-path-tracer_amd/csrc/device/mcpt_core.hpp", "mc-path-tracer_amd/csrc/runtime.cpp",
+                  "mc-path-tracer_amd/csrc/host/scene.cpp", "mc-path-tracer_amd/csrc/host/proxies.cpp")
+
+
+def source_hash():
+    """Hash of the kernel and scene sources: stamps the PMC summaries (tools/pmc.py) so that a
+    summary taken on other code is recognised as stale (the GPU box has no .git)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(REPO, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_summary(config, slots):
+    """The newest committed rocprofv3 PMC summary (profiles/pmc_*.json) and whether it was
+    measured on this code (source hash) and this workload (config, path slots)."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json")))
     if not files:
-        return None
+        return None, "no PMC summary in profiles/"
     try:
         d = json.load(open(files[-1]))
-        got = [v.get("hbm_bytes_per_launch") for k, v in d.get("kernels", {}).items()
-               if any(k.startswith(p) or k.startswith("void " + p) for p in kernel_prefix)]
-        return int(sum(got)) if got and None not in got else None
-    except Exception:
+    except Exception as e:  # noqa: BLE001
+        return None, f"unreadable PMC summary: {e}"
+    stamp = d.get("stamp", {})
+    why = []
+    if stamp.get("source_hash") != source_hash():
+        why.append("kernel sources changed since it was taken")
+    if stamp.get("config") != config or stamp.get("slots") != slots:
+        why.append(f"taken on config {stamp.get('config')} / {stamp.get('slots')} slots")
+    return d, ("; ".join(why) or None)
+
+
+def pmc_traffic(summary, kernel_prefix):
+    """Per-iteration HBM bytes of a stage from a PMC summary: the sum over the stage's kernels
+    (each launched once per iteration) of their bytes per launch."""
+    if not summary:
         return None
+    got = [v.get("hbm_bytes_per_launch") for k, v in summary.get("kernels", {}).items()
+           if any(k.startswith(p) or k.startswith("void " + p) for p in kernel_prefix)]
+    return int(sum(got)) if got and None not in got else None
 
 
 def cpu_baseline(scene_arrays, cam, W, H, spp, max_depth):
@@ -196,38 +228,57 @@ def main():
     per_launch = byts / K
     avg_ms = kern[dom] / K
     achieved = per_launch / (avg_ms * 1e-3)
-    traffic = pmc_traffic(names[dom])
+    # measured HBM bytes per launch from the committed PMC summary, used only when it was taken
+    # on this code and workload (tools/pmc.py stamps it)
+    summary, stale = pmc_summary(args.config, args.slots)
+    fresh = summary if stale is None else None
+    traffic = pmc_traffic(fresh, names[dom])
+    frac = achieved / HBM_PEAK
     roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
+            "frac": round(frac, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
             "algorithmic_bytes_per_launch": int(per_launch),
-            "note": "logical bytes (SURVEY 8d) count every BVH node/triangle fetch; those are served from L2/MALL, "
-                    "so frac can exceed HBM reality - traffic is the measured HBM bytes per launch; the traversal "
-                    "is bound by its divergent issue/latency mix (VALU ~70%, TD ~78%, TA ~64% busy: DESIGN.md)",
             "state_only_frac": round(state / K / (avg_ms * 1e-3) / HBM_PEAK, 4),
             "per_ray": {"ext_pair_nodes": round(st.ext_nodes / max(1, st.extend_rays), 2),
                         "ext_tri_tests": round(st.ext_tests / max(1, st.extend_rays), 2),
                         "any_pair_nodes": round(st.any_nodes / max(1, st.shadow_rays + st.vis_rays), 2),
                         "any_tri_tests": round(st.any_tests / max(1, st.shadow_rays + st.vis_rays), 2)}}
+    # What binds, from the numbers: SURVEY 8(d)'s logical bytes count every BVH node and triangle
+    # fetch; above the HBM peak they can only have come from the caches (L2 / MALL)
+    binding = []
+    if frac > 1.0:
+        binding.append(f"not HBM: the logical bytes run at {frac:.2f}x the HBM peak, so the node and triangle "
+                       f"fetches are cache-served ({achieved / L2_PEAK:.2f} of the 34.5 TB/s aggregate L2 rate)")
+        roof["l2_frac"] = round(achieved / L2_PEAK, 4)
+    if traffic is not None:
+        tf = traffic / (avg_ms * 1e-3) / HBM_PEAK
+        roof["traffic_GBps"] = round(traffic / (avg_ms * 1e-3) / 1e9, 1)
+        roof["traffic_frac"] = round(tf, 4)
+        binding.append(f"measured HBM traffic {tf:.2f} of peak")
+        if tf > 0.6:
+            binding.append("HBM-bound by measured traffic")
+    elif stale:
+        roof["pmc_stale"] = stale
+    if frac > 1.0 and (traffic is None or traffic / (avg_ms * 1e-3) / HBM_PEAK < 0.6):
+        binding.append("the traversal is bound by its divergent issue / gather-latency mix (DESIGN.md section 4)")
+    roof["binding"] = "; ".join(binding) if binding else "hbm"
     # the streaming stages (logic + generate + material: k_shade and k_material) on their own,
-    # by SURVEY 8(d) state bytes and by the committed PMC traffic
+    # by SURVEY 8(d) state bytes and by the PMC traffic
     t_shd = st.ms_shade / K * 1e-3
     roof["shade_stages"] = {"ms_per_iteration": round(st.ms_shade / K, 4),
                             "state_bytes_per_iteration": int(b_shd / K),
                             "state_frac": round(b_shd / K / t_shd / HBM_PEAK, 4)}
-    shd_traffic = pmc_traffic(names["k_shade"])
+    shd_traffic = pmc_traffic(fresh, names["k_shade"])
     if shd_traffic is not None:
         roof["shade_stages"]["traffic"] = shd_traffic
         roof["shade_stages"]["traffic_frac"] = round(shd_traffic / t_shd / HBM_PEAK, 4)
     # measured HBM ceiling on this device (hand-written dwordx4 copy) beside the spec peak
     copy = pt.hbm_copy_gbps(1 << 30, 20)
     roof["measured_copy_GBps"] = round(copy, 1)
-    if traffic is not None:
-        roof["traffic_GBps"] = round(traffic / (avg_ms * 1e-3) / 1e9, 1)
     # whole-pipeline form: all logical bytes of both kernels over their summed time
     t_pipe = (st.ms_extend + st.ms_shadow + st.ms_shade) * 1e-3
     roof["pipeline_frac"] = round((b_ext + b_any + b_shd) / t_pipe / HBM_PEAK, 4)
-    hbm_meas = [pmc_traffic(p) for p in names.values()]
-    if all(h is not None for h in hbm_meas):  # measured HBM bytes per iteration (committed PMC summary)
+    hbm_meas = [pmc_traffic(fresh, p) for p in names.values()]
+    if all(h is not None for h in hbm_meas):  # measured HBM bytes per iteration (fresh PMC summary)
         roof["pipeline_hbm_frac_measured"] = round(sum(hbm_meas) * K / t_pipe / HBM_PEAK, 4)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

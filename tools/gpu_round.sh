@@ -18,7 +18,7 @@ if [[ $STEP == all || $STEP == prof ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_kt -o kt --output-format csv -- python3 bench.py --no-cpu-baseline --no-full-frame --steps 60 --warmup 30 > $OUT/prof_kt.log 2>&1 || { echo "rocprof kt failed"; tail -30 $OUT/prof_kt.log; exit 1; }
   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/prof_fetch -o fetch --output-format csv -- python3 bench.py --no-cpu-baseline --no-full-frame --steps 20 --warmup 10 > $OUT/prof_fetch.log 2>&1 || { echo "rocprof fetch failed"; tail -30 $OUT/prof_fetch.log; exit 1; }
   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/prof_write -o write --output-format csv -- python3 bench.py --no-cpu-baseline --no-full-frame --steps 20 --warmup 10 > $OUT/prof_write.log 2>&1 || { echo "rocprof write failed"; tail -30 $OUT/prof_write.log; exit 1; }
-  python tools/pmc.py r01 $OUT > /dev/null  # box-local profiles/ so the bench below reads this run's traffic
+  python tools/pmc.py ${TAG:-r02} $OUT > /dev/null  # box-local profiles/ so the bench below reads this run's traffic
 fi
 if [[ $STEP == all || $STEP == prof || $STEP == bench2 ]]; then
   timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }

@@ -47,7 +47,15 @@ dur = {}
 if stats:
     for r in csv.DictReader(open(stats)):
         dur[r["Name"]] = float(r["AverageNs"])
-out = {"round": tag, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on "
+sys.path.insert(0, REPO)
+import bench  # noqa: E402  (source_hash only)
+
+# The profiled commands run bench.py's defaults (config 2, 3 path slots) unless PMC_CONFIG /
+# PMC_SLOTS say otherwise; bench.py uses the traffic only when this stamp matches its run.
+stamp = {"source_hash": bench.source_hash(), "config": int(os.environ.get("PMC_CONFIG", "2")),
+         "slots": int(os.environ.get("PMC_SLOTS", "3"))}
+out = {"round": tag, "stamp": stamp,
+       "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on "
        "'python3 bench.py --no-cpu-baseline --steps 20 --warmup 10'; durations from --kernel-trace --stats",
        "correction": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE reads half of 16 B/lane streams)",
        "kernels": {}}
