@@ -777,6 +777,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     uint64_t prof[12] = {};  // see mcpt_debug_trace_profile
 #endif
     uint64_t drained = 0;  // partitions this wave saw run dry (by an atomic: never stale)
+#ifdef MCPT_X_PREFETCH
+    uint32_t pfx = 0;
+#endif
     for (;;) {  // one trip per partition joined
     // Per-lane ray state is declared per partition trip: when the trip ends no lane holds a
     // ray, so none of it is live across the partition scan below (VGPR budget).
@@ -979,6 +982,14 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
               } else {
                 const float4* nd = sc.nodes + 4 * ref;
                 const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+#ifdef MCPT_X_PREFETCH  // experiment: touch both children (node line or triangle record) before the slab
+                {
+                    const int p0 = __float_as_int(q3.x), p1 = __float_as_int(q3.y);
+                    const uint32_t* w0 = p0 >= 0 ? (const uint32_t*)(sc.nodes + 4 * p0) : (const uint32_t*)(sc.tri + 3 * (p0 & 0xffffff));
+                    const uint32_t* w1 = p1 >= 0 ? (const uint32_t*)(sc.nodes + 4 * p1) : (const uint32_t*)(sc.tri + 3 * (p1 & 0xffffff));
+                    pfx ^= w0[0] ^ w1[0];
+                }
+#endif
 #ifdef MCPT_X_EXTRA_FETCH  // experiment: +50% node bytes (the neighbouring node's first half)
                 {
                     const float4* xn = sc.nodes + 4 * (ref > 0 ? ref - 1 : ref);
@@ -1112,6 +1123,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #ifdef MCPT_TRACE_PROF
     if (lane == 0)
         for (int i = 0; i < 12; i++) atomicAdd(&g_trace_prof[i], (unsigned long long)prof[i]);
+#endif
+#ifdef MCPT_X_PREFETCH
+    if (a.refill_min == 1000u && pfx == 0x9e3779b9u) a.hit_tri[0] = 0;  // keeps the touches (never true)
 #endif
     wave_stats(a.set[0].stats, lane, tot_n0, tot_t0, tot_h0);
     wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);
