@@ -141,11 +141,17 @@ int mcpt_create(int device, const mcpt_config *cfg, mcpt_ctx **out);
 void mcpt_destroy(mcpt_ctx *ctx);
 const char *mcpt_last_error(const mcpt_ctx *ctx);   /* ctx may be NULL: last global error */
 int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_scene_desc *desc);
-/* Same scene with the BVH built on the GPU (linear BVH: Morton codes + Karras radix tree,
- * one triangle per leaf) instead of taken from desc (its BVH arrays are
- * ignored and may be empty).  Hits and films are identical to mcpt_scene_upload's: the
- * traversal's result does not depend on the tree. */
+/* Same scene with the BVH built on the GPU instead of taken from desc (its
+ * BVH arrays are ignored and may be empty); one triangle per leaf.  Hits and films are
+ * identical to mcpt_scene_upload's: the traversal's result does not depend on the tree.
+ * Builders (mcpt_set_gpu_bvh_builder):
+ *   MCPT_GPU_BVH_PLOC (default): parallel locally-ordered clustering over Morton-sorted
+ *     triangles -- surface-area agglomeration, quality close to a full SAH build;
+ *   MCPT_GPU_BVH_LBVH: Karras' linear BVH (Morton-code splits; fastest build, slower trees). */
+#define MCPT_GPU_BVH_LBVH 0
+#define MCPT_GPU_BVH_PLOC 1
 int mcpt_scene_upload_gpu_bvh(mcpt_ctx *ctx, const mcpt_scene_desc *desc);
+int mcpt_set_gpu_bvh_builder(mcpt_ctx *ctx, int32_t builder);
 int mcpt_camera_set(mcpt_ctx *ctx, const mcpt_camera *cam);
 int mcpt_film_resize(mcpt_ctx *ctx, uint32_t w, uint32_t h, uint32_t tile_w, uint32_t tile_h);
 int mcpt_film_clear(mcpt_ctx *ctx);                                          /* == clear_dfilm */

@@ -155,10 +155,11 @@ void launch_clear(const ClearArgs& a, hipStream_t s);
 struct LbvhInput { int ntri; const float *v0, *v1, *v2; const float4 *d_tri, *d_sh; };
 struct LbvhOutput {
     float4 *nodes = nullptr, *tri = nullptr, *tri_sh = nullptr;  // hipMalloc'ed, owned by the caller
-    int nnodes = 0, root_ref = 0, depth = 0;
+    int nnodes = 0, root_ref = 0, depth = 0, rounds = 0;
     float root_mn[3], root_mx[3];
 };
 int build_lbvh(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
+int build_ploc(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
 int trace_profile(unsigned long long* out, int reset);
 int wave_times(unsigned long long* out, int n);
 void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStream_t s);

@@ -70,6 +70,7 @@ struct mcpt_ctx {
     std::vector<void*> tmp_bufs;
     float last_stage_ms = 0.f;
     float last_build_ms = 0.f;  // last GPU BVH build (mcpt_scene_upload_gpu_bvh)
+    int gpu_bvh_builder = MCPT_GPU_BVH_PLOC;  // mcpt_set_gpu_bvh_builder
 };
 
 static int set_err(mcpt_ctx* c, int rc, const std::string& msg) {
@@ -428,7 +429,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     if (gpu_bvh && d->ntri > 0) {
         HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
         LbvhInput li{d->ntri, d->v0, d->v1, d->v2, dt, dsh};
-        const int brc = build_lbvh(li, lb, c->stream);
+        const int brc = c->gpu_bvh_builder == MCPT_GPU_BVH_LBVH ? build_lbvh(li, lb, c->stream) : build_ploc(li, lb, c->stream);
         for (void* q : {(void*)lb.nodes, (void*)lb.tri, (void*)lb.tri_sh})
             if (q) c->scene_bufs.push_back(q);
         if (brc) return set_err(c, MCPT_E_HIP, "GPU BVH build failed (" + std::to_string(brc) + ")");
@@ -530,6 +531,12 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
 
 int mcpt_scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d) { return scene_upload(c, d, false); }
 int mcpt_scene_upload_gpu_bvh(mcpt_ctx* c, const mcpt_scene_desc* d) { return scene_upload(c, d, true); }
+int mcpt_set_gpu_bvh_builder(mcpt_ctx* c, int32_t builder) {
+    if (!c || (builder != MCPT_GPU_BVH_LBVH && builder != MCPT_GPU_BVH_PLOC))
+        return set_err(c, MCPT_E_INVALID, "unknown GPU BVH builder");
+    c->gpu_bvh_builder = builder;
+    return MCPT_OK;
+}
 float mcpt_debug_last_build_ms(const mcpt_ctx* c) { return c ? c->last_build_ms : -1.f; }
 int mcpt_debug_node_layout(const mcpt_ctx* c) { return c ? c->node_layout : MCPT_E_INVALID; }
 

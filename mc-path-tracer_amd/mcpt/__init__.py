@@ -106,6 +106,7 @@ ABI = {
     "mcpt_debug_last_build_ms": (C.c_float, [C.c_void_p]),
     "mcpt_debug_node_layout": (C.c_int, [C.c_void_p]),
     "mcpt_scene_upload_gpu_bvh": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mcpt_set_gpu_bvh_builder": (C.c_int, [C.c_void_p, C.c_int32]),
     "mcpt_film_size": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "mcpt_film_write_png": (C.c_int, [C.c_void_p, C.c_float, C.c_char_p]),
     "mcpt_film_write_pfm": (C.c_int, [C.c_void_p, C.c_char_p]),
@@ -355,11 +356,15 @@ class PathTracer:
         return buf.value.decode()
 
     def upload_scene(self, scene, gpu_bvh=False):
-        """mcpt_scene_upload (host BVH from the scene), or with gpu_bvh=True
-        mcpt_scene_upload_gpu_bvh (linear BVH built on the device; same hits)."""
+        """mcpt_scene_upload (host BVH from the scene), or with gpu_bvh=True / "ploc" / "lbvh"
+        mcpt_scene_upload_gpu_bvh (BVH built on the device, PLOC by default; same hits)."""
         d = scene.desc() if isinstance(scene, Scene) else scene
-        fn = lib().mcpt_scene_upload_gpu_bvh if gpu_bvh else lib().mcpt_scene_upload
-        self._ck(fn(self.h, C.byref(d)))
+        if gpu_bvh:
+            if gpu_bvh in ("ploc", "lbvh"):
+                self._ck(lib().mcpt_set_gpu_bvh_builder(self.h, 1 if gpu_bvh == "ploc" else 0))
+            self._ck(lib().mcpt_scene_upload_gpu_bvh(self.h, C.byref(d)))
+        else:
+            self._ck(lib().mcpt_scene_upload(self.h, C.byref(d)))
 
     @property
     def last_build_ms(self) -> float:

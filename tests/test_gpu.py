@@ -420,13 +420,14 @@ def test_fixed_mode_delta_light_parity(mcpt_mod, oracle):
         pt.close()
 
 
+@pytest.mark.parametrize("builder", ["ploc", "lbvh"])
 @pytest.mark.parametrize("which", ["scene_c1", "scene_c2", "scene_cube", "scene_c3"])
-def test_gpu_bvh_same_hits(request, mcpt_mod, oracle, which):
-    """GPU-built linear BVH (mcpt_scene_upload_gpu_bvh): hits bit-identical to the oracle, which
-    traverses the host SAH tree -- the traversal's result does not depend on the tree."""
+def test_gpu_bvh_same_hits(request, mcpt_mod, oracle, which, builder):
+    """GPU-built BVHs (mcpt_scene_upload_gpu_bvh, PLOC and linear BVH): hits bit-identical to the
+    oracle, which traverses the host SAH tree -- the traversal's result does not depend on the tree."""
     s, a = request.getfixturevalue(which)
     pt = mcpt_mod.PathTracer(0)
-    pt.upload_scene(s, gpu_bvh=True)
+    pt.upload_scene(s, gpu_bvh=builder)
     assert pt.last_build_ms > 0
     n = 20000 if which == "scene_c3" else 100000
     ro, rd = random_rays(n, 31, box=2.5)
@@ -443,12 +444,13 @@ def test_gpu_bvh_same_hits(request, mcpt_mod, oracle, which):
     pt.close()
 
 
-def test_gpu_bvh_film_parity(mcpt_mod, oracle, scene_c2):
+@pytest.mark.parametrize("builder", ["ploc", "lbvh"])
+def test_gpu_bvh_film_parity(mcpt_mod, oracle, scene_c2, builder):
     rc = mcpt_mod.CONFIGS[2]
     W, H = 160, 90
     cam = mcpt_mod.config_camera(rc, W, H)
     pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=3, max_depth=rc.max_depth))
-    pt.upload_scene(scene_c2[0], gpu_bvh=True)
+    pt.upload_scene(scene_c2[0], gpu_bvh=builder)
     pt.set_camera(cam)
     pt.resize(W, H)
     pt.render()
@@ -674,3 +676,25 @@ def test_path_slots_rejected_count_keeps_film(mcpt_mod, scene_c1):
     _, s2 = pt.film()
     assert s2.sum() == 0  # accepted change: film cleared
     pt.close()
+
+
+def test_ploc_small_and_degenerate_inputs(mcpt_mod, oracle):
+    """PLOC on 1, 2, 3 and 37 triangles, and on many coincident (identical) triangles: equal
+    union areas everywhere, so only the index tie-break orders the pairs; hits match the oracle."""
+    rng = np.random.default_rng(5)
+    for ntri, same in ((1, False), (2, False), (3, False), (37, False), (300, True)):
+        v = rng.uniform(-1, 1, (ntri, 3, 3)).astype(np.float32)
+        if same:
+            v[:] = v[0]
+        s = mcpt_mod.Scene()
+        nrm = np.tile(np.float32([0, 0, 1]), (ntri, 1))
+        s.add_mesh(v[:, 0], v[:, 1], v[:, 2], nrm, nrm, nrm, (0.5, 0.5, 0.5))
+        s.set_env_color((1, 1, 1), 1.0)
+        s.build(8)
+        a = s.arrays()
+        pt = mcpt_mod.PathTracer(0)
+        pt.upload_scene(s, gpu_bvh="ploc")
+        ro, rd = random_rays(20000, ntri, box=2.0)
+        assert np.array_equal(pt.trace_closest(ro, rd)[2], oracle.trace_closest(a, ro, rd)[2])
+        assert np.array_equal(pt.trace_any(ro, rd), oracle.trace_any(a, ro, rd))
+        pt.close()
