@@ -358,6 +358,13 @@ struct EnvView {
     // entries (tables up to 65535 wide/high): 256 x 1025 x 2 B = 512 KiB for a 512x256 map.
     const uint16_t* guide_m;
     const uint16_t* guide_c;
+    // Optional light-sample tables (device only, HRDI mode, built at upload by
+    // k_env_table from these same functions): in either mode env_dir's result is a
+    // function of the sampled cell (x, y) alone, and so are env_L and env_pdf at that
+    // direction.  Entry (y * (w + 1) + x + 1) = {dir.xyz, pdf}, {L.xyz, 0} for
+    // x = -1 .. w-1 (the reference's off-by-one column -1 included); [0] reference
+    // mode, [1] quality mode.
+    const float4* ltab[2];
 };
 // Bins per guide table.  Each bin is equally likely (val uniform), and a bin holds W / G
 // CDF entries on average, so G = 1024 leaves ~0.5 (conditional rows, W = 512) and
@@ -468,16 +475,12 @@ MCPT_HD void env_L_pdf(const EnvView& e, V3 wi, V3& L, float& pdf) {
     L = tex_bilinear(e.tex, e.w, e.h, u, v);
     pdf = env_pdf_uv<FIXED>(e, u, v);
 }
+// HRDI sampling, EnvironmentLight.cu:20-29: the cell (x, y) drawn from the marginal and
+// conditional CDFs (x can be -1 in reference mode; y < 0 is unreachable).
 template <bool FIXED = false>
-MCPT_HD V3 env_dir(const EnvView& e, const Rng& r) {  // EnvironmentLight.cu:10-33
-    if (e.mode == 0 || e.tex == nullptr) {
-        float u = r(SL_ENV_U);
-        float v = r(SL_ENV_V);
-        return spherical_direction(u, v);
-    }
+MCPT_HD void env_cell(const EnvView& e, const Rng& r, int& x, int& y) {
     float ex = r(SL_ENV_U);
     float ey = r(SL_ENV_V);
-    int y, x;
     if (e.guide_m) {
         y = (int)((float)upper_bound_guided(e.marginal_y, e.guide_m, ey) - 1.f);
         if (y < 0) y = 0;  // unreachable (marginal_y[0] == 0); reference reads row -1
@@ -490,11 +493,26 @@ MCPT_HD V3 env_dir(const EnvView& e, const Rng& r) {  // EnvironmentLight.cu:10-
     if (FIXED) {
         y = y > e.h - 1 ? e.h - 1 : y;
         x = x < 0 ? 0 : (x > e.w - 1 ? e.w - 1 : x);
-        return spherical_direction(((float)x + 0.5f) / (float)e.w, ((float)y + 0.5f) / (float)e.h);
     }
+}
+// the direction of a sampled cell (EnvironmentLight.cu:28-31: pixel corner u = x / W)
+template <bool FIXED = false>
+MCPT_HD V3 env_cell_dir(const EnvView& e, int x, int y) {
+    if (FIXED) return spherical_direction(((float)x + 0.5f) / (float)e.w, ((float)y + 0.5f) / (float)e.h);
     float u = (float)x / (float)e.w;
     float v = (float)y / (float)e.h;
     return spherical_direction(u, v);
+}
+template <bool FIXED = false>
+MCPT_HD V3 env_dir(const EnvView& e, const Rng& r) {  // EnvironmentLight.cu:10-33
+    if (e.mode == 0 || e.tex == nullptr) {
+        float u = r(SL_ENV_U);
+        float v = r(SL_ENV_V);
+        return spherical_direction(u, v);
+    }
+    int x, y;
+    env_cell<FIXED>(e, r, x, y);
+    return env_cell_dir<FIXED>(e, x, y);
 }
 
 // ---------------------------------------------------------------------------

@@ -292,15 +292,28 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
     const bool delta = light_id > 0;
     const float sel = FIXED ? 1.f / (float)sc.nlights : 1.f;  // light-selection pdf
     {
-        V3 ldir;
-        if (light_id == 0) ldir = env_dir<FIXED>(sc.env, r);
-        else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
+        V3 ldir, Li_l;
+        float pdfl_x;
+        const float4* lt = sc.env.ltab[FIXED ? 1 : 0];
+        if (light_id == 0 && lt) {
+            // HRDI env sample: direction, radiance and pdf are functions of the sampled cell
+            // alone, tabulated at upload by the same code (k_env_table): one 32-B fetch instead
+            // of the spherical direction, map, bilinear fetch and pdf of every sample
+            int cx, cy;
+            env_cell<FIXED>(sc.env, r, cx, cy);
+            const float4* t = lt + 2 * ((int64_t)cy * (sc.env.w + 1) + cx + 1);
+            const float4 t0 = t[0], t1 = t[1];
+            ldir = xyz(t0);
+            pdfl_x = t0.w;
+            Li_l = xyz(t1);
+        } else {
+            if (light_id == 0) ldir = env_dir<FIXED>(sc.env, r);
+            else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
+            light_L_pdf<FIXED>(sc, light_id, ldir, Li_l, pdfl_x);
+        }
         V3 f_l;
         float pdf_bl;
         brdf_f_pdf(m, n, ldir, wo, f_l, pdf_bl);
-        V3 Li_l;
-        float pdfl_x;
-        light_L_pdf<FIXED>(sc, light_id, ldir, Li_l, pdfl_x);
         if (FIXED) pdfl_x = pdfl_x * sel;
         float pdfb_y = !delta ? pdf_bl : (FIXED ? 0.f : 1.f);
         float wL = power_heuristic(pdfl_x, pdfb_y);
@@ -1135,6 +1148,28 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         g_wave_t[4 * blockIdx.x + 2] = part;
     }
 #endif
+}
+
+// Light-sample table of an HRDI env light (EnvView::ltab): entry (y, x + 1) holds the
+// direction env_dir returns for cell (x, y), and env_L / env_pdf at that direction --
+// computed by the very functions the per-sample path calls, so the values are the same.
+template <bool FIXED>
+__global__ void k_env_table(EnvView e, float4* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int W1 = e.w + 1;
+    if (i >= W1 * e.h) return;
+    const int y = i / W1, x = i - y * W1 - 1;
+    const V3 d = env_cell_dir<FIXED>(e, FIXED && x < 0 ? 0 : x, y);
+    V3 L;
+    float pdf;
+    env_L_pdf<FIXED>(e, d, L, pdf);
+    out[2 * i] = make_float4(d.x, d.y, d.z, pdf);
+    out[2 * i + 1] = make_float4(L.x, L.y, L.z, 0.f);
+}
+void launch_env_table(const EnvView& e, bool fixed_mode, float4* out, hipStream_t s) {
+    const int n = (e.w + 1) * e.h;
+    if (fixed_mode) hipLaunchKernelGGL(k_env_table<true>, dim3((n + 255) / 256), dim3(256), 0, s, e, out);
+    else hipLaunchKernelGGL(k_env_table<false>, dim3((n + 255) / 256), dim3(256), 0, s, e, out);
 }
 
 __global__ void k_hit_record(HitRecordArgs a) {  // stage_run(EXTEND) outputs

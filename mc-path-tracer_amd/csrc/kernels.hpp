@@ -149,6 +149,7 @@ int launch_geometry(int device, LaunchGeom& g);  // device must be current
 void launch_shade(const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fixed_mode, hipStream_t s);
 void launch_trace(const TraceArgs& a, const LaunchGeom& g, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
+void launch_env_table(const mcpt::EnvView& e, bool fixed_mode, float4* out, hipStream_t s);
 
 // GPU linear BVH (bvh_build.hip).  Inputs: host vertex arrays (3 floats per
 // triangle each) and the device triangle / shading records in scene order.

@@ -487,6 +487,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     s.env.h = d->env_h;
     s.env.tex = nullptr;
     s.env.guide_m = s.env.guide_c = nullptr;
+    s.env.ltab[0] = s.env.ltab[1] = nullptr;
     if (d->env_mode == 1) {
         float4* tx;
         float *my, *cy, *pd;
@@ -521,6 +522,18 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             if ((rc = dupload(c, c->scene_bufs, &dgc, gc.data(), gc.size()))) return rc;
             s.env.guide_m = dgm;
             s.env.guide_c = dgc;
+        }
+        // light-sample tables, reference and quality mode (k_env_table)
+        if ((size_t)(d->env_w + 1) * d->env_h < ((size_t)1 << 28)) {
+            const size_t ne = 2 * (size_t)(d->env_w + 1) * d->env_h;
+            float4 *lt0, *lt1;
+            if ((rc = dalloc(c, c->scene_bufs, &lt0, ne)) || (rc = dalloc(c, c->scene_bufs, &lt1, ne))) return rc;
+            launch_env_table(s.env, false, lt0, c->stream);
+            launch_env_table(s.env, true, lt1, c->stream);
+            HIPCHK(c, hipGetLastError());
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            s.env.ltab[0] = lt0;
+            s.env.ltab[1] = lt1;
         }
     }
     c->scene = s;
