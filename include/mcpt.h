@@ -178,6 +178,12 @@ int mcpt_film_read_device(mcpt_ctx *ctx, void *d_Ld_rgb, void *d_samples);  /* d
 int mcpt_film_pack_tiles(mcpt_ctx *ctx, void *d_out, uint32_t *npix);       /* tile-set pixels -> packed 16 B/px (rgb f32, samples u32) */
 int mcpt_film_tonemap_rgba8(mcpt_ctx *ctx, float exposure, uint8_t *out);   /* == draw_to_surface */
 int mcpt_film_size(const mcpt_ctx *ctx, uint32_t *w, uint32_t *h);
+/* Frame-end gather of a multi-GPU render in one process: the tile-set pixels of
+ * every context (one per GPU, same film and tile size, tile sets disjoint from the root's) are
+ * copied device-to-device over xGMI into ctxs[root]'s film, whose readers then return the whole
+ * frame.  Processes with one GPU each use one RCCL all_gather of mcpt_film_pack_tiles buffers
+ * instead (mcpt/parallel.py).  Synchronous. */
+int mcpt_gather(mcpt_ctx *const *ctxs, int32_t n, int32_t root);
 /* Film output (replaces stbi_write_png of the display buffer, RenderingContext.cpp:114-118):
  * PNG = tonemapped 8-bit RGB, row 0 = top; PFM = float RGB radiance Ld/samples (0 where no sample). */
 int mcpt_film_write_png(mcpt_ctx *ctx, float exposure, const char *path);

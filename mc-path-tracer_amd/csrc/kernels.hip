@@ -1290,6 +1290,20 @@ __global__ void k_pack(PackArgs a) {  // tile-set pixels -> packed 16 B/px (for 
     a.out[i] = o;
 }
 
+__global__ void k_unpack(UnpackArgs a) {  // packed 16 B/px of a tile set -> film accumulators (mcpt_gather)
+    const int tile_px = a.tile_w * a.tile_h;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint32_t)(a.ntiles * tile_px)) return;
+    const int tile = i / tile_px, li = i % tile_px;
+    const int2 t = a.tiles[tile];
+    const int x = t.x * a.tile_w + li % a.tile_w, y = t.y * a.tile_h + li / a.tile_w;
+    if (x >= a.W || y >= a.H) return;
+    const uint32_t pid = (uint32_t)y * a.W + x;
+    const float4 v = a.in[i];
+    a.Ld[pid] = make_float4(v.x, v.y, v.z, 0.f);
+    a.samples[pid] = __float_as_uint(v.w);
+}
+
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
@@ -1425,6 +1439,10 @@ void launch_tonemap(const TonemapArgs& a, hipStream_t s) {
 }
 void launch_accumulate(CounterBlock* c, uint32_t nparts, hipStream_t s) {
     hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(kShards), 0, s, c, std::min<uint32_t>(kMaxParts, std::max<uint32_t>(1, nparts)));
+}
+void launch_unpack(const UnpackArgs& a, hipStream_t s) {
+    const uint32_t n = (uint32_t)(a.ntiles * a.tile_w * a.tile_h);
+    if (n) hipLaunchKernelGGL(k_unpack, dim3((n + 255) / 256), dim3(256), 0, s, a);
 }
 void launch_pack(const PackArgs& a, hipStream_t s) {
     uint32_t n = (uint32_t)(a.ntiles * a.tile_w * a.tile_h);

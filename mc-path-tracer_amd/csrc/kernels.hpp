@@ -135,6 +135,7 @@ struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n; }
 struct ResolveArgs { const float4* Ld; const uint32_t* samples; float4* out_Ld; uint32_t* out_samples; uint32_t n; int slots; };
 struct TonemapArgs { const float4* Ld; const uint32_t* samples; uchar4* out; float exposure; uint32_t n; };
 struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* out; };
+struct UnpackArgs { const float4* in; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* Ld; uint32_t* samples; };
 
 // Launch geometry of one device (mcpt_create): persistent grids from the occupancy
 // calculator and the device's XCD count, with environment overrides for sweeps.
@@ -170,5 +171,6 @@ void launch_tonemap(const TonemapArgs& a, hipStream_t s);
 void launch_resolve(const ResolveArgs& a, hipStream_t s);
 void launch_accumulate(CounterBlock* c, uint32_t nparts, hipStream_t s);
 void launch_pack(const PackArgs& a, hipStream_t s);
+void launch_unpack(const UnpackArgs& a, hipStream_t s);
 
 }  // namespace mcpt_dev

@@ -1012,6 +1012,75 @@ int mcpt_film_pack_tiles(mcpt_ctx* c, void* d_out, uint32_t* npix) {
     return MCPT_OK;
 }
 
+// Frame-end gather of a multi-GPU render inside one process (SURVEY.md 8(b) mcpt_gather, 8(e)):
+// every context's tile-set pixels, resolved over its path slots and packed 16 B/px, are copied
+// device-to-device onto the root's device (hipMemcpyPeerAsync: SDMA over xGMI between MI355X
+// dies of a node) and scattered into the root's film accumulators, so the root's film readers
+// return the whole frame.  Tile sets must not overlap the root's own tiles (the interleaved
+// partition of mcpt/parallel.py); the multi-process form is one RCCL all_gather of the same
+// packed buffers (mcpt/parallel.py).
+int mcpt_gather(mcpt_ctx* const* ctxs, int32_t n, int32_t root) {
+    if (!ctxs || n < 1 || root < 0 || root >= n || !ctxs[root]) return set_err(nullptr, MCPT_E_INVALID, "bad gather arguments");
+    mcpt_ctx* R = ctxs[root];
+    for (int32_t i = 0; i < n; i++) {
+        mcpt_ctx* c = ctxs[i];
+        if (!c || !c->P) return set_err(R, MCPT_E_INVALID, "gather: a context has no film");
+        if (c->W != R->W || c->H != R->H || c->tile_w != R->tile_w || c->tile_h != R->tile_h)
+            return set_err(R, MCPT_E_INVALID, "gather: film or tile sizes differ between contexts");
+        for (int32_t j = 0; j < i; j++)
+            if (ctxs[j] == c) return set_err(R, MCPT_E_INVALID, "gather: a context is listed twice");
+    }
+    for (int32_t i = 0; i < n; i++) {
+        mcpt_ctx* c = ctxs[i];
+        if (c == R || c->tiles_h.empty()) continue;
+        const size_t npix = c->tiles_h.size() * (size_t)c->tile_w * c->tile_h;
+        // pack on the source device (its film view resolves the path slots)
+        HIPCHK(R, hipSetDevice(c->device));
+        const float4* fL;
+        const uint32_t* fs;
+        int rc = film_view(c, &fL, &fs);
+        if (rc) return set_err(R, rc, c->err);
+        float4* src = nullptr;
+        if (hipMalloc(&src, npix * sizeof(float4)) != hipSuccess) return set_err(R, MCPT_E_NOMEM, "gather: pack buffer");
+        PackArgs pa{fL, fs, c->tiles, (int)c->tiles_h.size(), (int)c->tile_w, (int)c->tile_h, (int)c->W, (int)c->H, src};
+        launch_pack(pa, c->stream);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        // copy to the root's device and scatter into its accumulators (slot 0; the other slots
+        // of pixels the root does not render are zero, so its slot sum returns these values)
+        float4* dst = nullptr;
+        int2* dt = nullptr;
+        if (e == hipSuccess) e = hipSetDevice(R->device);
+        if (e == hipSuccess && c->device != R->device) {
+            // direct xGMI access where the pair supports it; hipMemcpyPeerAsync also works
+            // without it (staged), so a refusal here is not an error
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, R->device, c->device) == hipSuccess && can)
+                (void)hipDeviceEnablePeerAccess(c->device, 0);
+            (void)hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMalloc(&dst, npix * sizeof(float4));
+        if (e == hipSuccess) e = hipMalloc(&dt, c->tiles_h.size() * sizeof(int2));
+        if (e == hipSuccess)
+            e = hipMemcpyPeerAsync(dst, R->device, src, c->device, npix * sizeof(float4), R->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(dt, c->tiles_h.data(), c->tiles_h.size() * sizeof(int2), hipMemcpyHostToDevice, R->stream);
+        if (e == hipSuccess) {
+            UnpackArgs ua{dst, dt, (int)c->tiles_h.size(), (int)R->tile_w, (int)R->tile_h, (int)R->W, (int)R->H, R->p.Ld, R->p.samples};
+            launch_unpack(ua, R->stream);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(R->stream);
+        (void)hipFree(dst);
+        (void)hipFree(dt);
+        (void)hipSetDevice(c->device);
+        (void)hipFree(src);
+        if (e != hipSuccess) return set_err(R, MCPT_E_HIP, std::string("gather: ") + hipGetErrorString(e));
+    }
+    (void)hipSetDevice(R->device);
+    return MCPT_OK;
+}
+
 int mcpt_film_size(const mcpt_ctx* c, uint32_t* w, uint32_t* h) {
     if (!c || !w || !h) return MCPT_E_INVALID;
     if (!c->P) return set_err(const_cast<mcpt_ctx*>(c), MCPT_E_INVALID, "film not allocated");

@@ -91,6 +91,7 @@ ABI = {
     "mcpt_set_tiles": (C.c_int, [C.c_void_p, _u, C.c_uint32]),
     "mcpt_set_path_slots": (C.c_int, [C.c_void_p, C.c_uint32]),
     "mcpt_set_trace_partitions": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "mcpt_gather": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_int32]),
     "mcpt_wavefront_step": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(StageStats)]),
     "mcpt_iterate": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(StageStats)]),
     "mcpt_render": (C.c_int, [C.c_void_p, C.POINTER(StageStats)]),
@@ -490,6 +491,13 @@ class PathTracer:
         rd = np.zeros((n.value, 3), np.float32)
         self._ck(lib().mcpt_debug_queue_rays(self.h, 0, fptr(ro), fptr(rd), C.byref(n)))
         return ro[: n.value], rd[: n.value]
+
+
+def gather(tracers, root=0):
+    """mcpt_gather: copy every PathTracer's tile-set pixels into tracers[root]'s film (one process,
+    one context per GPU, device-to-device over xGMI)."""
+    arr = (C.c_void_p * len(tracers))(*[t.h for t in tracers])
+    _check(lib().mcpt_gather(arr, len(tracers), root), tracers[root].h)
 
 
 @dataclass(frozen=True)

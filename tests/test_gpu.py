@@ -698,3 +698,36 @@ def test_ploc_small_and_degenerate_inputs(mcpt_mod, oracle):
         assert np.array_equal(pt.trace_closest(ro, rd)[2], oracle.trace_closest(a, ro, rd)[2])
         assert np.array_equal(pt.trace_any(ro, rd), oracle.trace_any(a, ro, rd))
         pt.close()
+
+
+@pytest.mark.parametrize("slots", [1, 2])
+def test_native_gather_equals_one_pass(mcpt_mod, scene_c2, slots):
+    """mcpt_gather (C ABI): three contexts render the interleaved tile partition of a frame
+    ((tx + ty) mod 3, as three GPUs would) and the root gathers the others' tiles; the root's film
+    then equals the single-context frame bit for bit (path slots resolved before the copy)."""
+    from mcpt import parallel
+
+    rc = mcpt_mod.CONFIGS[2]
+    W, H, T = 300, 200, 64
+    cam = mcpt_mod.config_camera(rc, W, H)
+    full = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)
+    full.set_path_slots(slots)
+    full.render()
+    L_full, s_full = full.film()
+    parts = []
+    for r in range(3):
+        pt = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)
+        pt.set_path_slots(slots)
+        pt.set_tiles(parallel.tiles_for_rank(r, 3, W, H, T))
+        pt.render()
+        parts.append(pt)
+    _, s0 = parts[0].film()
+    assert 0 < (s0 > 0).sum() < (s_full > 0).sum()  # the root alone has only its own tiles
+    mcpt_mod.gather(parts, root=0)
+    L, s = parts[0].film()
+    assert np.array_equal(s, s_full)
+    assert np.array_equal(L.view(np.uint32), L_full.view(np.uint32))
+    with pytest.raises(mcpt_mod.McptError):
+        mcpt_mod.gather([parts[0], parts[0]], root=0)  # a context listed twice
+    for pt in parts + [full]:
+        pt.close()
