@@ -674,6 +674,10 @@ __device__ unsigned long long g_trace_prof[12];
 #define MCPT_NODE_STEPS 4
 #endif
 constexpr int kNodeSteps = MCPT_NODE_STEPS;
+#ifndef MCPT_GRAB_MAX
+#define MCPT_GRAB_MAX 0
+#endif
+constexpr int kGrabMax = MCPT_GRAB_MAX;  // rays one hand-out atomic may reserve for a wave (<= 64: only the idle lanes)
 
 // 7 waves per SIMD (<= 72 VGPRs): the persistent grid's measured optimum (launch_geometry).
 // The attribute lets the register allocator park the partition scan's loop-invariant lane
@@ -796,6 +800,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     for (;;) {  // one trip per partition joined
     // Per-lane ray state is declared per partition trip: when the trip ends no lane holds a
     // ray, so none of it is live across the partition scan below (VGPR budget).
+    uint32_t buf_lo = 0, buf_hi = 0, last_p = 0;  // wave-uniform reservation of the partition (refill)
     bool act = false;
     int kind = 0;  // 0 closest, 1 any
     uint32_t rid = 0;
@@ -846,23 +851,47 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         // ---- refill idle lanes with the partition's next rays
         const uint64_t idle = __ballot(!act);
         const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (more && (nidle >= a.refill_min || nidle == 64u)) {
-            uint32_t p0 = 0;
-            if (lane == 0) p0 = __hip_atomic_fetch_add(grab, nidle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            p0 = __builtin_amdgcn_readfirstlane(p0);
-            if (p0 + nidle >= T) {  // the rest of the partition is taken
-                more = false;
-                drained |= 1ull << part;
+        if ((more || buf_lo < buf_hi) && (nidle >= a.refill_min || nidle == 64u)) {
+#ifdef MCPT_TRACE_PROF
+            const uint64_t _rf_t0 = __builtin_readcyclecounter();
+#endif
+            // Positions come from a per-wave reservation [buf_lo, buf_hi) of the partition,
+            // refilled by one atomic when empty.  By default (kGrabMax 0) an atomic reserves
+            // exactly the idle lanes' rays.  Reserving more (a share of what is left, up to
+            // kGrabMax, so later refills skip the atomic's round trip: a refill is three
+            // dependent memory round trips, 7.3K cycles in the profile build) measured slower
+            // on config 2: k_trace 0.775 / 0.785 / 0.812 / 0.874 ms at 0 / 128 / 256 / 512 --
+            // other waves hide the refill latency, the reserved backlog lengthens the tail.
+            if (buf_lo >= buf_hi) {
+                uint32_t G = nidle;
+                if (kGrabMax > 64) {
+                    const uint32_t rem = T > last_p ? T - last_p : 0u;
+                    const uint32_t wpp = max(1u, gridDim.x / nparts);
+                    G = max(nidle, min((uint32_t)kGrabMax, rem / (2u * wpp)));
+                }
+                uint32_t g0 = 0;
+                if (lane == 0) g0 = __hip_atomic_fetch_add(grab, G, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                g0 = __builtin_amdgcn_readfirstlane(g0);
+                last_p = g0 + G;
+                if (g0 + G >= T) {  // the rest of the partition is taken
+                    more = false;
+                    drained |= 1ull << part;
+                }
+                buf_lo = g0;
+                buf_hi = g0 < T ? min(g0 + G, T) : g0;
             }
+            const uint32_t p0 = buf_lo;
+            const uint32_t take = min(nidle, buf_hi - buf_lo);
+            buf_lo += take;
             const uint32_t q = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             const uint32_t pos = p0 + q;  // meaningful on idle lanes
             // entry of the first position: the last e with pre(e) <= p0 (a non-empty one)
-            const uint32_t e0 = p0 < T ? (uint32_t)__popcll(__ballot(s_pre[lane] <= p0)) +
-                                             (uint32_t)__popcll(__ballot(s_pre[64 + lane] <= p0)) - 1u
-                                       : 0u;
+            const uint32_t e0 = take ? (uint32_t)__popcll(__ballot(s_pre[lane] <= p0)) +
+                                           (uint32_t)__popcll(__ballot(s_pre[64 + lane] <= p0)) - 1u
+                                     : 0u;
             if (!act) {
-                if (pos < T) {
+                if (q < take) {
                     uint32_t my_e = e0;
                     while (pos >= s_pre[my_e + 1]) my_e++;  // the grab spans entries (rarely a step)
                     const uint32_t my_pre = s_pre[my_e];
@@ -916,10 +945,17 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #ifdef MCPT_WAVE_TIMES
             if (!more && lane == 0 && blockIdx.x < 16384) g_wave_t[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef MCPT_TRACE_PROF
+            {   // refill latency: atomic, queue entry and ray loads until the new lanes are set up
+                float _sink = inv.x + o.x;
+                __asm__ volatile("" :: "v"(_sink));
+                PROF_ADD(11, __builtin_readcyclecounter() - _rf_t0);
+            }
+#endif
             PROF_ADD(1, 1);
         }
         if (__ballot(act) == 0) {
-            if (!more) break;  // partition drained, every lane idle
+            if (!more && buf_lo >= buf_hi) break;  // partition drained, every lane idle
             continue;
         }
         // ---- node phase: up to kNodeSteps child-pair tests per lane holding an
