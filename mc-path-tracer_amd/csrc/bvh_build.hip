@@ -205,7 +205,7 @@ __global__ void k_permute(int n, const uint32_t* __restrict__ idx, const float4*
     if (i >= n) return;
     const uint32_t p = idx[i];
     for (int k = 0; k < 3; k++) {
-        tri_out[3 * i + k] = tri_in[3 * p + k];
+        tri_out[kTriF4 * i + k] = tri_in[kTriF4 * p + k];
         sh_out[3 * i + k] = sh_in[3 * p + k];
     }
 }
@@ -406,7 +406,7 @@ static int sort_prims(const LbvhInput& in, LbvhOutput& out, Bufs& tmp, hipStream
     const int ni = std::max(n - 1, 1);
     out.nodes = nullptr;
     if (hipMalloc(&out.nodes, std::max<size_t>((size_t)ni * 4 * sizeof(float4), 16)) != hipSuccess) return -2;
-    if (hipMalloc(&out.tri, 3 * (size_t)n * sizeof(float4)) != hipSuccess) return -2;
+    if (hipMalloc(&out.tri, kTriF4 * (size_t)n * sizeof(float4)) != hipSuccess) return -2;
     if (hipMalloc(&out.tri_sh, 3 * (size_t)n * sizeof(float4)) != hipSuccess) return -2;
     hipLaunchKernelGGL(k_permute, dim3(g), dim3(kB), 0, s, n, idx_s, in.d_tri, in.d_sh, out.tri, out.tri_sh);
     return 0;

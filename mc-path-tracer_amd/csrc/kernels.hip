@@ -182,7 +182,7 @@ __device__ inline bool ray_misses_scene(const DevScene& sc, V3 o, V3 d) {
 // (Triangle.cu:66-92): Moller-Trumbore t/u/v, the interpolated normal
 // normalised twice (identity transform), position o + t d, material id.
 __device__ inline void hit_record(const DevScene& sc, V3 o, V3 d, int tri, V3& pos, V3& nrm, int& mat, float& t_out) {
-    const float4* tp = sc.tri + 3 * tri;
+    const float4* tp = sc.tri + kTriF4 * tri;
     const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
     float t, u, v;
     tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v);
@@ -678,6 +678,13 @@ constexpr int kNodeSteps = MCPT_NODE_STEPS;
 #define MCPT_GRAB_MAX 0
 #endif
 constexpr int kGrabMax = MCPT_GRAB_MAX;  // rays one hand-out atomic may reserve for a wave (<= 64: only the idle lanes)
+// Order of a partition's ray sequence: extension rays first (MCPT_ANY_FIRST=1: the costlier
+// any-hit rays first, so the tail is made of cheap rays -- measured mixed: config 2 k_trace
+// 0.779 -> 0.791 ms, config 3 1.149 -> 1.129, config 5 17.09 -> 17.27).
+#ifndef MCPT_ANY_FIRST
+#define MCPT_ANY_FIRST 0
+#endif
+constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
 
 // 7 waves per SIMD (<= 72 VGPRs): the persistent grid's measured optimum (launch_geometry).
 // The attribute lets the register allocator park the partition scan's loop-invariant lane
@@ -758,8 +765,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #pragma unroll 1
         for (uint32_t h = 0; h < 2; h++) {
             const uint32_t e = (uint32_t)lane + 64u * h;
-            const bool k1 = e >= spart;
-            const uint32_t j = k1 ? e - spart : e;
+            const bool k1 = kAnyFirst ? e < spart : e >= spart;  // entry e belongs to set 1 (any hit)
+            const uint32_t j = e >= spart ? e - spart : e;
             uint32_t ne = 0;
             if (e < 2 * spart) {
                 const TraceSet& ts = k1 ? a.set[1] : a.set[0];
@@ -895,8 +902,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     uint32_t my_e = e0;
                     while (pos >= s_pre[my_e + 1]) my_e++;  // the grab spans entries (rarely a step)
                     const uint32_t my_pre = s_pre[my_e];
-                    kind = my_e >= spart;
-                    const uint32_t sh = part + (kind ? my_e - spart : my_e) * nparts;
+                    kind = kAnyFirst ? my_e < spart : my_e >= spart;
+                    const uint32_t sh = part + (my_e >= spart ? my_e - spart : my_e) * nparts;
                     const uint32_t qslot = sh * (kind ? a.set[1].shard_cap : a.set[0].shard_cap) + (pos - my_pre);
                     // select the set's fields with ternaries: indexing a.set[kind] with a
                     // per-lane kind makes hipcc fetch them from kernarg memory per lane
@@ -1034,8 +1041,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #ifdef MCPT_X_PREFETCH  // experiment: touch both children (node line or triangle record) before the slab
                 {
                     const int p0 = __float_as_int(q3.x), p1 = __float_as_int(q3.y);
-                    const uint32_t* w0 = p0 >= 0 ? (const uint32_t*)(sc.nodes + 4 * p0) : (const uint32_t*)(sc.tri + 3 * (p0 & 0xffffff));
-                    const uint32_t* w1 = p1 >= 0 ? (const uint32_t*)(sc.nodes + 4 * p1) : (const uint32_t*)(sc.tri + 3 * (p1 & 0xffffff));
+                    const uint32_t* w0 = p0 >= 0 ? (const uint32_t*)(sc.nodes + 4 * p0) : (const uint32_t*)(sc.tri + kTriF4 * (p0 & 0xffffff));
+                    const uint32_t* w1 = p1 >= 0 ? (const uint32_t*)(sc.nodes + 4 * p1) : (const uint32_t*)(sc.tri + kTriF4 * (p1 & 0xffffff));
                     pfx ^= w0[0] ^ w1[0];
                 }
 #endif
@@ -1104,7 +1111,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             PROF_ADD(4, n_tri);
             if (leaf != kEnd) {
                 const int id = leaf & 0xffffff;
-                const float4* tp = sc.tri + 3 * id;
+                const float4* tp = sc.tri + kTriF4 * id;
                 const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
                 RAY_STEP_TRI();
                 tot_t0 += kind == 0 ? 1u : 0u;
@@ -1115,7 +1122,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     !(t < 0.f) &&
                     (kind ? t < K_HUGE
                           : (t < best ||
-                             (t == best && tri >= 0 && __float_as_int(w2.y) < __float_as_int(sc.tri[3 * tri + 2].y))))) {
+                             (t == best && tri >= 0 && __float_as_int(w2.y) < __float_as_int(sc.tri[kTriF4 * tri + 2].y))))) {
                     if (kind) {
                         tri = id;  // occluded (tmax 1e32)
                         done = true;
@@ -1218,7 +1225,7 @@ __global__ void k_hit_record(HitRecordArgs a) {  // stage_run(EXTEND) outputs
         a.scene_tri[i] = -1;
         return;
     }
-    a.scene_tri[i] = __float_as_int(a.scene.tri[3 * tri + 2].y);  // storage position -> scene index
+    a.scene_tri[i] = __float_as_int(a.scene.tri[kTriF4 * tri + 2].y);  // storage position -> scene index
     V3 pos, nrm;
     int mat;
     float t;

@@ -48,10 +48,16 @@ enum : uint32_t {
 #endif
 constexpr int kNodeWidth = MCPT_BVH_WIDTH;
 constexpr int kNodeF4 = kNodeWidth == 4 ? 8 : 4;  // float4 per node
+// float4 per triangle intersection record: 3 (48 B, packed) or 4 (64 B: a record never
+// straddles two 64-B halves of a cache line; MCPT_TRI_F4)
+#ifndef MCPT_TRI_F4
+#define MCPT_TRI_F4 3
+#endif
+constexpr int kTriF4 = MCPT_TRI_F4;
 
 struct DevScene {
     const float4* nodes;    // BVH nodes (kNodeWidth children each, kNodeF4 x float4)
-    const float4* tri;      // 3 x float4: (v0.xyz, e1.x) (e1.yz, e2.xy) (e2.z, id, -, -); id = tri_id bits
+    const float4* tri;      // kTriF4 x float4: (v0.xyz, e1.x) (e1.yz, e2.xy) (e2.z, id, -, -) [pad]; id = tri_id bits
     const float4* tri_sh;   // 3 x float4: (n0.xyz, n1.x) (n1.yz, n2.xy) (n2.z, mat, -, -)
     float root_mn[3], root_mx[3];
     int root_ref;           // >= 0 pair node, < 0 leaf (0x80000000 | (count-1)<<24 | offset)

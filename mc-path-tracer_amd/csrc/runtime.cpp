@@ -399,16 +399,16 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     depth += xdepth;
     if (depth > kMaxStack) return set_err(c, MCPT_E_INVALID, "BVH deeper than the 64-entry traversal stack");
     c->pair_depth = depth;
-    std::vector<float4> tri((size_t)d->ntri * 3), sh((size_t)d->ntri * 3);
+    std::vector<float4> tri((size_t)d->ntri * kTriF4, make_float4(0.f, 0.f, 0.f, 0.f)), sh((size_t)d->ntri * 3);
     for (int32_t i = 0; i < d->ntri; i++) {
         mcpt::V3 p0 = mcpt::ld3(d->v0, i), p1 = mcpt::ld3(d->v1, i), p2 = mcpt::ld3(d->v2, i);
         mcpt::V3 e1 = p1 - p0, e2 = p2 - p0;  // Triangle.cu:13-14
-        tri[3 * i + 0] = make_float4(p0.x, p0.y, p0.z, e1.x);
-        tri[3 * i + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+        tri[kTriF4 * i + 0] = make_float4(p0.x, p0.y, p0.z, e1.x);
+        tri[kTriF4 * i + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
         const int32_t id = d->tri_id ? d->tri_id[i] : i;
         float fi;
         memcpy(&fi, &id, 4);  // triangle id: the traversal's tie-break key and the API's triangle id
-        tri[3 * i + 2] = make_float4(e2.z, fi, 0.f, 0.f);
+        tri[kTriF4 * i + 2] = make_float4(e2.z, fi, 0.f, 0.f);
         mcpt::V3 n0 = mcpt::ld3(d->n0, i), n1 = mcpt::ld3(d->n1, i), n2 = mcpt::ld3(d->n2, i);
         float fm;
         int mm = d->mat[i];
