@@ -7,7 +7,7 @@ sys.path[:0] = [os.path.join(REPO, "mc-path-tracer_amd")]
 import mcpt
 rc = mcpt.CONFIGS[int(os.environ.get("CFG", "2"))]
 pt = mcpt.PathTracer(0, mcpt.default_config(spp=rc.spp, max_depth=rc.max_depth))
-pt.upload_scene(mcpt.build_config_scene(int(os.environ.get("CFG", "2")))); pt.set_camera(mcpt.config_camera(rc)); pt.resize(rc.width, rc.height)
+pt.upload_scene(mcpt.build_config_scene(int(os.environ.get("CFG", "2")))); pt.set_camera(mcpt.config_camera(rc)); pt.set_path_slots(int(os.environ.get("SLOTS", "3"))); pt.resize(rc.width, rc.height)
 pt.iterate(30)
 L = mcpt.lib()
 f = L.mcpt_debug_wave_times
