@@ -60,6 +60,11 @@ __device__ inline void block_push(const bool (&want)[NQ], uint32_t* const (&coun
 }
 
 __device__ inline V3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
+// the xyz of a float4 element with one dwordx3 load (one VGPR fewer than the float4)
+__device__ inline V3 ld3f4(const float4* p) {
+    const float* f = reinterpret_cast<const float*>(p);
+    return v3(f[0], f[1], f[2]);
+}
 __device__ inline float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
 __device__ inline V3 light_L(const DevScene& sc, int id, V3 wi) {
@@ -407,6 +412,13 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     uint32_t cont_len = 0, cont_samples = 0;
     int32_t cont_htri = -1;
     V3 beta_store = v3(0.f, 0.f, 0.f);
+    // A primary ray that missed adds the background (env_L of its direction) to the film.
+    // That is done after the pushes, where the logic's state is dead: the env lookup's
+    // temporaries on top of the logic's live values set the kernel's register peak (81 VGPRs,
+    // 5 waves per SIMD, against 48 without it).  Nothing else touches such a path's film in
+    // this iteration, so the order of the two film updates does not change a bit.
+    bool bg = false;
+    V3 bg_film = v3(0.f, 0.f, 0.f), bg_dir = bg_film;
     if (valid) {
         // Every load the logic may need is issued up front, in one round: the
         // per-path state unconditionally, the len-dependent streams (ray_d for a
@@ -416,11 +428,11 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         uint32_t samples = a.p.samples[pid];
         const int32_t htri = a.p.hit_tri[pid];
         const float4 b4 = a.p.beta[(((fl >> F_LEN_SHIFT) & 0xffu) > 1u) ? pid : 0u];  // len 1: beta is (1,1,1), not loaded
-        const float4 ld4 = a.p.Ld[pid];
+        const V3 ld4 = ld3f4(a.p.Ld + pid);  // .w is always 0 (k_clear, k_resolve): xyz only
         const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
         const bool need_rd = len == 1 && htri < 0;
         const bool need_nee = len <= (uint32_t)a.max_depth && len > 1;
-        const float4 rd = a.p.ray_d[need_rd ? pid : 0u];
+        const V3 rd = ld3f4(a.p.ray_d + (need_rd ? pid : 0u));
         const float4 n0 = a.p.nee0[need_nee ? pid : 0u], n1 = a.p.nee1[need_nee ? pid : 0u];
         const uchar2 vv = reinterpret_cast<const uchar2*>(a.p.vis)[need_nee ? pid : 0u];
         bool dead = (fl & F_DEAD) != 0;
@@ -431,15 +443,16 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             const Rng r{rng_key(a.seed, pix, sidx), len};
             const bool found = htri >= 0;
             const V3 B = len == 1 ? v3(1.f, 1.f, 1.f) : xyz(b4);  // wf_generate's beta (:245)
-            V3 film = xyz(ld4);
+            V3 film = ld4;
             bool terminate = false;
             beta_store = B;
             if (len == 1) {  // :129-140
                 if (found) {
                     film = film + v3(0.f, 0.f, 0.f) * B;
-                } else {
-                    const int nbg = FIXED ? 1 : sc.nlights;  // reference adds it once per light (A.4)
-                    for (int i = 0; i < nbg; i++) film = film + env_L(sc.env, xyz(rd)) * B;
+                } else {  // background (:135-138): added below, after the pushes
+                    bg = true;
+                    bg_film = film;
+                    bg_dir = rd;
                 }
             }
             if (len > (uint32_t)a.max_depth || !found) terminate = true;  // :142-146
@@ -473,7 +486,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             // film unchanged bit for bit (a zero contribution): the store would rewrite the same bytes
             if (__float_as_uint(film.x) != __float_as_uint(ld4.x) || __float_as_uint(film.y) != __float_as_uint(ld4.y) ||
                 __float_as_uint(film.z) != __float_as_uint(ld4.z))
-                a.p.Ld[pid] = f4(film, ld4.w);
+                a.p.Ld[pid] = f4(film, 0.f);
             if (terminate) {  // :199-204
                 dead = true;
                 samples++;
@@ -527,6 +540,14 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     uint32_t n_ext = (gen_ext || gen_trivial) ? 1u : 0u;  // queued + resolved-in-place rays
     for (int off = 32; off > 0; off >>= 1) n_ext += __shfl_xor(n_ext, off);
     if (lane == 0 && n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
+    if (bg) {  // wavefront_kernels.cu:129-140, len 1 and no hit: beta is (1,1,1)
+        const int nbg = FIXED ? 1 : sc.nlights;  // the reference adds it once per light (A.4)
+        V3 film = bg_film;
+        for (int i = 0; i < nbg; i++) film = film + env_L(sc.env, bg_dir) * v3(1.f, 1.f, 1.f);
+        if (__float_as_uint(film.x) != __float_as_uint(bg_film.x) || __float_as_uint(film.y) != __float_as_uint(bg_film.y) ||
+            __float_as_uint(film.z) != __float_as_uint(bg_film.z))
+            a.p.Ld[pid] = f4(film, 0.f);
+    }
 #ifdef MCPT_SHADE_PROF
     {
         unsigned long long _n = __builtin_readcyclecounter();
