@@ -221,7 +221,7 @@ def main():
     # dominant kernel by summed HIP-event time over the timed region (same stream as the kernels);
     # k_trace traces the extension (closest-hit) and any-hit rays of an iteration in one launch
     kern = {"k_trace": st.ms_extend + st.ms_shadow, "k_shade": st.ms_shade}
-    names = {"k_trace": ("mcpt_dev::k_trace(",), "k_shade": ("mcpt_dev::k_shade<", "mcpt_dev::k_material<")}
+    names = {"k_trace": ("mcpt_dev::k_trace(", "mcpt_dev::k_trace<"), "k_shade": ("mcpt_dev::k_shade<", "mcpt_dev::k_material<")}
     dom = max(kern, key=kern.get)
     byts = b_ext + b_any if dom == "k_trace" else b_shd
     state = (B_EXT_STATE * st.extend_rays + B_ANY_STATE * (st.shadow_rays + st.vis_rays)) if dom == "k_trace" else b_shd

@@ -718,6 +718,7 @@ constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
 __device__ unsigned long long g_wave_t[4 * 16384];  // per wave: s_memrealtime (100 MHz, chip-wide) at entry and
                                                      // exit, partition, time its partition ran dry for it
 #endif
+template <int kLdsStack>
 __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs a) {
 #ifdef MCPT_WAVE_TIMES
     if (threadIdx.x == 0 && blockIdx.x < 16384) g_wave_t[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -1391,7 +1392,9 @@ int launch_geometry(int dev, LaunchGeom& g) {
     int cus = 0, nx = 1, per_cu = 0, mat0 = 0, mat1 = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
     if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess) nx = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace, kTraceBlock, 0) != hipSuccess ||
+    int per_cu_deep = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<kLdsStack>, kTraceBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_deep, k_trace<kLdsStackDeep>, kTraceBlock, 0) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat0, k_material<false>, kBlock, 0) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat1, k_material<true>, kBlock, 0) != hipSuccess)
         return -1;
@@ -1400,6 +1403,7 @@ int launch_geometry(int dev, LaunchGeom& g) {
     if (const char* e = getenv("MCPT_TRACE_WAVES")) per_cu = atoi(e);
     if (per_cu <= 0) per_cu = 16;
     g.trace_waves = (uint32_t)(cus * per_cu);
+    g.trace_waves_deep = (uint32_t)(cus * std::max(1, std::min(per_cu, per_cu_deep)));
     g.ndies = (uint32_t)std::max(1, nx);
     // Two partitions (hand-out counters) per die: one counter per die serialised the
     // returning atomics (config 2 k_trace 0.82 ms at 8 partitions, 0.767 at 16, 0.766 at
@@ -1429,8 +1433,16 @@ void launch_trace(const TraceArgs& args, const LaunchGeom& g, hipStream_t s) {
     a.nparts = std::min<uint32_t>(kMaxParts, std::max<uint32_t>(1, g.trace_parts));
     a.ndies = g.ndies;
     const uint32_t nsh = (uint32_t)a.nshards;
-    const uint32_t wps = std::max<uint32_t>(1, g.trace_waves / nsh);
-    hipLaunchKernelGGL(k_trace, dim3(wps * nsh), dim3(kTraceBlock), 0, s, a);
+    // Deep trees (beyond kDeepTree levels) take the deeper LDS stack: fewer pushes spill to
+    // scratch, at one resident wave per CU less (LDS-limited).  Config 5 (depth 25): 17.3 ->
+    // 16.5 ms per launch; config 2 (depth 16) 0.781 -> 0.815 ms with it, so shallow trees keep 8.
+    if (a.scene.depth > kDeepTree) {
+        const uint32_t wps = std::max<uint32_t>(1, g.trace_waves_deep / nsh);
+        hipLaunchKernelGGL(k_trace<kLdsStackDeep>, dim3(wps * nsh), dim3(kTraceBlock), 0, s, a);
+    } else {
+        const uint32_t wps = std::max<uint32_t>(1, g.trace_waves / nsh);
+        hipLaunchKernelGGL(k_trace<kLdsStack>, dim3(wps * nsh), dim3(kTraceBlock), 0, s, a);
+    }
 }
 __global__ void k_quot(const float* a, const float* b, float* out, uint32_t n) {  // mcpt_debug_quot
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -29,6 +29,8 @@ constexpr int kTraceBlock = 64;  // one wave per traversal block
 #define MCPT_LDS_STACK 8
 #endif
 constexpr int kLdsStack = MCPT_LDS_STACK;  // traversal stack entries per lane kept in LDS (deeper: scratch)
+constexpr int kLdsStackDeep = 10;          // the same for trees deeper than kDeepTree levels
+constexpr int kDeepTree = 20;
 constexpr int kMaxStack = 64;  // total (reference: int nodesToVisit[64], Triangle.cu:161)
 
 enum : uint32_t {
@@ -61,6 +63,7 @@ struct DevScene {
     const float4* tri_sh;   // 3 x float4: (n0.xyz, n1.x) (n1.yz, n2.xy) (n2.z, mat, -, -)
     float root_mn[3], root_mx[3];
     int root_ref;           // >= 0 pair node, < 0 leaf (0x80000000 | (count-1)<<24 | offset)
+    int depth;              // pair-tree depth (bound on stack pushes): picks the k_trace instantiation
     int nlights;            // 1 + ndir (Scene.cu:370-388)
     const float* mats;      // 8 floats per material
     const float* dirs;      // 7 floats per directional light
@@ -147,6 +150,7 @@ struct UnpackArgs { const float4* in; const int2* tiles; int ntiles, tile_w, til
 // calculator and the device's XCD count, with environment overrides for sweeps.
 struct LaunchGeom {
     uint32_t trace_waves;    // k_trace grid (waves), MCPT_TRACE_WAVES = waves per CU
+    uint32_t trace_waves_deep;  // the same for the deep-stack instantiation (LDS-limited)
     uint32_t trace_parts;    // k_trace work partitions, MCPT_TRACE_PARTS (1..kMaxParts)
     uint32_t ndies;          // XCDs
     uint32_t mat_blocks[2];  // k_material grid [reference mode, fixed mode]

@@ -536,6 +536,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             s.env.ltab[1] = lt1;
         }
     }
+    s.depth = c->pair_depth;
     c->scene = s;
     if (c->has_scene_before) c->film_stale = true;  // a re-upload notifies the film
     c->has_scene = true;
