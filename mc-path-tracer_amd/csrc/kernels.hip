@@ -710,15 +710,20 @@ constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
 // 7 waves per SIMD (<= 72 VGPRs): the persistent grid's measured optimum (launch_geometry).
 // The attribute lets the register allocator park the partition scan's loop-invariant lane
 // addresses in scratch (two spills, reloaded only by the scan) instead of giving up a wave.
+// The 4-wide instantiation holds 8 float4 of node data per step: 6 waves (80 VGPRs).
 #ifndef MCPT_TRACE_WPE
 #define MCPT_TRACE_WPE 7
 #endif
-#define MCPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_TRACE_WPE, MCPT_TRACE_WPE)))
+#ifndef MCPT_TRACE_WPE4
+#define MCPT_TRACE_WPE4 6
+#endif
+#define MCPT_TRACE_ATTR \
+    __attribute__((amdgpu_waves_per_eu(kW == 4 ? MCPT_TRACE_WPE4 : MCPT_TRACE_WPE, kW == 4 ? MCPT_TRACE_WPE4 : MCPT_TRACE_WPE)))
 #ifdef MCPT_WAVE_TIMES
 __device__ unsigned long long g_wave_t[4 * 16384];  // per wave: s_memrealtime (100 MHz, chip-wide) at entry and
                                                      // exit, partition, time its partition ran dry for it
 #endif
-template <int kLdsStack>
+template <int kW, int kLdsStack>  // node width (2: child pairs, 4: quads), LDS stack entries per lane
 __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs a) {
 #ifdef MCPT_WAVE_TIMES
     if (threadIdx.x == 0 && blockIdx.x < 16384) g_wave_t[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -1001,7 +1006,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
               tot_n0 += kind == 0 ? 1u : 0u;
               tot_n1 += kind != 0 ? 1u : 0u;
               const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;  // slow-path slab only
-              if constexpr (kNodeWidth == 4) {
+              if constexpr (kW == 4) {
                 // 4-wide node: test the four child boxes, visit the nearest hit, push the
                 // other hits far-to-near with their entry t (popped nearest-first)
                 const float4* nd = sc.nodes + 8 * ref;
@@ -1392,18 +1397,20 @@ int launch_geometry(int dev, LaunchGeom& g) {
     int cus = 0, nx = 1, per_cu = 0, mat0 = 0, mat1 = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
     if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess) nx = 1;
-    int per_cu_deep = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<kLdsStack>, kTraceBlock, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_deep, k_trace<kLdsStackDeep>, kTraceBlock, 0) != hipSuccess ||
+    int occ[2][2] = {};  // [width 2 / 4][LDS stack 8 / deep]
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0][0], k_trace<2, kLdsStack>, kTraceBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0][1], k_trace<2, kLdsStackDeep>, kTraceBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1][0], k_trace<4, kLdsStack>, kTraceBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1][1], k_trace<4, kLdsStackDeep>, kTraceBlock, 0) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat0, k_material<false>, kBlock, 0) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat1, k_material<true>, kBlock, 0) != hipSuccess)
         return -1;
     if (cus <= 0) cus = 256;
-    per_cu = std::min(per_cu, 28);
+    per_cu = 28;
     if (const char* e = getenv("MCPT_TRACE_WAVES")) per_cu = atoi(e);
     if (per_cu <= 0) per_cu = 16;
-    g.trace_waves = (uint32_t)(cus * per_cu);
-    g.trace_waves_deep = (uint32_t)(cus * std::max(1, std::min(per_cu, per_cu_deep)));
+    for (int w = 0; w < 2; w++)
+        for (int k = 0; k < 2; k++) g.trace_waves[w][k] = (uint32_t)(cus * std::max(1, std::min(per_cu, occ[w][k])));
     g.ndies = (uint32_t)std::max(1, nx);
     // Two partitions (hand-out counters) per die: one counter per die serialised the
     // returning atomics (config 2 k_trace 0.82 ms at 8 partitions, 0.767 at 16, 0.766 at
@@ -1436,13 +1443,14 @@ void launch_trace(const TraceArgs& args, const LaunchGeom& g, hipStream_t s) {
     // Deep trees (beyond kDeepTree levels) take the deeper LDS stack: fewer pushes spill to
     // scratch, at one resident wave per CU less (LDS-limited).  Config 5 (depth 25): 17.3 ->
     // 16.5 ms per launch; config 2 (depth 16) 0.781 -> 0.815 ms with it, so shallow trees keep 8.
-    if (a.scene.depth > kDeepTree) {
-        const uint32_t wps = std::max<uint32_t>(1, g.trace_waves_deep / nsh);
-        hipLaunchKernelGGL(k_trace<kLdsStackDeep>, dim3(wps * nsh), dim3(kTraceBlock), 0, s, a);
-    } else {
-        const uint32_t wps = std::max<uint32_t>(1, g.trace_waves / nsh);
-        hipLaunchKernelGGL(k_trace<kLdsStack>, dim3(wps * nsh), dim3(kTraceBlock), 0, s, a);
-    }
+    // The node width is the scene's (DevScene::width, chosen at upload).
+    const int w = a.scene.width == 4 ? 1 : 0, k = a.scene.depth > kDeepTree ? 1 : 0;
+    const uint32_t wps = std::max<uint32_t>(1, g.trace_waves[w][k] / nsh);
+    const dim3 grid(wps * nsh), block(kTraceBlock);
+    if (w == 0 && k == 0) hipLaunchKernelGGL((k_trace<2, kLdsStack>), grid, block, 0, s, a);
+    else if (w == 0) hipLaunchKernelGGL((k_trace<2, kLdsStackDeep>), grid, block, 0, s, a);
+    else if (k == 0) hipLaunchKernelGGL((k_trace<4, kLdsStack>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_trace<4, kLdsStackDeep>), grid, block, 0, s, a);
 }
 __global__ void k_quot(const float* a, const float* b, float* out, uint32_t n) {  // mcpt_debug_quot
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

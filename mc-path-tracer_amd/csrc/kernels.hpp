@@ -42,14 +42,9 @@ enum : uint32_t {
     F_HASVIS = 1u << 12     // non-delta light: a BRDF visibility ray was traced
 };
 
-// BVH node width of the traversal (MCPT_BVH_WIDTH, 2 or 4).  Width 2: child-pair
-// nodes, 4 x float4 (per axis (mn0, mn1, mx0, mx1), then refs).  Width 4: 8 x float4:
+// BVH node width of the traversal, per scene (DevScene::width): width 2, child-pair
+// nodes, 4 x float4 (per axis (mn0, mn1, mx0, mx1), then refs); width 4, 8 x float4:
 // mn.x[4], mx.x[4], mn.y[4], mx.y[4], mn.z[4], mx.z[4], refs[4] (kEnd = empty), pad.
-#ifndef MCPT_BVH_WIDTH
-#define MCPT_BVH_WIDTH 2
-#endif
-constexpr int kNodeWidth = MCPT_BVH_WIDTH;
-constexpr int kNodeF4 = kNodeWidth == 4 ? 8 : 4;  // float4 per node
 // float4 per triangle intersection record: 3 (48 B, packed) or 4 (64 B: a record never
 // straddles two 64-B halves of a cache line; MCPT_TRI_F4)
 #ifndef MCPT_TRI_F4
@@ -58,12 +53,13 @@ constexpr int kNodeF4 = kNodeWidth == 4 ? 8 : 4;  // float4 per node
 constexpr int kTriF4 = MCPT_TRI_F4;
 
 struct DevScene {
-    const float4* nodes;    // BVH nodes (kNodeWidth children each, kNodeF4 x float4)
+    const float4* nodes;    // BVH nodes (width children each: 4 or 8 float4)
     const float4* tri;      // kTriF4 x float4: (v0.xyz, e1.x) (e1.yz, e2.xy) (e2.z, id, -, -) [pad]; id = tri_id bits
     const float4* tri_sh;   // 3 x float4: (n0.xyz, n1.x) (n1.yz, n2.xy) (n2.z, mat, -, -)
     float root_mn[3], root_mx[3];
     int root_ref;           // >= 0 pair node, < 0 leaf (0x80000000 | (count-1)<<24 | offset)
-    int depth;              // pair-tree depth (bound on stack pushes): picks the k_trace instantiation
+    int depth;              // bound on stack pushes of the uploaded tree: picks the k_trace instantiation
+    int width;              // node width: 2 (child pairs) or 4 (quads)
     int nlights;            // 1 + ndir (Scene.cu:370-388)
     const float* mats;      // 8 floats per material
     const float* dirs;      // 7 floats per directional light
@@ -149,8 +145,8 @@ struct UnpackArgs { const float4* in; const int2* tiles; int ntiles, tile_w, til
 // Launch geometry of one device (mcpt_create): persistent grids from the occupancy
 // calculator and the device's XCD count, with environment overrides for sweeps.
 struct LaunchGeom {
-    uint32_t trace_waves;    // k_trace grid (waves), MCPT_TRACE_WAVES = waves per CU
-    uint32_t trace_waves_deep;  // the same for the deep-stack instantiation (LDS-limited)
+    uint32_t trace_waves[2][2];  // k_trace grid (waves) per [node width 2/4][LDS stack normal/deep];
+                                 // at most 28 waves per CU (MCPT_TRACE_WAVES overrides)
     uint32_t trace_parts;    // k_trace work partitions, MCPT_TRACE_PARTS (1..kMaxParts)
     uint32_t ndies;          // XCDs
     uint32_t mat_blocks[2];  // k_material grid [reference mode, fixed mode]

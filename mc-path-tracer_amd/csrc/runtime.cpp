@@ -176,7 +176,7 @@ int mcpt_device_name(mcpt_ctx* c, char* buf, int32_t len) {
 // Scene upload: LinearBVHNode (BVH.h:63-72) -> child-pair nodes, dTriangle
 // (Triangle.h:11-23, 288 B) -> 48-B intersection + 48-B shading records.
 
-// Collapse a child-pair BVH into 4-wide nodes (kNodeWidth == 4): every 4-wide node
+// Collapse a child-pair BVH into 4-wide nodes (DevScene::width 4): every 4-wide node
 // is a pair node at even depth; its slots are the children of its two children
 // (a leaf child takes one slot itself).  Boxes are copied, never recomputed, so
 // every leaf box is the pair tree's (and the reference builder's) exact box.
@@ -445,8 +445,17 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     if ((rc = dupload(c, c->scene_bufs, &dm, d->mat_params, (size_t)d->nmat * 8))) return rc;
     if ((rc = dupload(c, c->scene_bufs, &dd, d->dir_params, (size_t)d->ndir * 7))) return rc;
     s.nodes = dn; s.tri = dt; s.tri_sh = dsh; s.mats = dm; s.dirs = dd;
-    int quad_root = 0;
-    if (kNodeWidth == 4) {
+    // Node width: 4-wide nodes (one 128-B line tests four boxes, half the levels) for trees
+    // of more than 32 MB of pair nodes, child pairs otherwise.  Per launch, interleaved on one
+    // box: config 5 (2 M tris, 128 MB) 16.7 -> 15.6 ms and config 3 (871K, 55 MB) 1.154 ->
+    // 1.148 ms with quads; config 4 (252K, 16 MB) 7.69 -> 7.79 ms and config 2 (4.8K) 0.783 ->
+    // 0.848 ms, so those keep pairs.  MCPT_BVH_WIDTH=2/4 forces a width.
+    const size_t tree_pairs = gpu_bvh ? (size_t)lb.nnodes : pn.size() / 4;
+    int width = tree_pairs * 64 > ((size_t)32 << 20) ? 4 : 2;
+    if (const char* we = getenv("MCPT_BVH_WIDTH"))
+        if ((we[0] == '2' || we[0] == '4') && we[1] == 0) width = we[0] - '0';
+    int quad_root = 0, quad_push = 0;
+    if (width == 4) {
         // 4-wide traversal: collapse the pair tree (host SAH or GPU LBVH) into 4-wide nodes
         std::vector<float4> pairs;
         int proot;
@@ -463,6 +472,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         if (d->ntri > 0) {
             pairs_to_quads(pairs, proot, quads, quad_root, max_push);
             if (max_push > kMaxStack) return set_err(c, MCPT_E_INVALID, "4-wide BVH needs more than 64 stack entries");
+            quad_push = max_push;
             float4* dq;
             if ((rc = dupload(c, c->scene_bufs, &dq, quads.data(), quads.size()))) return rc;
             s.nodes = dq;
@@ -471,10 +481,10 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     s.nlights = 1 + d->ndir;
     if (gpu_bvh && d->ntri > 0) {
         for (int k = 0; k < 3; k++) { s.root_mn[k] = lb.root_mn[k]; s.root_mx[k] = lb.root_mx[k]; }
-        s.root_ref = kNodeWidth == 4 ? (lb.root_ref < 0 ? lb.root_ref : quad_root) : lb.root_ref;
+        s.root_ref = width == 4 ? (lb.root_ref < 0 ? lb.root_ref : quad_root) : lb.root_ref;
     } else if (N > 0) {
         for (int k = 0; k < 3; k++) { s.root_mn[k] = d->bmin[k]; s.root_mx[k] = d->bmax[k]; }
-        s.root_ref = kNodeWidth == 4 ? (ref_of(0) < 0 ? ref_of(0) : quad_root) : ref_of(0);
+        s.root_ref = width == 4 ? (ref_of(0) < 0 ? ref_of(0) : quad_root) : ref_of(0);
     } else {
         // empty scene: a root box that no ray can enter
         for (int k = 0; k < 3; k++) { s.root_mn[k] = 1.f; s.root_mx[k] = -1.f; }
@@ -536,7 +546,8 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             s.env.ltab[1] = lt1;
         }
     }
-    s.depth = c->pair_depth;
+    s.depth = width == 4 ? quad_push : c->pair_depth;
+    s.width = width;
     c->scene = s;
     if (c->has_scene_before) c->film_stale = true;  // a re-upload notifies the film
     c->has_scene = true;

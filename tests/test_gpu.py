@@ -757,3 +757,52 @@ def test_config45_full_frame_band_parity(mcpt_mod, oracle, cid, rows, slots):
     ok, nbad = film_close(Ld[r0:r1], rL[r0:r1])
     assert ok, f"{nbad} radiance values differ"
     pt.close()
+
+
+@pytest.mark.parametrize("gpu_bvh", [False, "ploc"])
+@pytest.mark.parametrize("which", ["scene_c1", "scene_c2", "scene_cube", "scene_c3"])
+def test_quad_nodes_same_hits(request, mcpt_mod, oracle, which, gpu_bvh):
+    """4-wide nodes (the default for trees beyond L2; MCPT_BVH_WIDTH=4 forces them here): the
+    collapse copies boxes, never recomputes them, so hits stay bit-identical to the oracle's."""
+    s, a = request.getfixturevalue(which)
+    old = os.environ.get("MCPT_BVH_WIDTH")
+    os.environ["MCPT_BVH_WIDTH"] = "4"
+    try:
+        pt = mcpt_mod.PathTracer(0)
+        pt.upload_scene(s, gpu_bvh=gpu_bvh)
+    finally:
+        if old is None:
+            os.environ.pop("MCPT_BVH_WIDTH", None)
+        else:
+            os.environ["MCPT_BVH_WIDTH"] = old
+    n = 20000 if which == "scene_c3" else 100000
+    ro, rd = random_rays(n, 41, box=2.5)
+    if which == "scene_c3":
+        ro[:, 1] += 1.0
+    ro[:4] = [[0, 0, 5], [0, 0, 5], [0, 0, 5], [0, 0, 1]]
+    rd[:4] = [[np.nan, 0, -1], [0, 0, 0], [0, 0, -1], [1, 0, 0]]
+    gp, gn, gt = pt.trace_closest(ro, rd)
+    op_, on, ot = oracle.trace_closest(a, ro, rd)
+    assert np.array_equal(gt, ot)
+    assert np.array_equal(gp.view(np.uint32), op_.view(np.uint32))
+    assert np.array_equal(gn.view(np.uint32), on.view(np.uint32))
+    assert np.array_equal(pt.trace_any(ro, rd), oracle.trace_any(a, ro, rd))
+    if which == "scene_c2":  # a film through the 4-wide traversal
+        rc = mcpt_mod.CONFIGS[2]
+        W, H = 160, 90
+        cam = mcpt_mod.config_camera(rc, W, H)
+        pt.close()
+        os.environ["MCPT_BVH_WIDTH"] = "4"
+        try:
+            pt = make_pt(mcpt_mod, s, cam, W, H, 3, rc.max_depth)
+        finally:
+            if old is None:
+                os.environ.pop("MCPT_BVH_WIDTH", None)
+            else:
+                os.environ["MCPT_BVH_WIDTH"] = old
+        pt.render()
+        Ld, smp = pt.film()
+        rL, rs, _ = oracle.render(a, cam, W, H, 3, rc.max_depth)
+        assert np.array_equal(smp, rs)
+        assert np.array_equal(Ld.view(np.uint32), rL.view(np.uint32))
+    pt.close()
