@@ -1416,6 +1416,10 @@ int launch_geometry(int dev, LaunchGeom& g) {
     // returning atomics (config 2 k_trace 0.82 ms at 8 partitions, 0.767 at 16, 0.766 at
     // 32, 0.779 at 64; interleaved runs on one box)
     g.trace_parts = env_u32("MCPT_TRACE_PARTS", std::min(kMaxParts, 2 * std::max(1, nx)), 1, kMaxParts);
+    if (const char* e = getenv("MCPT_MAT_BLOCKS_PER_CU")) {  // diagnostics: a smaller persistent grid
+        const int m = atoi(e);                               // (4 -> 3 / 2 blocks: shade stage +5 % / +18 %)
+        if (m > 0) { mat0 = std::min(mat0, m); mat1 = std::min(mat1, m); }
+    }
     g.mat_blocks[0] = (uint32_t)std::max(1, cus * std::max(1, mat0) / kShards) * (uint32_t)kShards;
     g.mat_blocks[1] = (uint32_t)std::max(1, cus * std::max(1, mat1) / kShards) * (uint32_t)kShards;
     g.refill_min = env_u32("MCPT_REFILL_MIN", 16, 1, 64);
