@@ -62,6 +62,10 @@ struct mcpt_ctx {
     size_t queue_alloc = 0;             // entries allocated for ext_q (any_q holds twice)
     CounterBlock* cnt = nullptr;
     CounterBlock* cnt_host = nullptr;  // pinned
+    CounterBlock totals{};             // host copy of the counters after the last call (valid: totals_ok)
+    bool totals_ok = false;
+    int2* step_tile = nullptr;         // mcpt_wavefront_step's one-tile set: device + pinned staging
+    int2* step_tile_h = nullptr;
     int2* tiles = nullptr;
     std::vector<int2> tiles_h;
     uint32_t tiles_cap = 0;
@@ -159,6 +163,8 @@ void mcpt_destroy(mcpt_ctx* c) {
     if (c->cnt) (void)hipFree(c->cnt);
     if (c->cnt_host) (void)hipHostFree(c->cnt_host);
     if (c->tiles) (void)hipFree(c->tiles);
+    if (c->step_tile) (void)hipFree(c->step_tile);
+    if (c->step_tile_h) (void)hipHostFree(c->step_tile_h);
     if (c->ext_q) (void)hipFree(c->ext_q);
     if (c->any_q) (void)hipFree(c->any_q);
     if (c->mat_q) (void)hipFree(c->mat_q);
@@ -626,6 +632,8 @@ int mcpt_film_clear(mcpt_ctx* c) {
     c->film_stale = false;
     HIPCHK(c, hipMemsetAsync(c->cnt, 0, sizeof(CounterBlock), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    memset(&c->totals, 0, sizeof(c->totals));  // the counters are now zero on the device too
+    c->totals_ok = true;
     return MCPT_OK;
 }
 
@@ -700,13 +708,13 @@ static int check_ready(mcpt_ctx* c) {
 }
 
 // One wavefront iteration over the current tile set: shade -> extend -> any-hit.
-static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
+static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2* tiles, int ntiles) {
     ShadeArgs sa;
     sa.scene = c->scene;
     sa.cam = c->cam;
     sa.p = c->p;
-    sa.tiles = c->tiles;
-    sa.ntiles = (int)c->tiles_h.size();
+    sa.tiles = tiles;
+    sa.ntiles = ntiles;
     sa.tile_w = (int)c->tile_w;
     sa.tile_h = (int)c->tile_h;
     sa.W = (int)c->W;
@@ -758,22 +766,39 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing) {
     return MCPT_OK;
 }
 
-static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st) {
+// n iterations over a tile set (the context's, or one tile for mcpt_wavefront_step).  One
+// host synchronisation per call: the counter totals before the call are the host copy the
+// previous call (or the film clear) left.
+static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st, const int2* tiles = nullptr, int ntiles = -1) {
     int rc = check_ready(c);
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     if (c->film_stale && !(c->cfg.flags & MCPT_FLAG_NO_AUTO_CLEAR) && (rc = mcpt_film_clear(c))) return rc;
-    HIPCHK(c, hipMemcpyAsync(c->cnt_host, c->cnt, sizeof(CounterBlock), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    CounterBlock before = *c->cnt_host;
+    if (!tiles) {
+        tiles = c->tiles;
+        ntiles = (int)c->tiles_h.size();
+    }
+    if (!c->totals_ok) {
+        HIPCHK(c, hipMemcpyAsync(c->cnt_host, c->cnt, sizeof(CounterBlock), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->totals = *c->cnt_host;
+        c->totals_ok = true;
+    }
+    const CounterBlock before = c->totals;
     for (uint32_t i = 0; i < n; i++) {
         // events for at most the first 4096 iterations of a call
         bool timing = i < 4096;
-        if ((rc = enqueue_iteration(c, (size_t)3 * i, timing))) return rc;
+        if ((rc = enqueue_iteration(c, (size_t)3 * i, timing, tiles, ntiles))) {
+            c->totals_ok = false;
+            return rc;
+        }
     }
+    c->totals_ok = false;
     HIPCHK(c, hipMemcpyAsync(c->cnt_host, c->cnt, sizeof(CounterBlock), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const CounterBlock& after = *c->cnt_host;
+    c->totals = *c->cnt_host;
+    c->totals_ok = true;
+    const CounterBlock& after = c->totals;
     if (after.trace_short != before.trace_short)  // k_accumulate's drain check (never expected)
         return set_err(c, MCPT_E_HIP, "k_trace left queued rays untraced in " +
                                           std::to_string(after.trace_short - before.trace_short) + " launch(es)");
@@ -810,6 +835,21 @@ int mcpt_wavefront_step(mcpt_ctx* c, uint32_t tx, uint32_t ty, mcpt_stage_stats*
     if (rc) return rc;
     uint32_t nx = (c->W + c->tile_w - 1) / c->tile_w, ny = (c->H + c->tile_h - 1) / c->tile_h;
     if (tx >= nx || ty >= ny) return set_err(c, MCPT_E_INVALID, "tile out of range");
+    // The one-tile set goes through its own small buffer (pinned staging, stream-ordered
+    // copy): the context's tile set and queues stay as they are when their per-shard queue
+    // capacity covers one tile, which it does unless the tile set is empty.
+    const uint32_t bpt = (c->tile_w * c->tile_h + kBlock - 1) / kBlock;
+    const uint32_t need = std::max<uint32_t>(1, (bpt * c->slots + kShards - 1) / kShards) * kBlock;
+    if (c->ext_cap >= need) {
+        if (!c->step_tile) {
+            HIPCHK(c, hipSetDevice(c->device));
+            HIPCHK(c, hipMalloc(&c->step_tile, sizeof(int2)));
+            HIPCHK(c, hipHostMalloc(&c->step_tile_h, sizeof(int2)));
+        }
+        *c->step_tile_h = make_int2((int)tx, (int)ty);  // the previous call's copy has completed
+        HIPCHK(c, hipMemcpyAsync(c->step_tile, c->step_tile_h, sizeof(int2), hipMemcpyHostToDevice, c->stream));
+        return run_iterations(c, 1, st, c->step_tile, 1);
+    }
     std::vector<int2> saved = c->tiles_h;
     if ((rc = set_tiles_internal(c, {make_int2((int)tx, (int)ty)}))) return rc;
     rc = run_iterations(c, 1, st);
