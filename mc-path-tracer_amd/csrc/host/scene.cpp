@@ -8,13 +8,17 @@
 //   Scene::transfer_data_to_device CUDA-RayTracer/Scene.cu:363-470        -> flat SoA arrays (mcpt_scene_desc)
 // Everything here is setup; the per-bounce hot path lives in kernels.hip.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <functional>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../device/mcpt_core.hpp"
@@ -579,10 +583,11 @@ struct Builder {
     double ct = 1.0, ci = 1.0;
     Builder(std::vector<PrimInfo>& i, int mp) : info(i), max_prims(mp) {}
 
+    // Leaves are created left to right over disjoint ranges, so the final orderedPrims is
+    // info's prim order and a leaf's first triangle is its range start.
     int leaf(int start, int end, const Bounds& b) {
         BuildNode n;
-        n.b = b; n.first = (int)ordered.size(); n.n = end - start;
-        for (int i = start; i < end; i++) ordered.push_back(info[i].prim);
+        n.b = b; n.first = start; n.n = end - start;
         nodes.push_back(n);
         return (int)nodes.size() - 1;
     }
@@ -607,11 +612,15 @@ struct Builder {
         nodes[me].n = 0;
         return me;
     }
-    int build_sah3(int start, int end, int depth) {
+    // The split decision for info[start, end), partitioning the range in place: a leaf, or
+    // the split position and axis.  Depends on the range's contents alone, so subtrees can
+    // be built concurrently with the same result (build_parallel).
+    struct Split { bool leaf; int mid, dim; Bounds b; };
+    Split decide_sah3(int start, int end) {
         Bounds b;
         for (int i = start; i < end; i++) b.add(info[i].b);
         const int np = end - start;
-        if (np == 1) return leaf(start, end, b);
+        if (np == 1) return {true, 0, 0, b};
         Bounds cb;
         for (int i = start; i < end; i++) cb.add(info[i].c);
         const double A = b.area();
@@ -652,11 +661,11 @@ struct Builder {
             }
         }
         if (bdim < 0) {  // all centroids coincide (or one bin): leaf, or an index split to bound leaf size
-            if (np <= max_prims) return leaf(start, end, b);
+            if (np <= max_prims) return {true, 0, 0, b};
             const int dim = b.max_extent();
-            return inner(start, median_split(start, end, dim), end, depth, dim);
+            return {false, median_split(start, end, dim), dim, b};
         }
-        if (np <= max_prims && ci * np <= best) return leaf(start, end, b);
+        if (np <= max_prims && ci * np <= best) return {true, 0, 0, b};
         const float lo = comp(cb.mn, bdim), hi = comp(cb.mx, bdim);
         const double scale = (double)nb / ((double)hi - (double)lo);
         auto it = std::partition(info.begin() + start, info.begin() + end, [&](const PrimInfo& p) {
@@ -666,22 +675,21 @@ struct Builder {
         });
         int mid = (int)(it - info.begin());
         if (mid == start || mid == end) mid = median_split(start, end, bdim);
-        return inner(start, mid, end, depth, bdim);
+        return {false, mid, bdim, b};
     }
-    int build(int start, int end, int depth) {
-        max_depth = std::max(max_depth, depth);
-        if (mode == 1) return build_sah3(start, end, depth);
+    Split decide(int start, int end) {
+        if (mode == 1) return decide_sah3(start, end);
         Bounds b;
         for (int i = start; i < end; i++) b.add(info[i].b);
         int np = end - start;
-        if (np == 1) return leaf(start, end, b);
+        if (np == 1) return {true, 0, 0, b};
         Bounds cb;
         for (int i = start; i < end; i++) cb.add(info[i].c);
         int dim = cb.max_extent();
         int mid = (start + end) / 2;
         float cmin = comp(cb.mn, dim), cmax = comp(cb.mx, dim);
         if (cmax == cmin) {
-            if (np <= max_prims) return leaf(start, end, b);
+            if (np <= max_prims) return {true, 0, 0, b};
             mid = (start + end) / 2;  // deviation: index split keeps leaves small
         } else if (np <= 2) {
             std::nth_element(info.begin() + start, info.begin() + mid, info.begin() + end,
@@ -722,20 +730,82 @@ struct Builder {
                                      [dim](const PrimInfo& a, const PrimInfo& c) { return comp(a.c, dim) < comp(c.c, dim); });
                 }
             } else {
-                return leaf(start, end, b);
+                return {true, 0, 0, b};
             }
         }
-        int me = (int)nodes.size();
-        nodes.push_back(BuildNode());
-        int c0 = build(start, mid, depth + 1);
-        int c1 = build(mid, end, depth + 1);
-        nodes[me].child[0] = c0;
-        nodes[me].child[1] = c1;
-        nodes[me].axis = dim;
-        nodes[me].b = nodes[c0].b;
-        nodes[me].b.add(nodes[c1].b);
-        nodes[me].n = 0;
-        return me;
+        return {false, mid, dim, b};
+    }
+    int build(int start, int end, int depth) {
+        max_depth = std::max(max_depth, depth);
+        const Split sp = decide(start, end);
+        if (sp.leaf) return leaf(start, end, sp.b);
+        return inner(start, sp.mid, end, depth, sp.dim);
+    }
+    // Same tree as build(0, T, 0), with the subtrees below a cut built by worker threads:
+    // the top of the tree is split here; ranges of at most `grain` triangles become tasks,
+    // each a Builder of its own over its disjoint range of info (every decision depends on
+    // the range alone, so the tree -- and the flattened arrays -- are identical).  Task
+    // nodes are appended afterwards and the cut's child links re-pointed.
+    int build_parallel(int T, int nthreads) {
+        struct Task { int start, end, depth, parent, slot; Builder* b; int root; };
+        std::vector<Task> tasks;
+        const int grain = std::max(4096, T / (8 * nthreads));
+        std::function<int(int, int, int, int, int)> top = [&](int start, int end, int depth, int parent, int slot) -> int {
+            max_depth = std::max(max_depth, depth);
+            if (end - start <= grain) {
+                tasks.push_back({start, end, depth, parent, slot, nullptr, -1});
+                return -1;  // filled in after the tasks ran
+            }
+            const Split sp = decide(start, end);
+            if (sp.leaf) return leaf(start, end, sp.b);
+            const int me = (int)nodes.size();
+            nodes.push_back(BuildNode());
+            const int c0 = top(start, sp.mid, depth + 1, me, 0);
+            const int c1 = top(sp.mid, end, depth + 1, me, 1);
+            nodes[me].child[0] = c0;
+            nodes[me].child[1] = c1;
+            nodes[me].axis = sp.dim;
+            nodes[me].n = 0;
+            return me;
+        };
+        const int root = top(0, T, 0, -1, 0);
+        std::vector<std::unique_ptr<Builder>> owned;
+        for (Task& t : tasks) {
+            owned.emplace_back(new Builder(info, max_prims));
+            t.b = owned.back().get();
+            t.b->mode = mode; t.b->nb = nb; t.b->ct = ct; t.b->ci = ci;
+        }
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+            for (size_t k; (k = next.fetch_add(1)) < tasks.size();)
+                tasks[k].root = tasks[k].b->build(tasks[k].start, tasks[k].end, tasks[k].depth);
+        };
+        std::vector<std::thread> pool;
+        for (int i = 1; i < nthreads; i++) pool.emplace_back(work);
+        work();
+        for (auto& th : pool) th.join();
+        const int cut_end = (int)nodes.size();
+        int rootref = root;
+        for (Task& t : tasks) {
+            const int off = (int)nodes.size();
+            for (BuildNode n : t.b->nodes) {
+                if (n.n == 0) { n.child[0] += off; n.child[1] += off; }
+                nodes.push_back(n);
+            }
+            max_depth = std::max(max_depth, t.b->max_depth);
+            if (t.parent < 0) rootref = t.root + off;
+            else nodes[t.parent].child[t.slot] = t.root + off;
+        }
+        // boxes of the interior nodes above the cut, bottom-up
+        std::function<void(int)> fix = [&](int i) {
+            if (i >= cut_end || nodes[i].n > 0) return;
+            fix(nodes[i].child[0]);
+            fix(nodes[i].child[1]);
+            nodes[i].b = nodes[nodes[i].child[0]].b;
+            nodes[i].b.add(nodes[nodes[i].child[1]].b);
+        };
+        fix(rootref);
+        return rootref;
     }
 };
 
@@ -771,7 +841,10 @@ int Scene::build(const mcpt_bvh_params& prm, std::string& err) {
     node_bmin.clear(); node_bmax.clear(); node_offset.clear(); node_nprims.clear(); node_axis.clear();
     bvh_depth = 0;
     if (T > 0) {
-        int root = bld.build(0, (int)T, 0);
+        // MCPT_BVH_THREADS: worker threads for the subtrees (default min(16, cores); 1 = sequential)
+        int nth = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+        if (const char* e = std::getenv("MCPT_BVH_THREADS")) nth = std::max(1, std::atoi(e));
+        int root = (T >= 65536 && nth > 1) ? bld.build_parallel((int)T, nth) : bld.build(0, (int)T, 0);
         bvh_depth = bld.max_depth;
         // flatten_tree (BVH.cu:312-333): depth-first, first child adjacent.
         std::function<int(int)> flatten = [&](int ni) -> int {
@@ -793,6 +866,8 @@ int Scene::build(const mcpt_bvh_params& prm, std::string& err) {
         flatten(root);
     }
     // gather triangles in orderedPrims order (Scene.cu:459-469)
+    bld.ordered.resize(T);
+    for (size_t i = 0; i < T; i++) bld.ordered[i] = info[i].prim;  // orderedPrims (leaf ranges in order)
     size_t N = T;
     f_v0.resize(3 * N); f_v1.resize(3 * N); f_v2.resize(3 * N);
     f_n0.resize(3 * N); f_n1.resize(3 * N); f_n2.resize(3 * N);
