@@ -7,7 +7,7 @@ PKG     := mc-path-tracer_amd
 BUILD   := $(PKG)/build
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
             -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -Iinclude -I$(PKG)/csrc
-SRCS := $(PKG)/csrc/kernels.hip $(PKG)/csrc/bvh_build.hip $(PKG)/csrc/runtime.cpp \
+SRCS := $(PKG)/csrc/kernels.hip $(PKG)/csrc/bvh_build.hip $(PKG)/csrc/env_build.hip $(PKG)/csrc/runtime.cpp \
         $(PKG)/csrc/host/scene.cpp $(PKG)/csrc/host/proxies.cpp $(PKG)/csrc/host/capi_host.cpp \
         $(PKG)/csrc/host/image_io.cpp
 OBJS := $(patsubst $(PKG)/csrc/%,$(BUILD)/%.o,$(SRCS))

@@ -197,6 +197,12 @@ int mcpt_device_name(mcpt_ctx *ctx, char *buf, int32_t len);
 int mcpt_debug_queue_rays(mcpt_ctx *ctx, int which, float *ray_o, float *ray_d, uint32_t *n_inout);
 float mcpt_debug_last_stage_ms(const mcpt_ctx *ctx);
 float mcpt_debug_last_build_ms(const mcpt_ctx *ctx);  /* device time of the last GPU BVH build */
+/* HRDI tables: an upload whose desc has env_tex but no env_marginal_y / env_conds_y / env_pdf builds
+ * them on the device (build_environment_light, light_initialization_kernels.cu:3-161; bit-identical to
+ * the host build).  Device time of the last such build, and a copy of the uploaded scene's device
+ * tables (any output may be NULL; *flags bit 0 = built on the device, bit 1 = env_cell search guides on). */
+float mcpt_debug_last_env_build_ms(const mcpt_ctx *ctx);
+int mcpt_debug_env_tables(mcpt_ctx *ctx, float *marginal_y, float *conds_y, float *pdf, int32_t *flags);
 /* pair-node numbering of the last uploaded tree: 0 depth-first, 1 depth-first by sibling pairs,
  * 2 breadth-first (default 2 for trees of <= 2 MiB of nodes, else 0; MCPT_SIBLING_LAYOUT=0/1/2
  * at upload forces one; inputs that are not a tree -- a shared child -- always get 0). */
@@ -220,6 +226,10 @@ int mcpt_scene_load_glb(mcpt_scene *s, const char *path, const float *xform16); 
 int mcpt_scene_add_mesh(mcpt_scene *s, int32_t ntri, const float *v0, const float *v1, const float *v2,
                         const float *n0, const float *n1, const float *n2, const float *base_rgb);
 int mcpt_scene_set_env_hdr(mcpt_scene *s, const char *path, int32_t mode);
+/* flags MCPT_ENV_DEVICE_TABLES: keep the texture only; mcpt_scene_upload then builds the tables on
+ * the device (for large maps: the host build is several serial passes over every texel). */
+#define MCPT_ENV_DEVICE_TABLES 1
+int mcpt_scene_set_env_hdr_ex(mcpt_scene *s, const char *path, int32_t mode, uint32_t flags);
 int mcpt_scene_set_env_color(mcpt_scene *s, const float *rgb, float ls);
 int mcpt_scene_add_dir_light(mcpt_scene *s, const float *dir, const float *rgb, float ls);
 int mcpt_scene_transform(mcpt_scene *s, const float *xform16);   /* bake a transform into all meshes */

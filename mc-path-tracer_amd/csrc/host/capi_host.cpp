@@ -59,6 +59,14 @@ int mcpt_scene_set_env_hdr(mcpt_scene* s, const char* path, int32_t mode) {
     return rc ? fail(s, rc, err) : MCPT_OK;
 }
 
+int mcpt_scene_set_env_hdr_ex(mcpt_scene* s, const char* path, int32_t mode, uint32_t flags) {
+    if (!s || !path || (mode != 0 && mode != 1) || (flags & ~(uint32_t)MCPT_ENV_DEVICE_TABLES))
+        return fail(s, MCPT_E_INVALID, "bad env arguments");
+    std::string err;
+    int rc = s->s.set_env_hdr(path, mode, err, !(flags & MCPT_ENV_DEVICE_TABLES));
+    return rc ? fail(s, rc, err) : MCPT_OK;
+}
+
 int mcpt_scene_set_env_color(mcpt_scene* s, const float* rgb, float ls) {
     if (!s || !rgb) return fail(s, MCPT_E_INVALID, "null argument");
     for (int i = 0; i < 3; i++) s->s.env_color[i] = rgb[i];

@@ -42,7 +42,7 @@ struct Scene {
                   const std::vector<uint32_t>& idx, mcpt::V3 base);
     void transform(const float* xf16);
     int load_glb(const char* path, const float* xf16, std::string& err);
-    int set_env_hdr(const char* path, int mode, std::string& err);
+    int set_env_hdr(const char* path, int mode, std::string& err, bool host_tables = true);
     int build(int max_prims, std::string& err);
     int build(const mcpt_bvh_params& p, std::string& err);
     void desc(mcpt_scene_desc* d) const;

@@ -518,7 +518,7 @@ void build_env_tables(int W, int H, const std::vector<float>& tex, std::vector<f
     denom_out = denom;
 }
 
-int Scene::set_env_hdr(const char* path, int mode, std::string& err) {
+int Scene::set_env_hdr(const char* path, int mode, std::string& err, bool host_tables) {
     int W = 0, H = 0;
     std::vector<float> tex;
     int rc = load_hdr(path, W, H, tex, err);
@@ -527,6 +527,11 @@ int Scene::set_env_hdr(const char* path, int mode, std::string& err) {
     env_h = H;
     env_tex.swap(tex);
     env_mode = mode;
+    if (!host_tables) {  // built on the device at upload (env_build.hip)
+        env_marginal_y.clear(); env_marginal_p.clear(); env_conds_y.clear(); env_pdf.clear();
+        env_pdf_denom = 0.f;
+        return MCPT_OK;
+    }
     float denom;
     build_env_tables(W, H, env_tex, env_marginal_y, env_marginal_p, env_conds_y, env_pdf, denom);
     env_pdf_denom = denom;

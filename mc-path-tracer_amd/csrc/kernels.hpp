@@ -157,6 +157,14 @@ void launch_shade(const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fix
 void launch_trace(const TraceArgs& a, const LaunchGeom& g, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
 void launch_env_table(const mcpt::EnvView& e, bool fixed_mode, float4* out, hipStream_t s);
+// HRDI tables on the device (env_build.hip), bit-identical to the host build: scratch holds
+// env_build_scratch_floats(W, H) floats; W * H < 2^31.
+size_t env_build_scratch_floats(int W, int H);
+void launch_env_build(const float4* tex, int W, int H, float* scratch, float* marginal_y, float* conds_y,
+                      float* pdf, hipStream_t s);
+// CDF check (*bad |= 1 unless the guides are valid) + the env_cell search guides
+void launch_env_guides(const float* marginal_y, const float* conds_y, int W, int H, uint16_t* gm, uint16_t* gc,
+                       uint32_t* bad, hipStream_t s);
 
 // GPU linear BVH (bvh_build.hip).  Inputs: host vertex arrays (3 floats per
 // triangle each) and the device triangle / shading records in scene order.

@@ -74,6 +74,9 @@ struct mcpt_ctx {
     std::vector<void*> tmp_bufs;
     float last_stage_ms = 0.f;
     float last_build_ms = 0.f;  // last GPU BVH build (mcpt_scene_upload_gpu_bvh)
+    float last_env_build_ms = 0.f;  // last device build of the HRDI tables (env_build.hip)
+    bool env_device_built = false;  // the uploaded scene's HRDI tables were built on the device
+    bool env_guides = false;        // env_cell uses the search guides
     int gpu_bvh_builder = MCPT_GPU_BVH_PLOC;  // mcpt_set_gpu_bvh_builder
 };
 
@@ -256,8 +259,13 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     if (d->ntri > 0 && d->nnodes == 0 && !gpu_bvh) return set_err(c, MCPT_E_INVALID, "triangles without BVH");
     for (int32_t i = 0; i < d->ntri; i++)
         if (d->mat[i] < 0 || d->mat[i] >= d->nmat) return set_err(c, MCPT_E_INVALID, "material id out of range");
-    if (d->env_mode == 1 && (!d->env_tex || !d->env_marginal_y || !d->env_conds_y || !d->env_pdf || d->env_w < 2 || d->env_h < 2))
-        return set_err(c, MCPT_E_INVALID, "HRDI env light without tables");
+    if (d->env_mode == 1) {
+        // tables: all three given (host build), or none (built on the device from env_tex)
+        const int given = !!d->env_marginal_y + !!d->env_conds_y + !!d->env_pdf;
+        if (!d->env_tex || d->env_w < 2 || d->env_h < 2 || (given != 0 && given != 3))
+            return set_err(c, MCPT_E_INVALID, "HRDI env light without texture or with partial tables");
+        if ((int64_t)d->env_w * d->env_h >= ((int64_t)1 << 31)) return set_err(c, MCPT_E_INVALID, "env map too large");
+    }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     free_list(c->scene_bufs);
@@ -507,37 +515,62 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     if (d->env_mode == 1) {
         float4* tx;
         float *my, *cy, *pd;
-        size_t WH = (size_t)d->env_w * d->env_h;
+        const int W = d->env_w, H = d->env_h;
+        size_t WH = (size_t)W * H;
         if ((rc = dupload(c, c->scene_bufs, &tx, reinterpret_cast<const float4*>(d->env_tex), WH))) return rc;
-        if ((rc = dupload(c, c->scene_bufs, &my, d->env_marginal_y, (size_t)d->env_h))) return rc;
-        if ((rc = dupload(c, c->scene_bufs, &cy, d->env_conds_y, WH))) return rc;
-        if ((rc = dupload(c, c->scene_bufs, &pd, d->env_pdf, WH))) return rc;
+        c->env_device_built = !d->env_marginal_y;
+        if (!c->env_device_built) {
+            if ((rc = dupload(c, c->scene_bufs, &my, d->env_marginal_y, (size_t)H))) return rc;
+            if ((rc = dupload(c, c->scene_bufs, &cy, d->env_conds_y, WH))) return rc;
+            if ((rc = dupload(c, c->scene_bufs, &pd, d->env_pdf, WH))) return rc;
+        } else {
+            // build_environment_light (light_initialization_kernels.cu:134-161) on the device
+            if ((rc = dalloc(c, c->scene_bufs, &my, (size_t)H)) || (rc = dalloc(c, c->scene_bufs, &cy, WH)) ||
+                (rc = dalloc(c, c->scene_bufs, &pd, WH)))
+                return rc;
+            float* scratch = nullptr;
+            hipError_t e = hipMalloc(&scratch, mcpt_dev::env_build_scratch_floats(W, H) * sizeof(float));
+            if (e != hipSuccess) return set_err(c, MCPT_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+            HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
+            mcpt_dev::launch_env_build(tx, W, H, scratch, my, cy, pd, c->stream);
+            HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
+            e = hipGetLastError();
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            (void)hipFree(scratch);
+            if (e != hipSuccess) return set_err(c, MCPT_E_HIP, std::string("env build: ") + hipGetErrorString(e));
+            float ms = 0.f;
+            HIPCHK(c, hipEventElapsedTime(&ms, ev(c, 0), ev(c, 1)));
+            c->last_env_build_ms = ms;
+        }
         s.env.tex = tx; s.env.marginal_y = my; s.env.conds_y = cy; s.env.pdf = pd;
-        // search guides for env_dir (only valid on sorted, NaN-free CDFs, which prefix sums
-        // of non-negative luminance are; otherwise the plain bisection is used)
-        auto sorted = [](const float* a, int n) {
-            for (int i = 0; i < n; i++)
-                if (!(a[i] == a[i]) || (i > 0 && a[i] < a[i - 1])) return false;
-            return true;
-        };
-        bool ok = sorted(d->env_marginal_y, d->env_h);
-        for (int y = 0; ok && y < d->env_h; y++) ok = sorted(d->env_conds_y + (size_t)y * d->env_w, d->env_w);
+        // search guides for env_cell, on the device for either source of tables: valid on
+        // a sorted, NaN-free marginal CDF and conditional rows that are sorted and NaN-free
+        // or NaN throughout (upper_bound returns 0 on such a row for every value, and so
+        // does the guided search with its all-zero guide).  Every HRDI map has one: row 0's
+        // sin(0) = 0 makes it 0 / (denom * 0) (light_initialization_kernels.cu:72).
+        // Otherwise the plain bisection is used.
         s.env.guide_m = s.env.guide_c = nullptr;
-        if (ok && d->env_w <= 65535 && d->env_h <= 65535) {
-            const int G = mcpt::kEnvGuide;
-            std::vector<uint16_t> gm(G + 1), gc((size_t)d->env_h * (G + 1));
-            for (int k = 0; k <= G; k++) {
-                const float val = (float)k / (float)G;
-                gm[k] = (uint16_t)mcpt::upper_bound(d->env_marginal_y, d->env_h, val);
-                for (int y = 0; y < d->env_h; y++)
-                    gc[(size_t)y * (G + 1) + k] =
-                        (uint16_t)mcpt::upper_bound(d->env_conds_y + (size_t)y * d->env_w, d->env_w, val);
-            }
+        c->env_guides = false;
+        if (W <= 65535 && H <= 65535) {
+            const size_t G1 = mcpt::kEnvGuide + 1;
             uint16_t *dgm, *dgc;
-            if ((rc = dupload(c, c->scene_bufs, &dgm, gm.data(), gm.size()))) return rc;
-            if ((rc = dupload(c, c->scene_bufs, &dgc, gc.data(), gc.size()))) return rc;
-            s.env.guide_m = dgm;
-            s.env.guide_c = dgc;
+            uint32_t* dbad;
+            if ((rc = dalloc(c, c->scene_bufs, &dgm, G1)) || (rc = dalloc(c, c->scene_bufs, &dgc, (size_t)H * G1)) ||
+                (rc = dalloc(c, c->scene_bufs, &dbad, 1)))
+                return rc;
+            HIPCHK(c, hipMemsetAsync(dbad, 0, sizeof(uint32_t), c->stream));
+            mcpt_dev::launch_env_guides(my, cy, W, H, dgm, dgc, dbad, c->stream);
+            HIPCHK(c, hipGetLastError());
+            uint32_t bad = 1;
+            HIPCHK(c, hipMemcpyAsync(&bad, dbad, sizeof(bad), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            bool ok = bad == 0;
+            if (const char* g = std::getenv("MCPT_ENV_GUIDES")) ok = ok && g[0] != '0';  // 0: plain bisection (A/B, tests)
+            if (ok) {
+                s.env.guide_m = dgm;
+                s.env.guide_c = dgc;
+                c->env_guides = true;
+            }
         }
         // light-sample tables, reference and quality mode (k_env_table)
         if ((size_t)(d->env_w + 1) * d->env_h < ((size_t)1 << 28)) {
@@ -569,6 +602,21 @@ int mcpt_set_gpu_bvh_builder(mcpt_ctx* c, int32_t builder) {
     return MCPT_OK;
 }
 float mcpt_debug_last_build_ms(const mcpt_ctx* c) { return c ? c->last_build_ms : -1.f; }
+float mcpt_debug_last_env_build_ms(const mcpt_ctx* c) { return c ? c->last_env_build_ms : -1.f; }
+
+int mcpt_debug_env_tables(mcpt_ctx* c, float* marginal_y, float* conds_y, float* pdf, int32_t* flags) {
+    if (!c) return set_err(c, MCPT_E_INVALID, "null context");
+    if (!c->has_scene || c->scene.env.mode != 1 || !c->scene.env.tex) return set_err(c, MCPT_E_INVALID, "no HRDI scene uploaded");
+    const mcpt::EnvView& e = c->scene.env;
+    const size_t WH = (size_t)e.w * e.h;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (marginal_y) HIPCHK(c, hipMemcpy(marginal_y, e.marginal_y, (size_t)e.h * sizeof(float), hipMemcpyDeviceToHost));
+    if (conds_y) HIPCHK(c, hipMemcpy(conds_y, e.conds_y, WH * sizeof(float), hipMemcpyDeviceToHost));
+    if (pdf) HIPCHK(c, hipMemcpy(pdf, e.pdf, WH * sizeof(float), hipMemcpyDeviceToHost));
+    if (flags) *flags = (c->env_device_built ? 1 : 0) | (c->env_guides ? 2 : 0);
+    return MCPT_OK;
+}
 int mcpt_debug_node_layout(const mcpt_ctx* c) { return c ? c->node_layout : MCPT_E_INVALID; }
 
 int mcpt_camera_set(mcpt_ctx* c, const mcpt_camera* cam) {

@@ -105,6 +105,8 @@ ABI = {
     "mcpt_debug_queue_rays": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _u]),
     "mcpt_debug_last_stage_ms": (C.c_float, [C.c_void_p]),
     "mcpt_debug_last_build_ms": (C.c_float, [C.c_void_p]),
+    "mcpt_debug_last_env_build_ms": (C.c_float, [C.c_void_p]),
+    "mcpt_debug_env_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _i]),
     "mcpt_debug_node_layout": (C.c_int, [C.c_void_p]),
     "mcpt_scene_upload_gpu_bvh": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mcpt_set_gpu_bvh_builder": (C.c_int, [C.c_void_p, C.c_int32]),
@@ -122,6 +124,7 @@ ABI = {
     "mcpt_scene_load_glb": (C.c_int, [C.c_void_p, C.c_char_p, _f]),
     "mcpt_scene_add_mesh": (C.c_int, [C.c_void_p, C.c_int32, _f, _f, _f, _f, _f, _f, _f]),
     "mcpt_scene_set_env_hdr": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
+    "mcpt_scene_set_env_hdr_ex": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32, C.c_uint32]),
     "mcpt_scene_set_env_color": (C.c_int, [C.c_void_p, _f, C.c_float]),
     "mcpt_scene_add_dir_light": (C.c_int, [C.c_void_p, _f, _f, C.c_float]),
     "mcpt_scene_transform": (C.c_int, [C.c_void_p, _f]),
@@ -176,6 +179,7 @@ class BvhParams(C.Structure):  # mcpt_bvh_params
 BVH_REFERENCE, BVH_SAH3 = 0, 1
 FLAG_FIXED = 1  # MCPT_FLAG_FIXED: quality-mode integrator
 FLAG_NO_AUTO_CLEAR = 2  # MCPT_FLAG_NO_AUTO_CLEAR: camera / scene changes do not clear the film
+ENV_DEVICE_TABLES = 1  # MCPT_ENV_DEVICE_TABLES: HRDI tables built on the device at upload
 
 
 def default_config(spp=16, max_depth=5, rr_depth=3, seed=0x5EED2026, tile=256, fixed=False,
@@ -230,7 +234,11 @@ class Scene:
         bc = np.asarray(base_rgb, np.float32)
         return self._ck(lib().mcpt_scene_add_mesh(self.h, len(arrs[0]), *[fptr(a) for a in arrs], fptr(bc)))
 
-    def set_env_hdr(self, path, mode=1):
+    def set_env_hdr(self, path, mode=1, device_tables=False):
+        """EnvironmentLight from an .hdr.  device_tables=True keeps the texture only; the
+        light tables are then built on the device at upload (MCPT_ENV_DEVICE_TABLES)."""
+        if device_tables:
+            return self._ck(lib().mcpt_scene_set_env_hdr_ex(self.h, str(path).encode(), mode, ENV_DEVICE_TABLES))
         return self._ck(lib().mcpt_scene_set_env_hdr(self.h, str(path).encode(), mode))
 
     def set_env_color(self, rgb, ls=1.0):
@@ -284,8 +292,9 @@ class Scene:
         W, H = d.env_w, d.env_h
         out["env_tex"] = _arr(d.env_tex, 4 * W * H, np.float32).reshape(H, W, 4)
         out["env_marginal_y"] = _arr(d.env_marginal_y, H, np.float32)
-        out["env_conds_y"] = _arr(d.env_conds_y, W * H, np.float32).reshape(H, W)
-        out["env_pdf"] = _arr(d.env_pdf, W * H, np.float32).reshape(H, W)
+        # tables are absent (size 0) when left to the device build (set_env_hdr(device_tables=True))
+        out["env_conds_y"] = _arr(d.env_conds_y, W * H, np.float32).reshape(H, W) if d.env_conds_y else np.zeros(0, np.float32)
+        out["env_pdf"] = _arr(d.env_pdf, W * H, np.float32).reshape(H, W) if d.env_pdf else np.zeros(0, np.float32)
         out["tri_id"] = _arr(d.tri_id, T, np.int32) if d.tri_id else np.arange(T, dtype=np.int32)
         return out
 
@@ -370,6 +379,22 @@ class PathTracer:
     @property
     def last_build_ms(self) -> float:
         return lib().mcpt_debug_last_build_ms(self.h)
+
+    @property
+    def last_env_build_ms(self) -> float:
+        """Device time of the last HRDI table build at upload (tables not in the desc)."""
+        return lib().mcpt_debug_last_env_build_ms(self.h)
+
+    def env_tables(self, W, H) -> dict:
+        """The uploaded scene's device HRDI tables (W x H map) and whether they were built on the
+        device / the env_cell search guides are on."""
+        my = np.zeros(H, np.float32)
+        cy = np.zeros((H, W), np.float32)
+        pdf = np.zeros((H, W), np.float32)
+        fl = C.c_int32(0)
+        self._ck(lib().mcpt_debug_env_tables(self.h, fptr(my), fptr(cy), fptr(pdf), C.byref(fl)))
+        return {"marginal_y": my, "conds_y": cy, "pdf": pdf, "device_built": bool(fl.value & 1),
+                "guides": bool(fl.value & 2)}
 
     def set_camera(self, cam: Camera):
         self._ck(lib().mcpt_camera_set(self.h, C.byref(cam)))

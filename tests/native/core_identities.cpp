@@ -65,6 +65,18 @@ int main() {
                 std::printf("upper_bound_guided n=%d val=%a\n", n, val);
         }
     }
+    // ... and on a row that is NaN throughout (row 0 of every HRDI map: 0 / (denom * 0))
+    for (int n : {1, 2, 7, 512}) {
+        std::vector<float> a(n, std::nanf(""));
+        std::vector<int> guide(kEnvGuide + 1);
+        for (int k = 0; k <= kEnvGuide; k++) guide[k] = upper_bound(a.data(), n, (float)k / (float)kEnvGuide);
+        for (int q = 0; q < 20000; q++) {
+            float val = (float)((double)(uint32_t)g() * 0.00000000023283064365386962890625);
+            if ((upper_bound_guided(a.data(), guide.data(), val) != upper_bound(a.data(), n, val) ||
+                 upper_bound(a.data(), n, val) != 0) && bad++ < 5)
+                std::printf("upper_bound_guided NaN row n=%d val=%a\n", n, val);
+        }
+    }
     // fp64 island == fp32 quotient: random significands and exponents, plus all-ones significands
     std::uniform_int_distribution<uint32_t> M(0, 0x7FFFFF);
     std::uniform_int_distribution<int> E(-60, 60);

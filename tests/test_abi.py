@@ -4,6 +4,8 @@ import ctypes as C
 import os
 import re
 
+import numpy as np
+
 from conftest import REPO
 
 
@@ -81,3 +83,22 @@ def test_cpp_example_links_against_the_abi():
                          capture_output=True, text=True, check=True).stdout
     defined = {l.split()[-1] for l in lib.splitlines()}
     assert used and all(u in defined for u in used), [u for u in used if u not in defined]
+
+
+def test_env_hdr_device_tables_flag(mcpt_mod):
+    """mcpt_scene_set_env_hdr_ex(MCPT_ENV_DEVICE_TABLES) keeps the texture and leaves the tables to
+    the upload (built on the device); the plain call builds them on the host; bad flags are codes."""
+    import os
+    hdr = os.path.join(mcpt_mod.ASSET_DIR, "night_free_Env.hdr")
+    out = []
+    for dev in (False, True):
+        s = mcpt_mod.Scene()
+        s.set_env_hdr(hdr, 1, device_tables=dev)
+        s.build()
+        out.append(s.arrays())
+    host, dev = out
+    assert np.array_equal(host["env_tex"], dev["env_tex"]) and host["env_conds_y"].size > 0
+    for k in ("env_marginal_y", "env_conds_y", "env_pdf"):
+        assert dev[k].size == 0
+    rc = mcpt_mod.lib().mcpt_scene_set_env_hdr_ex(mcpt_mod.Scene().h, hdr.encode(), 1, 6)
+    assert rc == -1

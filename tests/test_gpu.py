@@ -806,3 +806,70 @@ def test_quad_nodes_same_hits(request, mcpt_mod, oracle, which, gpu_bvh):
         assert np.array_equal(smp, rs)
         assert np.array_equal(Ld.view(np.uint32), rL.view(np.uint32))
     pt.close()
+
+
+def _nan_equal(x, y):
+    """bitwise, except that NaNs only need to be NaN on both sides (x86's 0/0 is -NaN, gfx950's +NaN;
+    the tables' consumers only compare against them)"""
+    return bool(((x.view(np.uint32) == y.view(np.uint32)) | (np.isnan(x) & np.isnan(y))).all())
+
+
+def _env_only(a, tex):
+    b = dict(a)
+    b["env_tex"] = np.ascontiguousarray(tex, np.float32)
+    for k in ("env_marginal_y", "env_conds_y", "env_pdf"):
+        b[k] = np.zeros(0, np.float32)
+    return b
+
+
+@pytest.mark.parametrize("shape", ["c2", (77, 300), (512, 1024), "zeros", "spike"])
+def test_env_tables_built_on_device_equal_oracle(mcpt_mod, oracle, scene_c2, shape):
+    """build_environment_light (light_initialization_kernels.cu:3-161) on the device: marginal,
+    conditional and pdf tables equal the oracle's or_env_build for the config-2 map and synthetic
+    ones (odd sizes, an all-zero map whose tables are NaN, one dominant texel)."""
+    _, a = scene_c2
+    rng = np.random.default_rng(5)
+    if shape == "c2":
+        tex = a["env_tex"]
+    elif shape == "zeros":
+        tex = np.zeros((64, 128, 4), np.float32)
+    elif shape == "spike":
+        tex = rng.uniform(0, 0.01, (128, 256, 4)).astype(np.float32)
+        tex[40, 17, :3] = 5e4
+    else:
+        tex = (rng.lognormal(0, 2, shape + (4,)) * (rng.uniform(size=shape + (1,)) > 0.2)).astype(np.float32)
+    H, W = tex.shape[:2]
+    pt = mcpt_mod.PathTracer(0)
+    pt.upload_scene(mcpt_mod.desc_from_arrays(_env_only(a, tex)))
+    got = pt.env_tables(W, H)
+    ref = oracle.env_build(tex)
+    assert got["device_built"]
+    for k in ("marginal_y", "conds_y", "pdf"):
+        assert _nan_equal(got[k], ref[k]), k
+    # guides: on for real maps (row 0 is NaN throughout: 0 / (denom * 0)), off for the NaN tables
+    assert got["guides"] == (shape != "zeros")
+    assert pt.last_env_build_ms > 0
+    pt.close()
+
+
+def test_env_device_tables_same_film(mcpt_mod, scene_c2):
+    """Config-2 film with the HRDI tables built on the device equals the host-table film bit for bit
+    (and host tables uploaded as given read back unchanged)."""
+    s, a = scene_c2
+    rc = mcpt_mod.CONFIGS[2]
+    W, H = 160, 90
+    cam = mcpt_mod.config_camera(rc, W, H)
+    films = []
+    for desc in (s, mcpt_mod.desc_from_arrays(_env_only(a, a["env_tex"]))):
+        pt = make_pt(mcpt_mod, desc, cam, W, H, 4, rc.max_depth)
+        t = pt.env_tables(a["env_tex"].shape[1], a["env_tex"].shape[0])
+        assert t["guides"]
+        if desc is s:
+            assert not t["device_built"]
+            for k in ("marginal_y", "conds_y", "pdf"):
+                assert np.array_equal(t[k].view(np.uint32), a["env_" + k].view(np.uint32))
+        pt.render()
+        films.append(pt.film())
+        pt.close()
+    (L0, s0), (L1, s1) = films
+    assert np.array_equal(s0, s1) and np.array_equal(L0.view(np.uint32), L1.view(np.uint32))

@@ -5,7 +5,7 @@ name=$1; shift
 out=/root/repo/mc-path-tracer_amd/build_$name
 mkdir -p $out
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -I/root/repo/include -I/root/repo/mc-path-tracer_amd/csrc $@"
-for f in kernels.hip bvh_build.hip runtime.cpp host/scene.cpp host/proxies.cpp host/capi_host.cpp host/image_io.cpp; do
+for f in kernels.hip bvh_build.hip env_build.hip runtime.cpp host/scene.cpp host/proxies.cpp host/capi_host.cpp host/image_io.cpp; do
   /opt/rocm/bin/hipcc $F -x hip -c /root/repo/mc-path-tracer_amd/csrc/$f -o $out/$(basename $f).o &
 done
 wait
