@@ -707,18 +707,25 @@ constexpr int kGrabMax = MCPT_GRAB_MAX;  // rays one hand-out atomic may reserve
 #endif
 constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
 
-// 7 waves per SIMD (<= 72 VGPRs): the persistent grid's measured optimum (launch_geometry).
-// The attribute lets the register allocator park the partition scan's loop-invariant lane
-// addresses in scratch (two spills, reloaded only by the scan) instead of giving up a wave.
-// The 4-wide instantiation holds 8 float4 of node data per step: 6 waves (80 VGPRs).
+// Waves per SIMD: 8 (<= 64 VGPRs) for child pairs with the 8-entry LDS stack, 7 (<= 72) with
+// the deep stack (the 8-wave build falls back to 6 there), 6 (80) for 4-wide nodes (8 float4
+// of node data per step).  The attribute lets the register allocator park the partition
+// scan's loop-invariant lane addresses (and a few scalars) in scratch -- reloaded only by
+// the scan -- instead of giving up a wave.  Config 2 k_trace 0.777 -> 0.758 ms at 8 waves
+// (32 per CU) against 7 (interleaved runs on one box).
 #ifndef MCPT_TRACE_WPE
-#define MCPT_TRACE_WPE 7
+#define MCPT_TRACE_WPE 8
+#endif
+#ifndef MCPT_TRACE_WPE_DEEP
+#define MCPT_TRACE_WPE_DEEP 7
 #endif
 #ifndef MCPT_TRACE_WPE4
 #define MCPT_TRACE_WPE4 6
 #endif
+#define MCPT_TRACE_WPE_OF(kW, kS) \
+    ((kW) == 4 ? MCPT_TRACE_WPE4 : ((kS) > ::mcpt_dev::kLdsStack ? MCPT_TRACE_WPE_DEEP : MCPT_TRACE_WPE))
 #define MCPT_TRACE_ATTR \
-    __attribute__((amdgpu_waves_per_eu(kW == 4 ? MCPT_TRACE_WPE4 : MCPT_TRACE_WPE, kW == 4 ? MCPT_TRACE_WPE4 : MCPT_TRACE_WPE)))
+    __attribute__((amdgpu_waves_per_eu(MCPT_TRACE_WPE_OF(kW, kLdsStack), MCPT_TRACE_WPE_OF(kW, kLdsStack))))
 #ifdef MCPT_WAVE_TIMES
 __device__ unsigned long long g_wave_t[4 * 16384];  // per wave: s_memrealtime (100 MHz, chip-wide) at entry and
                                                      // exit, partition, time its partition ran dry for it
@@ -1388,10 +1395,11 @@ static uint32_t env_u32(const char* name, int def, int lo, int hi) {
 // the context owns.
 //  * k_material: resident blocks (occupancy calculator x CUs) rounded down to a multiple
 //    of the shard count (at least one block per shard).
-//  * k_trace: resident waves per CU from the occupancy calculator, at most 28 (7 per
-//    SIMD): on config 2 the launch takes 0.406 / 0.368 / 0.354 / 0.329 / 0.382 ms at
-//    16 / 20 / 24 / 28 / 32 waves per CU (more resident rays thrash the per-CU L1 with
-//    unrelated node fetches past 28).  MCPT_TRACE_WAVES overrides the waves per CU.
+//  * k_trace: resident waves per CU from the occupancy calculator (32 for the 64-VGPR
+//    child-pair instantiation, 28 deep-stack, 24 quads).  Round 1 measured 28 best on an
+//    earlier kernel (0.406 / 0.368 / 0.354 / 0.329 / 0.382 ms at 16 / 20 / 24 / 28 / 32 waves
+//    per CU); the round-2 kernel at 64 VGPRs runs 0.758 ms at 32 against 0.784 at 28 and
+//    0.777 for the 72-VGPR build at 28.  MCPT_TRACE_WAVES caps the waves per CU.
 //  * k_trace partitions: two per XCD, MCPT_TRACE_PARTS overrides.
 int launch_geometry(int dev, LaunchGeom& g) {
     int cus = 0, nx = 1, per_cu = 0, mat0 = 0, mat1 = 0;
@@ -1406,7 +1414,7 @@ int launch_geometry(int dev, LaunchGeom& g) {
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat1, k_material<true>, kBlock, 0) != hipSuccess)
         return -1;
     if (cus <= 0) cus = 256;
-    per_cu = 28;
+    per_cu = 32;
     if (const char* e = getenv("MCPT_TRACE_WAVES")) per_cu = atoi(e);
     if (per_cu <= 0) per_cu = 16;
     for (int w = 0; w < 2; w++)
