@@ -29,8 +29,14 @@ constexpr int kTraceBlock = 64;  // one wave per traversal block
 #define MCPT_LDS_STACK 8
 #endif
 constexpr int kLdsStack = MCPT_LDS_STACK;  // traversal stack entries per lane kept in LDS (deeper: scratch)
-constexpr int kLdsStackDeep = 10;          // the same for trees deeper than kDeepTree levels
-constexpr int kDeepTree = 20;
+#ifndef MCPT_LDS_STACK_DEEP
+#define MCPT_LDS_STACK_DEEP 10
+#endif
+constexpr int kLdsStackDeep = MCPT_LDS_STACK_DEEP;  // the same for trees deeper than kDeepTree levels
+#ifndef MCPT_DEEP_TREE
+#define MCPT_DEEP_TREE 20
+#endif
+constexpr int kDeepTree = MCPT_DEEP_TREE;  // stack pushes beyond which the deep-stack k_trace runs
 constexpr int kMaxStack = 64;  // total (reference: int nodesToVisit[64], Triangle.cu:161)
 
 enum : uint32_t {
