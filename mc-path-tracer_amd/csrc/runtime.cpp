@@ -519,6 +519,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         size_t WH = (size_t)W * H;
         if ((rc = dupload(c, c->scene_bufs, &tx, reinterpret_cast<const float4*>(d->env_tex), WH))) return rc;
         c->env_device_built = !d->env_marginal_y;
+        c->last_env_build_ms = 0.f;
         if (!c->env_device_built) {
             if ((rc = dupload(c, c->scene_bufs, &my, d->env_marginal_y, (size_t)H))) return rc;
             if ((rc = dupload(c, c->scene_bufs, &cy, d->env_conds_y, WH))) return rc;
