@@ -759,5 +759,33 @@ MCPT_HD bool tri_test(V3 o, V3 d, V3 p0, V3 e1, V3 e2, float& t, float& u_out, f
     v_out = (float)((double)v * inv_det);
     return true;
 }
+// The same test when only t is needed (the traversal keeps the triangle index; the hit
+// record is rebuilt from it where it is consumed).  Acceptance does not depend on the
+// quotients, and t is the same value: its fast path is taken on its own range check
+// alone (u and v no longer send a hit to the fp64 path, which gives the same t anyway).
+MCPT_HD bool tri_test_t(V3 o, V3 d, V3 p0, V3 e1, V3 e2, float& t) {
+    V3 pvec = cross(d, e2);
+    float detf = dot(e1, pvec);
+    if (detf < K_EPSILON) return false;
+    V3 tvec = o - p0;
+    float u = dot(tvec, pvec);
+    if (u < 0.f || u > detf) return false;
+    V3 qvec = cross(tvec, e1);
+    float v = dot(d, qvec);
+    if (v < 0.f || u + v > detf) return false;
+    float tf = dot(e2, qvec);
+#if defined(__HIP_DEVICE_COMPILE__)
+    {
+        const Recip r = recip(detf);
+        float tq;
+        if (quot_fp64(tf, r.y, tq) && r.ok) {
+            t = tq;
+            return true;
+        }
+    }
+#endif
+    t = (float)((double)tf * (1.0 / (double)detf));
+    return true;
+}
 
 }  // namespace mcpt

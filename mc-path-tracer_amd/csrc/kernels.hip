@@ -1150,9 +1150,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 RAY_STEP_TRI();
                 tot_t0 += kind == 0 ? 1u : 0u;
                 tot_t1 += kind != 0 ? 1u : 0u;
-                float t, u, v;
+                float t;
                 bool done = false;
-                if (tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v) &&
+                if (tri_test_t(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t) &&
                     !(t < 0.f) &&
                     (kind ? t < K_HUGE
                           : (t < best ||
