@@ -13,7 +13,7 @@ SRCS := $(PKG)/csrc/kernels.hip $(PKG)/csrc/bvh_build.hip $(PKG)/csrc/env_build.
 OBJS := $(patsubst $(PKG)/csrc/%,$(BUILD)/%.o,$(SRCS))
 HDRS := include/mcpt.h $(PKG)/csrc/kernels.hpp $(PKG)/csrc/device/mcpt_core.hpp $(PKG)/csrc/host/host_internal.hpp
 
-all: $(PKG)/libmcpt.so oracle/liboracle.so examples/mcpt_render
+all: $(PKG)/libmcpt.so oracle/liboracle.so examples/mcpt_render tests/native/facade_test
 
 $(BUILD)/%.o: $(PKG)/csrc/% $(HDRS)
 	@mkdir -p $(dir $@)
@@ -28,11 +28,15 @@ examples/mcpt_render: examples/mcpt_render.cpp include/mcpt.h $(PKG)/libmcpt.so
 
 example: examples/mcpt_render
 
+# C++ host facade (include/mcpt.hpp) test driver: host checks on the CPU, a config-1 render on the GPU
+tests/native/facade_test: tests/native/facade_test.cpp include/mcpt.hpp include/mcpt.h $(PKG)/libmcpt.so
+	g++ -O2 -std=c++17 -Wall -Wextra -Iinclude $< -L$(PKG) -lmcpt -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -o $@
+
 oracle/liboracle.so: oracle/mcpt_oracle.c oracle/mcpt_oracle.h
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(BUILD) $(PKG)/libmcpt.so examples/mcpt_render
+	rm -rf $(BUILD) $(PKG)/libmcpt.so examples/mcpt_render tests/native/facade_test
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean

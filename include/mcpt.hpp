@@ -1,0 +1,607 @@
+/*
+ * mcpt.hpp -- C++ host facade over the C ABI (mcpt.h), header-only, std only.
+ *
+ * The reference's host objects for the hot path, with their names, argument meanings and call
+ * order, so reference code keeps its shape when it moves to the MI355X backend:
+ *
+ *   PathTracer        CUDA-RayTracer/PathTracer.h:11-54, PathTracer.cpp:112-164
+ *   Scene             CUDA-RayTracer/Scene.h:35-103 (load, add_light, set_environment_light, ...)
+ *   Film              CUDA-RayTracer/Film.h:47-107, Film.cu:1-103,278-281
+ *   Camera            CUDA-RayTracer/Camera.h:57-118, Camera.cu:62-224
+ *   PerspectiveCamera CUDA-RayTracer/PerspectiveCamera.h:4-12, PerspectiveCamera.cpp:5-50
+ *   Light             CUDA-RayTracer/Light.h:39-67, Light.cu:46-78
+ *   DirectionalLight  CUDA-RayTracer/DirectionalLight.h:18-29, DirectionalLight.cu:49-92
+ *   EnvironmentLight  CUDA-RayTracer/EnvironmentLight.h:178-197, EnvironmentLight.cu:278-392
+ *
+ * What differs, and why:
+ *  * Errors: the reference prints and exit(99)s (checkCudaErrors, CudaHelpers.cpp:3-11); every
+ *    failing call here throws mcpt::Error carrying the MCPT_E_* code and mcpt_last_error().
+ *  * Display: render_image returns the tonemapped RGBA8 film (draw_to_surface,
+ *    wavefront_kernels.cu:6-40) in host memory instead of a GL texture id (no GL interop).
+ *  * Device state: the reference's Scene/Film/Camera own managed-memory structs that the kernels
+ *    read; here one mcpt_ctx per PathTracer owns all device memory, and PathTracer brings it up
+ *    to date from the host objects at each render call (scene upload, camera matrices, film
+ *    size and clears).
+ *  * Observers: the reference's Film observes the camera and scene and clears on any change
+ *    (Film::update -> clear, Film.cu:278-281).  Here every edit bumps a revision counter
+ *    (Subject::revision) and the render call clears the film when the camera's, the scene's or
+ *    a light's revision moved -- the same clears at the same points of the render loop.
+ *  * Scene::load keeps the reference's signature; as there (Scene.cu:24-63) translate and scale
+ *    are accepted and not applied.
+ *  * EnvironmentLight(path) renders in HRDI mode.  The reference's constructor sets the host type
+ *    to HRDI but leaves the device light in Color mode until set_type is called
+ *    (EnvironmentLight.cu:153 vs :335); SURVEY.md 8(d)'s configs specify HRDI, which is what a
+ *    path-constructed light renders here.  Atmosphere (a raster-only type) is rejected.
+ *
+ * Batch mode (MI355X): render_iterations / render_frame run every tile per iteration with no
+ * host round trips (mcpt_iterate / mcpt_render); render_image keeps the reference's one
+ * iteration on one tile per call.
+ */
+#ifndef MCPT_HPP
+#define MCPT_HPP
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "mcpt.h"
+
+namespace mcpt {
+
+class Error : public std::runtime_error {
+public:
+    Error(int code, const std::string& what) : std::runtime_error(what), code_(code) {}
+    int code() const { return code_; }
+
+private:
+    int code_;
+};
+
+namespace detail {
+inline void check(int rc, const mcpt_ctx* ctx, const char* what) {
+    if (rc != MCPT_OK) {
+        const char* msg = mcpt_last_error(ctx);
+        throw Error(rc, std::string(what) + ": " + (msg && *msg ? msg : "error " + std::to_string(rc)));
+    }
+}
+inline uint32_t gen_id() {  // globals.cpp gen_id: process-wide object ids
+    static uint32_t next = 0;
+    return ++next;
+}
+}  // namespace detail
+
+// glm::vec3 stand-in (the facade takes no glm dependency)
+struct vec3 {
+    float x = 0.f, y = 0.f, z = 0.f;
+    vec3() = default;
+    vec3(float a, float b, float c) : x(a), y(b), z(c) {}
+    explicit vec3(float s) : x(s), y(s), z(s) {}
+    bool operator==(const vec3& o) const { return x == o.x && y == o.y && z == o.z; }
+    bool operator!=(const vec3& o) const { return !(*this == o); }
+};
+inline vec3 operator+(vec3 a, vec3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline vec3 operator-(vec3 a, vec3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline vec3 operator*(vec3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline vec3 cross(vec3 a, vec3 b) { return {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y}; }
+inline vec3 normalize(vec3 v) {  // glm::normalize: v * inversesqrt(dot(v, v))
+    const float s = 1.f / std::sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+    return v * s;
+}
+inline float radians(float deg) { return deg * 0.01745329251994329576923690768489f; }  // glm::radians
+
+// Subject (Subject.h): observers are replaced by a revision counter that PathTracer compares.
+class Subject {
+public:
+    uint64_t revision() const { return rev_; }
+
+protected:
+    void notify() { ++rev_; }
+
+private:
+    uint64_t rev_ = 0;
+};
+
+// ---- lights (Light.h:39-67) ------------------------------------------------------------------
+class Light : public Subject {
+public:
+    virtual ~Light() = default;
+    std::string get_name() const { return name; }
+    int get_id() const { return id; }
+    vec3 get_color() const { return color; }
+    float get_ls() const { return ls; }
+    float get_range() const { return range; }
+    void set_color(const vec3 c) { color = c; notify(); }  // Light.cu:62-67
+    void set_ls(const float s) { ls = s; notify(); }        // Light.cu:68-73
+    void set_range(const float r) { range = r; notify(); }  // Light.cu:74-78
+
+protected:
+    std::string name;
+    int id = (int)detail::gen_id();
+    bool delta = false;
+    vec3 color{1.f, 1.f, 1.f};
+    float ls = 1.f;
+    float range = 100.f;
+};
+
+class DirectionalLight : public Light {  // DirectionalLight.cu:49-92
+public:
+    DirectionalLight() : dir_(1.f), ddir_(1.f) { name = "Directional Light"; delta = true; }
+    DirectionalLight(const vec3 dir, const vec3 c) : dir_(dir), ddir_(dir) {
+        name = "Directional Light";
+        color = c;
+        delta = true;
+    }
+    // The host copy is normalised, the device copy is not (DirectionalLight.cu:82-88): the
+    // kernels see the argument as given.
+    void set_dir(const vec3 dir) {
+        dir_ = normalize(dir);
+        ddir_ = dir;
+        notify();
+    }
+    vec3 get_dir() const { return dir_; }
+    vec3 device_dir() const { return ddir_; }
+
+private:
+    vec3 dir_, ddir_;
+};
+
+enum EnvironmentLightType { Color = 0, HRDI = 1, Atmosphere = 2 };  // EnvironmentLight.h:10-14
+
+class EnvironmentLight : public Light {  // EnvironmentLight.cu:278-392
+public:
+    EnvironmentLight() { name = "Environment Light"; }
+    explicit EnvironmentLight(const vec3 c) {
+        name = "Environment Light";
+        color = c;
+    }
+    explicit EnvironmentLight(const std::string& path) : type_(HRDI), path_(path) { name = "Environment Light"; }
+    void set_type(const EnvironmentLightType t) {
+        if (t == Atmosphere) throw Error(MCPT_E_INVALID, "EnvironmentLight: Atmosphere is a raster-only type");
+        type_ = t;
+        notify();
+    }
+    void set_texture_filepath(const std::string& path) {
+        path_ = path;
+        notify();
+    }
+    std::string get_texture_filepath() const { return path_; }
+    vec3 get_color() const { return color; }
+    EnvironmentLightType get_light_type() const { return type_; }
+    // MI355X extension: build the HRDI CDF tables on the device at upload (env_build.hip)
+    // instead of on the host; bit-identical tables, for large maps.
+    void set_device_tables(bool on) {
+        device_tables_ = on;
+        notify();
+    }
+    bool get_device_tables() const { return device_tables_; }
+
+private:
+    EnvironmentLightType type_ = Color;
+    std::string path_;
+    bool device_tables_ = false;
+};
+
+// ---- scene (Scene.h:35-103) ------------------------------------------------------------------
+class Scene : public Subject {
+public:
+    // The reference scene starts with a grey Color environment (Scene.cu:13, :21).
+    Scene() : s_(mcpt_scene_new()) {
+        if (!s_) throw Error(MCPT_E_NOMEM, "mcpt_scene_new");
+        environment_light = std::make_shared<EnvironmentLight>(vec3(0.8f));
+    }
+    ~Scene() { mcpt_scene_free(s_); }
+    Scene(const Scene&) = delete;
+    Scene& operator=(const Scene&) = delete;
+
+    // Scene::load (Scene.cu:24-63): glTF 2.0 binary, node transforms baked, roughness 1 /
+    // metallic 0 (Scene.cu:306-307).  translate / scale are unused, as in the reference.
+    void load(const std::string& path, vec3 translate = vec3(0.f), vec3 scale = vec3(1.f)) {
+        (void)translate;
+        (void)scale;
+        detail::check(mcpt_scene_load_glb(s_, path.c_str(), nullptr), nullptr, "Scene::load");
+        geometry_changed();
+    }
+    // Triangle soup (the RenderObject path, Scene::add_render_object): 3*ntri floats per array.
+    void add_mesh(int32_t ntri, const float* v0, const float* v1, const float* v2, const float* n0, const float* n1,
+                  const float* n2, vec3 base_color) {
+        const float rgb[3] = {base_color.x, base_color.y, base_color.z};
+        detail::check(mcpt_scene_add_mesh(s_, ntri, v0, v1, v2, n0, n1, n2, rgb), nullptr, "Scene::add_mesh");
+        geometry_changed();
+    }
+    // MI355X extension: the BASELINE config proxies of SURVEY.md 8(d) (geometry + environment).
+    void make_proxy(int config_id, const std::string& asset_dir) {
+        detail::check(mcpt_scene_make_proxy(s_, config_id, asset_dir.c_str()), nullptr, "Scene::make_proxy");
+        proxy_env_ = true;
+        geometry_changed();
+    }
+    void add_light(std::shared_ptr<DirectionalLight> light) {  // Scene.h:53
+        if (light && std::find(dir_lights.begin(), dir_lights.end(), light) == dir_lights.end()) {
+            dir_lights.push_back(std::move(light));
+            notify();
+        }
+    }
+    void remove_light(const std::shared_ptr<DirectionalLight>& light) {  // Scene.h:56
+        auto it = std::find(dir_lights.begin(), dir_lights.end(), light);
+        if (it != dir_lights.end()) {
+            dir_lights.erase(it);
+            notify();
+        }
+    }
+    void set_environment_light(std::shared_ptr<EnvironmentLight> env) {  // Scene.h:58
+        if (!env) throw Error(MCPT_E_INVALID, "Scene::set_environment_light: null light");
+        environment_light = std::move(env);
+        proxy_env_ = false;
+        notify();
+    }
+    std::vector<std::shared_ptr<DirectionalLight>> get_lights() const { return dir_lights; }
+    std::shared_ptr<EnvironmentLight> get_environment_light() const { return environment_light; }
+    // MI355X extension: host BVH builder (films do not depend on it: mcpt.h, mcpt_bvh_params)
+    void set_bvh_params(const mcpt_bvh_params& p) {
+        bvh_ = p;
+        geometry_changed();
+    }
+    int bvh_depth() const { return mcpt_scene_bvh_depth(s_); }
+
+    // Everything a render depends on, as (object, revision) pairs: PathTracer re-uploads and
+    // clears the film when it changes (the reference's Scene/Light -> Film observer chain).
+    std::vector<std::pair<const void*, uint64_t>> state() const {
+        std::vector<std::pair<const void*, uint64_t>> st{{this, revision()},
+                                                         {environment_light.get(), environment_light->revision()}};
+        for (const auto& l : dir_lights) st.emplace_back(l.get(), l->revision());
+        return st;
+    }
+
+    // The device description: geometry, BVH and environment from the builder, lights from the
+    // light objects.  Builds the BVH / env tables when geometry or the environment changed.
+    // The returned desc points into this Scene and `dir_params`; valid until the next edit.
+    mcpt_scene_desc desc(std::vector<float>& dir_params) {
+        const EnvironmentLight& env = *environment_light;
+        const std::pair<const void*, uint64_t> env_key{&env, env.revision()};
+        if (!proxy_env_ && env.get_light_type() == HRDI && env_key != env_built_) {
+            if (env.get_texture_filepath().empty()) throw Error(MCPT_E_INVALID, "EnvironmentLight: HRDI without a texture");
+            detail::check(mcpt_scene_set_env_hdr_ex(s_, env.get_texture_filepath().c_str(), 1,
+                                                    env.get_device_tables() ? MCPT_ENV_DEVICE_TABLES : 0u),
+                          nullptr, "EnvironmentLight");
+            env_built_ = env_key;
+            built_ = false;
+        }
+        if (!built_) {
+            detail::check(mcpt_scene_build_ex(s_, &bvh_), nullptr, "Scene build");
+            built_ = true;
+        }
+        mcpt_scene_desc d;
+        detail::check(mcpt_scene_get_desc(s_, &d), nullptr, "Scene desc");
+        if (!proxy_env_ && env.get_light_type() == Color) {  // EnvironmentLight.cu:36-38: color * ls
+            d.env_mode = 0;
+            d.env_color[0] = env.get_color().x;
+            d.env_color[1] = env.get_color().y;
+            d.env_color[2] = env.get_color().z;
+            d.env_ls = env.get_ls();
+        }
+        dir_params.clear();
+        for (const auto& l : dir_lights) {  // light ids 1..N after the env light (Scene.cu:365-388)
+            const vec3 dd = l->device_dir(), c = l->get_color();
+            const float p[7] = {dd.x, dd.y, dd.z, c.x, c.y, c.z, l->get_ls()};
+            dir_params.insert(dir_params.end(), p, p + 7);
+        }
+        d.ndir = (int32_t)dir_lights.size();
+        d.dir_params = dir_params.empty() ? nullptr : dir_params.data();
+        return d;
+    }
+
+    std::vector<std::shared_ptr<DirectionalLight>> dir_lights;
+    std::shared_ptr<EnvironmentLight> environment_light;
+
+private:
+    void geometry_changed() {
+        built_ = false;
+        notify();
+    }
+    mcpt_scene* s_;
+    bool built_ = false;
+    bool proxy_env_ = false;  // make_proxy set the environment (until set_environment_light)
+    std::pair<const void*, uint64_t> env_built_{nullptr, ~0ull};
+    mcpt_bvh_params bvh_{MCPT_BVH_SAH3, 8, 128, 0.5f, 1.0f};
+};
+
+// ---- cameras (Camera.h:57-118) ---------------------------------------------------------------
+enum Camera_Movement { FORWARD, BACKWARD, LEFT, RIGHT, UP, DOWN };
+
+class Camera : public Subject {
+public:
+    virtual ~Camera() = default;
+
+    void move(const Camera_Movement direction, const float deltaTime) {  // Camera.cu:62-79
+        const float velocity = movement_speed * deltaTime;
+        if (direction == FORWARD) position = position + front * velocity;
+        if (direction == BACKWARD) position = position - front * velocity;
+        if (direction == LEFT) position = position - right * velocity;
+        if (direction == RIGHT) position = position + right * velocity;
+        if (direction == UP) position = position + up * velocity;
+        if (direction == DOWN) position = position - up * velocity;
+        update();
+    }
+    void rotate(const float dyaw, const float dpitch) {  // Camera.cu:80-95 (pitch clamped to +-89)
+        yaw += dyaw * look_sensitivity;
+        pitch += dpitch * look_sensitivity;
+        pitch = std::min(89.f, std::max(-89.f, pitch));
+        update();
+    }
+    void set_position(const vec3 p) { position = p; update(); }
+    void set_yaw_pitch(const float y, const float p) { yaw = y; pitch = p; update(); }
+    void set_zoom(const float z) { zoom = z; update(); }
+    void set_focal_distance(const float f) { focal_distance = f; update(); }
+    void set_lens_radius(const float r) { lens_radius = r; update(); }
+    void set_aspect_ratio(const float a) { aspect_ratio = a; update(); }
+
+    vec3 get_position() const { return position; }
+    void get_yaw_pitch(float& y, float& p) const { y = yaw; p = pitch; }
+    float get_zoom() const { return zoom; }
+    float get_focal_distance() const { return focal_distance; }
+    float get_lens_radius() const { return lens_radius; }
+    float get_aspect_ratio() const { return aspect_ratio; }
+    uint32_t get_id() const { return id; }
+    vec3 get_front() const { return front; }
+    vec3 get_up() const { return up; }
+    vec3 get_right() const { return right; }
+    // dCamera (Camera.h:34-46) as the kernels read it: Camera::update's matrices.
+    const mcpt_camera& get_dptr() const { return dcam; }
+
+    // Camera::update (Camera.cu:194-224): view basis, projection, inverse matrices; notify.
+    void update() {
+        const float cy = std::cos(radians(yaw)), sy = std::sin(radians(yaw));
+        const float cp = std::cos(radians(pitch)), sp = std::sin(radians(pitch));
+        front = normalize(vec3(cy * cp, sp, sy * cp));
+        right = normalize(cross(front, worldUp));
+        up = normalize(cross(right, front));
+        mcpt_camera_params p{{position.x, position.y, position.z}, yaw, pitch, zoom, aspect_ratio, znear, zfar,
+                             lens_radius, focal_distance};
+        detail::check(mcpt_camera_make(&p, &dcam), nullptr, "Camera::update");
+        notify();
+    }
+
+protected:
+    Camera() = default;
+    uint32_t id = detail::gen_id();
+    float zfar = 100.f, znear = 1.f;
+    vec3 position{0.f, 0.f, 0.f};
+    vec3 front{0.f, 0.f, -1.f}, up{0.f, 1.f, 0.f}, right{1.f, 0.f, 0.f};
+    vec3 worldUp{0.f, 1.f, 0.f};
+    float yaw = -90.f, pitch = 0.f;
+    float movement_speed = 2.5f, look_sensitivity = 0.1f;
+    float zoom = 0.f;  // the vertical field of view in radians (glm::perspective(zoom, ...))
+    float lens_radius = 0.0001f, focal_distance = 35.f;
+    float aspect_ratio = 1.f;
+    mcpt_camera dcam{};
+};
+
+class PerspectiveCamera : public Camera {  // PerspectiveCamera.cpp:5-50
+public:
+    PerspectiveCamera() {
+        zoom = 90.f;  // as the reference's default constructor (a radian argument of 90)
+        znear = 1.f;
+        zfar = 100.f;
+        update();
+    }
+    PerspectiveCamera(float yfov, float zn, float zf) { init(yfov, zn, zf); }
+    PerspectiveCamera(vec3 pos, float yfov, float zn, float zf) {
+        position = pos;
+        init(yfov, zn, zf);
+    }
+
+private:
+    void init(float yfov, float zn, float zf) {
+        if (std::isnan(yfov) || std::isnan(zn) || std::isnan(zf))  // m_assert (PerspectiveCamera.cpp:33-35)
+            throw Error(MCPT_E_INVALID, "PerspectiveCamera: NaN argument");
+        zoom = yfov;
+        znear = zn;
+        zfar = zf;
+        update();
+    }
+};
+
+// ---- film (Film.h:47-107) --------------------------------------------------------------------
+class Film : public Subject {
+public:
+    Film() { set_tile_size(256, 256); }  // Film.cu:5-18: 1x1, 256x256 tiles
+
+    void set_exposure(const float e) { exposure = e; }
+    void set_size(const uint32_t w, const uint32_t h) {  // Film.cu:26-37: resize + clear
+        width = w;
+        height = h;
+        update_tile_info();
+        clear();
+    }
+    void set_tile_size(const uint32_t w, const uint32_t h) {
+        tile_width = w;
+        tile_height = h;
+        update_tile_info();
+    }
+    float get_exposure() const { return exposure; }
+    void get_size(uint32_t& w, uint32_t& h) const { w = width; h = height; }
+    void get_tile_size(uint32_t& w, uint32_t& h) const { w = tile_width; h = tile_height; }
+    uint32_t get_id() const { return id; }
+    // clear_dfilm + first tile (Film.cu:76-87); the device film is cleared at the next render call
+    void clear() {
+        tile_id = 0;
+        tile_x_pos = 0;
+        tile_y_pos = 0;
+        ++clears_;
+        notify();
+    }
+    void update_tile_position() {  // Film.cu:94-103: tiles round-robin, row-major
+        tile_id = (tile_id + 1) % nmb_tiles;
+        tile_x_pos = tile_id % nmb_tile_cols;
+        tile_y_pos = tile_id / nmb_tile_cols;
+    }
+    uint32_t get_tile_x_pos() const { return tile_x_pos; }
+    uint32_t get_tile_y_pos() const { return tile_y_pos; }
+    uint32_t get_nmb_tiles() const { return nmb_tiles; }
+    // The displayed image (the GL texture of the reference): RGBA8, row 0 = top, written by
+    // PathTracer::render_image.
+    const std::vector<uint8_t>& get_image() const { return image; }
+    uint64_t clear_count() const { return clears_; }
+
+private:
+    friend class PathTracer;
+    void update_tile_info() {  // Film.cu:172-178
+        nmb_tile_cols = tile_width ? (width + tile_width - 1) / tile_width : 0;
+        nmb_tile_rows = tile_height ? (height + tile_height - 1) / tile_height : 0;
+        nmb_tiles = std::max(1u, nmb_tile_cols * nmb_tile_rows);
+        nmb_tile_cols = std::max(1u, nmb_tile_cols);
+    }
+    uint32_t id = detail::gen_id();
+    uint32_t width = 1, height = 1, tile_width = 0, tile_height = 0;
+    uint32_t tile_id = 0, nmb_tiles = 1, nmb_tile_cols = 1, nmb_tile_rows = 1, tile_x_pos = 0, tile_y_pos = 0;
+    float exposure = 1.f;
+    uint64_t clears_ = 0;
+    std::vector<uint8_t> image;
+};
+
+// ---- path tracer (PathTracer.h:11-54) ---------------------------------------------------------
+inline mcpt_config default_config() {  // reference mode: wavefront_kernels.cu:124,142,189
+    mcpt_config c{0x5EED2026ull, 250, 5, 3, 256, 256, 0};
+    return c;
+}
+
+class PathTracer {
+public:
+    // One device context per PathTracer (PathTracer.cpp: stream, queues, interop).  Throws
+    // Error(MCPT_E_NODEVICE) without a gfx950 device: there is no CPU fallback.
+    explicit PathTracer(int device = 0, mcpt_config cfg = default_config()) : cfg_(cfg) {
+        cfg.flags |= MCPT_FLAG_NO_AUTO_CLEAR;  // the facade applies the observer clears itself
+        detail::check(mcpt_create(device, &cfg, &ctx_), nullptr, "PathTracer");
+    }
+    ~PathTracer() { mcpt_destroy(ctx_); }
+    PathTracer(const PathTracer&) = delete;
+    PathTracer& operator=(const PathTracer&) = delete;
+
+    // PathTracer::render_image (PathTracer.cpp:112-130): one wavefront iteration of the film's
+    // current tile, the display image refreshed, the tile advanced.
+    const std::vector<uint8_t>& render_image(const std::shared_ptr<Scene>& scene, const std::shared_ptr<Camera>& camera,
+                                             const std::shared_ptr<Film>& film) {
+        sync(*scene, *camera, *film);
+        detail::check(mcpt_wavefront_step(ctx_, film->tile_x_pos, film->tile_y_pos, &stats_), ctx_, "render_image");
+        if (display_) tonemap(*film);
+        film->update_tile_position();
+        return film->image;
+    }
+    // Batch mode: `iterations` wavefront iterations over every tile (mcpt_iterate), no host
+    // round trips between them.
+    const mcpt_stage_stats& render_iterations(const std::shared_ptr<Scene>& scene, const std::shared_ptr<Camera>& camera,
+                                              const std::shared_ptr<Film>& film, uint32_t iterations) {
+        sync(*scene, *camera, *film);
+        detail::check(mcpt_iterate(ctx_, iterations, &stats_), ctx_, "render_iterations");
+        if (display_) tonemap(*film);
+        return stats_;
+    }
+    // Batch mode: iterate until every pixel has its samples (mcpt_render).
+    const mcpt_stage_stats& render_frame(const std::shared_ptr<Scene>& scene, const std::shared_ptr<Camera>& camera,
+                                         const std::shared_ptr<Film>& film) {
+        sync(*scene, *camera, *film);
+        detail::check(mcpt_render(ctx_, &stats_), ctx_, "render_frame");
+        if (display_) tonemap(*film);
+        return stats_;
+    }
+
+    // Queues live on the device and are rebuilt every iteration (PathTracer.cpp:149-155 resets
+    // the reference's managed counters): nothing to do.
+    void clear_queues() {}
+    // The reference's stubs (PathTracer.cpp:156-164): no effect, 0.
+    void set_samples(int) {}
+    int get_samples() { return 0; }
+
+    // MI355X extensions
+    void set_path_slots(uint32_t slots) {  // paths in flight per pixel; clears the film
+        detail::check(mcpt_set_path_slots(ctx_, slots), ctx_, "set_path_slots");
+    }
+    void set_display(bool on) { display_ = on; }  // tonemap into Film::get_image after each call
+    const mcpt_stage_stats& last_stats() const { return stats_; }
+    const mcpt_config& config() const { return cfg_; }
+    mcpt_ctx* handle() const { return ctx_; }
+    std::string device_name() const {
+        char buf[256] = {0};
+        detail::check(mcpt_device_name(ctx_, buf, (int32_t)sizeof(buf)), ctx_, "device_name");
+        return buf;
+    }
+    // Radiance buffers (parity): Ld 3*W*H floats, samples W*H
+    void read_film(std::vector<float>& Ld, std::vector<uint32_t>& samples) {
+        uint32_t w = 0, h = 0;
+        detail::check(mcpt_film_size(ctx_, &w, &h), ctx_, "read_film");
+        Ld.resize((size_t)w * h * 3);
+        samples.resize((size_t)w * h);
+        detail::check(mcpt_film_read(ctx_, Ld.data(), samples.data()), ctx_, "read_film");
+    }
+    void write_png(const std::shared_ptr<Film>& film, const std::string& path) {
+        detail::check(mcpt_film_write_png(ctx_, film->get_exposure(), path.c_str()), ctx_, "write_png");
+    }
+    void write_pfm(const std::string& path) {
+        detail::check(mcpt_film_write_pfm(ctx_, path.c_str()), ctx_, "write_pfm");
+    }
+
+private:
+    // Bring the context up to date with the host objects.  Order as the reference's observer
+    // chain: a scene or camera edit clears the film (Film::update), a film resize clears it.
+    void sync(Scene& scene, Camera& camera, Film& film) {
+        bool edited = false;
+        const auto st = scene.state();
+        if (&scene != scene_ || st != scene_state_) {
+            std::vector<float> dir_params;
+            const mcpt_scene_desc d = scene.desc(dir_params);
+            detail::check(mcpt_scene_upload(ctx_, &d), ctx_, "scene upload");
+            scene_ = &scene;
+            scene_state_ = st;
+            edited = true;
+        }
+        if (&camera != camera_ || camera.revision() != camera_rev_) {
+            detail::check(mcpt_camera_set(ctx_, &camera.get_dptr()), ctx_, "camera");
+            camera_ = &camera;
+            camera_rev_ = camera.revision();
+            edited = true;
+        }
+        if (&film != film_ || film.width != fw_ || film.height != fh_ || film.tile_width != ftw_ ||
+            film.tile_height != fth_) {
+            // (re)allocates the device film, cleared: Film::set_size -> update_path_size + clear
+            detail::check(mcpt_film_resize(ctx_, film.width, film.height, film.tile_width, film.tile_height), ctx_,
+                          "film resize");
+            film_ = &film;
+            fw_ = film.width;
+            fh_ = film.height;
+            ftw_ = film.tile_width;
+            fth_ = film.tile_height;
+            film.clear();
+            film_clears_ = film.clears_;
+            edited = false;
+        }
+        if (edited) film.clear();  // Film::update -> clear (Film.cu:278-281)
+        if (film.clears_ != film_clears_) {
+            detail::check(mcpt_film_clear(ctx_), ctx_, "film clear");  // clear_dfilm
+            film_clears_ = film.clears_;
+        }
+    }
+    void tonemap(Film& film) {
+        film.image.resize((size_t)film.width * film.height * 4);
+        detail::check(mcpt_film_tonemap_rgba8(ctx_, film.exposure, film.image.data()), ctx_, "tonemap");
+    }
+
+    mcpt_config cfg_;
+    mcpt_ctx* ctx_ = nullptr;
+    mcpt_stage_stats stats_{};
+    bool display_ = true;
+    const Scene* scene_ = nullptr;
+    std::vector<std::pair<const void*, uint64_t>> scene_state_;
+    const Camera* camera_ = nullptr;
+    uint64_t camera_rev_ = 0;
+    const Film* film_ = nullptr;
+    uint32_t fw_ = 0, fh_ = 0, ftw_ = 0, fth_ = 0;
+    uint64_t film_clears_ = 0;
+};
+
+}  // namespace mcpt
+#endif

@@ -820,9 +820,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     enter(home);
     const DevScene& sc = a.scene;
 
-    // per-lane work counters per set (wave-reduced at exit); per-ray step counts only in
-    // diagnostics builds (MCPT_RAY_STEPS)
-    uint32_t tot_n0 = 0, tot_t0 = 0, tot_h0 = 0, tot_n1 = 0, tot_t1 = 0, tot_h1 = 0;
+    // per-lane work counters (wave-reduced at exit): tot_* count every node step, triangle
+    // test and hit; the any-hit set's share is attributed per ray (tot_n1 -= tot_n when an
+    // any-hit ray starts, += when it finishes), so a step costs one add instead of a
+    // kind-selected add per set.  Per-ray step counts only in diagnostics builds
+    // (MCPT_RAY_STEPS).
+    uint32_t tot_n = 0, tot_t = 0, tot_h = 0, tot_n1 = 0, tot_t1 = 0, tot_h1 = 0;
 #ifdef MCPT_RAY_STEPS
     uint32_t rn = 0, rt = 0;
 #define RAY_STEP_NODE() (rn++)
@@ -877,8 +880,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         return kEnd;
     };
     auto finish = [&]() {
-        tot_h0 += (kind == 0 && tri >= 0) ? 1u : 0u;
-        tot_h1 += (kind != 0 && tri >= 0) ? 1u : 0u;
+        tot_h += tri >= 0 ? 1u : 0u;
+        if (kind) {
+            tot_n1 += tot_n;
+            tot_t1 += tot_t;
+            tot_h1 += tri >= 0 ? 1u : 0u;
+        }
 #ifdef MCPT_RAY_STEPS
         uint32_t* rs = kind ? a.set[1].ray_steps : a.set[0].ray_steps;
         if (rs) rs[qi] = rn + rt;
@@ -961,6 +968,10 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     sp = 0;
                     leaf = kEnd;
                     act = true;
+                    if (kind) {  // the any-hit set's counts start here (see tot_n)
+                        tot_n1 -= tot_n;
+                        tot_t1 -= tot_t;
+                    }
                     const bool pre = kind ? a.set[1].prefiltered : a.set[0].prefiltered;
                     // NaN / zero direction: a miss / visible
                     if (!pre &&
@@ -1010,8 +1021,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             bool need_pop = false;
             if (ref >= 0) {
               RAY_STEP_NODE();
-              tot_n0 += kind == 0 ? 1u : 0u;
-              tot_n1 += kind != 0 ? 1u : 0u;
+              tot_n++;
               const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;  // slow-path slab only
               if constexpr (kW == 4) {
                 // 4-wide node: test the four child boxes, visit the nearest hit, push the
@@ -1148,8 +1158,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 const float4* tp = sc.tri + kTriF4 * id;
                 const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
                 RAY_STEP_TRI();
-                tot_t0 += kind == 0 ? 1u : 0u;
-                tot_t1 += kind != 0 ? 1u : 0u;
+                tot_t++;
                 float t;
                 bool done = false;
                 if (tri_test_t(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t) &&
@@ -1217,7 +1226,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #ifdef MCPT_X_PREFETCH
     if (a.refill_min == 1000u && pfx == 0x9e3779b9u) a.hit_tri[0] = 0;  // keeps the touches (never true)
 #endif
-    wave_stats(a.set[0].stats, lane, tot_n0, tot_t0, tot_h0);
+    wave_stats(a.set[0].stats, lane, tot_n - tot_n1, tot_t - tot_t1, tot_h - tot_h1);
     wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);
 #ifdef MCPT_WAVE_TIMES
     if (threadIdx.x == 0 && blockIdx.x < 16384) {

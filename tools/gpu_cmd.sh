@@ -1,5 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-MCPT_LIB=$PWD/mc-path-tracer_amd/libmcpt_tprof.so timeout -k 10 120 python -u tools/trace_prof.py > gpurun_out/tprof.log 2>&1 || { cat gpurun_out/tprof.log; exit 1; }
-cat gpurun_out/tprof.log
+timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+grep -E "passed|failed" gpurun_out/gpu_tests.log | tail -2
+grep facade gpurun_out/gpu_tests.log
+timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/quick_bench.json 2> gpurun_out/quick_bench.err || { tail -20 gpurun_out/quick_bench.err; exit 1; }
+python -c "
+import json; d = json.load(open('gpurun_out/quick_bench.json'))
+print('value', d['value'], 'stage ms', d['stage_ms_per_step'], 'per_ray', d['roofline']['per_ray'])"

@@ -11,7 +11,7 @@ pt.trace_profile(reset=True)
 N = 10
 st = pt.iterate(N)
 p = pt.trace_profile()
-waves = 7168  # 28 per CU x 256 CUs
+waves = int(os.environ.get("WAVES", "8192"))  # resident waves: 32 per CU x 256 CUs (8-wave child-pair build)
 print({k: v / N for k, v in p.items()})
 trips = p["trips"] / N
 print("per iteration: trips/wave %.0f  node-lane util %.3f  idle-lane frac %.3f  tri phases/trip %.3f  tri lanes/phase %.1f" % (
