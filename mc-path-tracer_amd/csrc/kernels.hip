@@ -189,10 +189,18 @@ __device__ inline bool ray_misses_scene(const DevScene& sc, V3 o, V3 d) {
 __device__ inline void hit_record(const DevScene& sc, V3 o, V3 d, int tri, V3& pos, V3& nrm, int& mat, float& t_out) {
     const float4* tp = sc.tri + kTriF4 * tri;
     const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-    float t, u, v;
-    tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v);
     const float4* sp4 = sc.tri_sh + 3 * tri;
     const float4 s0 = sp4[0], s1 = sp4[1], s2 = sp4[2];
+#ifndef MCPT_X_LAZY_V0
+    // All six loads in one round trip: the compiler otherwise issues the vertex load after
+    // the determinant test and the shading record after the whole test (three serialised
+    // fetches; the hit is known to exist, so every value is used).
+    __asm__ volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w),
+                     "v"(w2.x), "v"(s0.x), "v"(s0.y), "v"(s0.z), "v"(s0.w), "v"(s1.x), "v"(s1.y), "v"(s1.z),
+                     "v"(s1.w), "v"(s2.x), "v"(s2.y));
+#endif
+    float t, u, v;
+    tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v);
     const V3 n0 = v3(s0.x, s0.y, s0.z), n1 = v3(s0.w, s1.x, s1.y), n2 = v3(s1.z, s1.w, s2.x);
     const float w = (1.f - u) - v;
     nrm = normalize((n1 * u + n2 * v) + n0 * w);  // Triangle.cu:76
@@ -955,6 +963,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     qi = qslot;
 #endif
                     rid = qp ? qp[qslot] : qslot;
+#ifdef MCPT_X_EXTRA_HOP  // experiment: one more dependent load before the ray loads (refill latency cost)
+                    rid += a.vis[rid] == 0x7bu ? 1u : 0u;
+#endif
                     const float4 o4 = rop[rid], d4 = rdp[rid];
                     o = xyz(o4);
                     d = xyz(d4);
@@ -1157,6 +1168,13 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 const int id = leaf & 0xffffff;
                 const float4* tp = sc.tri + kTriF4 * id;
                 const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
+#ifndef MCPT_X_LAZY_V0
+                // One memory round trip per test: without this the compiler sinks the vertex
+                // load (w0.xyz) below the determinant test, so every front-facing test waits
+                // for a second, dependent fetch of the same record.
+                __asm__ volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z),
+                                 "v"(w1.w), "v"(w2.x), "v"(w2.y));
+#endif
                 RAY_STEP_TRI();
                 tot_t++;
                 float t;
