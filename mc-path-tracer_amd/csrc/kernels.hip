@@ -258,7 +258,7 @@ struct MatOut {
 // Gram-Schmidt (A.9), env sampling/pdf on matched, clamped cells (A.11).
 template <bool FIXED>
 __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t samples, uint32_t len, V3 beta_store,
-                                 int32_t htri) {
+                                 int32_t htri, float4* stage) {
     const DevScene& sc = a.scene;
     MatOut mo{false, false, false, false, false, 0u};
     SPROF_T0();
@@ -338,8 +338,13 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
             a.p.vis[2 * pid] = 1;
             mo.trivial_any++;
         } else {
+#ifndef MCPT_SPARSE_ANY  // staged: stored at its any-queue position after the block push
+            stage[0 * kBlock + threadIdx.x] = f4(so_l, 0.f);
+            stage[1 * kBlock + threadIdx.x] = f4(ldir, 0.f);
+#else
             a.p.sray_o[2 * pid] = f4(so_l, 0.f);
             a.p.sray_d[2 * pid] = f4(ldir, 0.f);
+#endif
             mo.want_l = true;
         }
     }
@@ -364,8 +369,13 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
             a.p.vis[2 * pid + 1] = 1;
             mo.trivial_any++;
         } else {
+#ifndef MCPT_SPARSE_ANY
+            stage[2 * kBlock + threadIdx.x] = f4(so_b, 0.f);
+            stage[3 * kBlock + threadIdx.x] = f4(wi_b, 0.f);
+#else
             a.p.sray_o[2 * pid + 1] = f4(so_b, 0.f);
             a.p.sray_d[2 * pid + 1] = f4(wi_b, 0.f);
+#endif
             mo.want_b = true;
         }
     }
@@ -590,6 +600,11 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
     unsigned long long _t_mat = __builtin_readcyclecounter();
 #endif
     uint32_t n_ext = 0, n_any = 0, n_vis = 0;
+    // Any-hit rays are staged here (light ray o/d, BRDF visibility ray o/d) and stored after
+    // the block push at their queue positions: the block's rays of one kind land contiguously,
+    // so k_trace reads them densely and without the queue-entry hop (the pid-indexed layout
+    // wrote and read 32-B pieces of partly used lines).
+    __shared__ float4 s_any[4][kBlock];
     for (uint32_t base = w_in * kBlock; base < n; base += bps * kBlock) {  // block-uniform trip count
         const uint32_t i = base + threadIdx.x;
         MatOut mo{false, false, false, false, false, 0u};
@@ -598,15 +613,29 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
             const uint4 q = a.mat_rec[shard * a.ext_cap + i];  // {pid, len, samples, hit_tri}
             const float4 b4 = a.mat_beta[shard * a.ext_cap + i];
             mpid = q.x;
-            mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w);
+            mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w, &s_any[0][0]);
         }
         bool want[3] = {mo.want_ext, mo.want_l, mo.want_b};
         uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
         uint32_t slot[3], total[3];
         block_push<3>(want, ctr, slot, total);
         if (mo.want_ext) a.ext_q[shard * a.ext_cap + slot[0]] = mpid;
-        if (mo.want_l) a.any_q[shard * a.any_cap + slot[1]] = 2 * mpid;
-        if (mo.want_b) a.any_q[shard * a.any_cap + slot[2]] = 2 * mpid + 1;
+        if (mo.want_l) {
+            const uint32_t k = shard * a.any_cap + slot[1];
+            a.any_q[k] = 2 * mpid;
+#ifndef MCPT_SPARSE_ANY
+            a.p.sray_o[k] = s_any[0][threadIdx.x];
+            a.p.sray_d[k] = s_any[1][threadIdx.x];
+#endif
+        }
+        if (mo.want_b) {
+            const uint32_t k = shard * a.any_cap + slot[2];
+            a.any_q[k] = 2 * mpid + 1;
+#ifndef MCPT_SPARSE_ANY
+            a.p.sray_o[k] = s_any[2][threadIdx.x];
+            a.p.sray_d[k] = s_any[3][threadIdx.x];
+#endif
+        }
         n_ext += (mo.want_ext || mo.trivial_ext) ? 1u : 0u;  // queued + resolved-in-place rays
         n_any += (mo.want_l ? 1u : 0u) + (mo.want_b ? 1u : 0u) + mo.trivial_any;
         n_vis += mo.vis_ray ? 1u : 0u;
@@ -962,11 +991,15 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #ifdef MCPT_RAY_STEPS
                     qi = qslot;
 #endif
-                    rid = qp ? qp[qslot] : qslot;
+                    // a dense set (ray_at_slot: the any-hit rays k_material stores at their queue
+                    // positions) issues its ray loads with the queue-entry load, not after it
+                    const bool at_slot = kind ? a.set[1].ray_at_slot : a.set[0].ray_at_slot;
+                    rid = at_slot ? qslot : (qp ? qp[qslot] : qslot);
 #ifdef MCPT_X_EXTRA_HOP  // experiment: one more dependent load before the ray loads (refill latency cost)
                     rid += a.vis[rid] == 0x7bu ? 1u : 0u;
 #endif
                     const float4 o4 = rop[rid], d4 = rdp[rid];
+                    if (at_slot && qp) rid = qp[qslot];  // the result index, needed only when the ray finishes
                     o = xyz(o4);
                     d = xyz(d4);
 #ifdef MCPT_RAY_STEPS

@@ -8,7 +8,11 @@
 //   ray_o/ray_d   float4 [P]    extension ray (xyz, pad)
 //   hit_p         float4 [P]    isect.position, t
 //   hit_n         float4 [P]    isect.normal, material id (int bits, -1 = miss)
-//   sray_o/sray_d float4 [2P]   any-hit rays: [2p] light sample, [2p+1] BRDF visibility
+//   sray_o/sray_d float4 [2Q]   any-hit rays at their any-queue position (Q = queue entries,
+//                               allocated with the queues): written densely by k_material after
+//                               its block push, read densely by k_trace; the queue entry itself
+//                               holds the result index 2p (light sample) / 2p+1 (BRDF visibility).
+//                               (MCPT_SPARSE_ANY: the previous layout, [2P] indexed 2p / 2p+1)
 //   beta          float4 [P]    throughput, (f_sample/pdf_sample).x
 //   nee0 / nee1   float4 [P]    precomputed light / BRDF MIS terms, ratio .y / .z
 //   flags         u32    [P]    dead, len, MIS condition bits
@@ -127,6 +131,8 @@ struct TraceSet {
     uint32_t* stats;            // optional: shard s counters at stats[s * C_WORDS + 0..2] (nodes, tests, hits)
     uint32_t* ray_steps;        // optional per-queue-entry node fetches + triangle tests (diagnostics)
     int prefiltered;            // 1: every ray has a valid direction and enters the root box (k_shade checked)
+    int ray_at_slot;            // 1: the ray of queue position k is ro/rd[k] (dense); queue[k] is only the
+                                //    result index.  0: the ray is ro/rd[queue[k]]
 };
 struct TraceArgs {
     DevScene scene;

@@ -58,6 +58,7 @@ struct mcpt_ctx {
     std::vector<void*> film_bufs;
     DevPaths p{};
     uint32_t *ext_q = nullptr, *any_q = nullptr, *mat_q = nullptr;
+    float4* any_ray = nullptr;          // any-hit rays at their queue positions: o [2 queue_alloc], then d
     uint32_t ext_cap = 0, any_cap = 0;  // per-shard capacities
     size_t queue_alloc = 0;             // entries allocated for ext_q (any_q holds twice)
     CounterBlock* cnt = nullptr;
@@ -171,6 +172,7 @@ void mcpt_destroy(mcpt_ctx* c) {
     if (c->ext_q) (void)hipFree(c->ext_q);
     if (c->any_q) (void)hipFree(c->any_q);
     if (c->mat_q) (void)hipFree(c->mat_q);
+    if (c->any_ray) (void)hipFree(c->any_ray);
     for (auto e : c->events) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -645,14 +647,21 @@ static int set_tiles_internal(mcpt_ctx* c, const std::vector<int2>& t) {
         if (c->ext_q) (void)hipFree(c->ext_q);
         if (c->any_q) (void)hipFree(c->any_q);
         if (c->mat_q) (void)hipFree(c->mat_q);
+        if (c->any_ray) (void)hipFree(c->any_ray);
         c->ext_q = c->any_q = c->mat_q = nullptr;
+        c->any_ray = nullptr;
         c->queue_alloc = 0;
         if (hipMalloc(&c->ext_q, need * sizeof(uint32_t)) != hipSuccess ||
             hipMalloc(&c->any_q, 2 * need * sizeof(uint32_t)) != hipSuccess ||
-            hipMalloc(&c->mat_q, need * 8 * sizeof(uint32_t)) != hipSuccess)  // MatRec + beta per slot
+            hipMalloc(&c->mat_q, need * 8 * sizeof(uint32_t)) != hipSuccess ||  // MatRec + beta per slot
+            hipMalloc(&c->any_ray, 4 * need * sizeof(float4)) != hipSuccess)    // o + d per any-queue entry
             return set_err(c, MCPT_E_NOMEM, "queue allocation failed");
         c->queue_alloc = need;
     }
+#ifndef MCPT_SPARSE_ANY
+    c->p.sray_o = c->any_ray;  // indexed by any-queue position (kShards * any_cap = 2 * need entries)
+    c->p.sray_d = c->any_ray + 2 * c->queue_alloc;
+#endif
     if (t.size() > c->tiles_cap) {
         if (c->tiles) HIPCHK(c, hipFree(c->tiles));
         c->tiles = nullptr;
@@ -701,7 +710,9 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
     int rc;
     if ((rc = dalloc(c, c->film_bufs, &p.ray_o, P)) || (rc = dalloc(c, c->film_bufs, &p.ray_d, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.hit_tri, P)) ||
+#ifdef MCPT_SPARSE_ANY
         (rc = dalloc(c, c->film_bufs, &p.sray_o, 2 * P)) || (rc = dalloc(c, c->film_bufs, &p.sray_d, 2 * P)) ||
+#endif
         (rc = dalloc(c, c->film_bufs, &p.beta, P)) || (rc = dalloc(c, c->film_bufs, &p.nee0, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.nee1, P)) || (rc = dalloc(c, c->film_bufs, &p.Ld, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.flags, P)) || (rc = dalloc(c, c->film_bufs, &p.samples, P)) ||
@@ -716,6 +727,8 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
         if (*q) (void)hipFree(*q);
         *q = nullptr;
     }
+    if (c->any_ray) (void)hipFree(c->any_ray);
+    c->any_ray = nullptr;
     c->queue_alloc = 0;
     HIPCHK(c, hipMemset(p.hit_tri, 0xff, P * sizeof(int32_t)));
     HIPCHK(c, hipMemset(p.vis, 0, 2 * P));
@@ -805,6 +818,9 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     v.shard_cap = c->any_cap;
     v.stats = &c->cnt->shard[0][C_STATS + 3];
     v.prefiltered = 1;
+#ifndef MCPT_SPARSE_ANY
+    v.ray_at_slot = 1;  // k_material stores the any-hit rays at their queue positions
+#endif
     ta.hit_tri = c->p.hit_tri;
     ta.vis = c->p.vis;
     ta.grab = &c->cnt->grab[0][0];  // reset by k_accumulate below
