@@ -327,12 +327,16 @@ MCPT_HD void spherical_map(V3 d, float& u, float& v) {
     u = 0.5f + datan2(d.z, d.x) * ONE_2PI_F;
     v = 0.5f - dasin(d.y) * ONE_PI_F;
 }
-MCPT_HD V3 spherical_direction(float u, float v) {
+// The two factors of spherical_direction: (sin, cos) of theta (from v) and of phi (from u).
+MCPT_HD void spherical_theta(float v, float& st, float& ct) { dsincos(PI_F * v, st, ct); }
+MCPT_HD void spherical_phi(float u, float& sp, float& cp) {
     float phi = (float)((double)(2.f * PI_F) * ((double)u - 0.5));  // fp64 island
-    float theta = PI_F * v;
-    float st, ct, sp, cp;
-    dsincos(theta, st, ct);
     dsincos(phi, sp, cp);
+}
+MCPT_HD V3 spherical_direction(float u, float v) {
+    float st, ct, sp, cp;
+    spherical_theta(v, st, ct);
+    spherical_phi(u, sp, cp);
     V3 n;
     n.x = cp * st;
     n.z = sp * st;
@@ -361,10 +365,14 @@ struct EnvView {
     // Optional light-sample tables (device only, HRDI mode, built at upload by
     // k_env_table from these same functions): in either mode env_dir's result is a
     // function of the sampled cell (x, y) alone, and so are env_L and env_pdf at that
-    // direction.  Entry (y * (w + 1) + x + 1) = {dir.xyz, pdf}, {L.xyz, 0} for
-    // x = -1 .. w-1 (the reference's off-by-one column -1 included); [0] reference
-    // mode, [1] quality mode.
+    // direction.  Entry (y * (w + 1) + x + 1) = {L.xyz, pdf} for x = -1 .. w-1 (the
+    // reference's off-by-one column -1 included); the direction is separable,
+    // (cos phi * sin theta, cos theta, sin phi * sin theta), so its factors come from a
+    // row table lrow[y] = (sin theta, cos theta) and a column table lcol[x + 1] =
+    // (sin phi, cos phi).  [0] reference mode, [1] quality mode.
     const float4* ltab[2];
+    const float2* lrow[2];
+    const float2* lcol[2];
 };
 // Bins per guide table.  Each bin is equally likely (val uniform), and a bin holds W / G
 // CDF entries on average, so G = 1024 leaves ~0.5 (conditional rows, W = 512) and
@@ -497,11 +505,12 @@ MCPT_HD void env_cell(const EnvView& e, const Rng& r, int& x, int& y) {
 }
 // the direction of a sampled cell (EnvironmentLight.cu:28-31: pixel corner u = x / W)
 template <bool FIXED = false>
+MCPT_HD float env_cell_u(const EnvView& e, int x) { return FIXED ? ((float)x + 0.5f) / (float)e.w : (float)x / (float)e.w; }
+template <bool FIXED = false>
+MCPT_HD float env_cell_v(const EnvView& e, int y) { return FIXED ? ((float)y + 0.5f) / (float)e.h : (float)y / (float)e.h; }
+template <bool FIXED = false>
 MCPT_HD V3 env_cell_dir(const EnvView& e, int x, int y) {
-    if (FIXED) return spherical_direction(((float)x + 0.5f) / (float)e.w, ((float)y + 0.5f) / (float)e.h);
-    float u = (float)x / (float)e.w;
-    float v = (float)y / (float)e.h;
-    return spherical_direction(u, v);
+    return spherical_direction(env_cell_u<FIXED>(e, x), env_cell_v<FIXED>(e, y));
 }
 template <bool FIXED = false>
 MCPT_HD V3 env_dir(const EnvView& e, const Rng& r) {  // EnvironmentLight.cu:10-33

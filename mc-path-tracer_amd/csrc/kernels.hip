@@ -310,15 +310,17 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
         const float4* lt = sc.env.ltab[FIXED ? 1 : 0];
         if (light_id == 0 && lt) {
             // HRDI env sample: direction, radiance and pdf are functions of the sampled cell
-            // alone, tabulated at upload by the same code (k_env_table): one 32-B fetch instead
-            // of the spherical direction, map, bilinear fetch and pdf of every sample
+            // alone, tabulated at upload by the same code (k_env_table): a 16-B cell fetch and
+            // the direction's row / column factors instead of the spherical direction, map,
+            // bilinear fetch and pdf of every sample (16 B per cell keeps the table at 2 MiB
+            // for a 512x256 map: half the L2 footprint of the previous {dir, pdf, L} cells)
             int cx, cy;
             env_cell<FIXED>(sc.env, r, cx, cy);
-            const float4* t = lt + 2 * ((int64_t)cy * (sc.env.w + 1) + cx + 1);
-            const float4 t0 = t[0], t1 = t[1];
-            ldir = xyz(t0);
+            const float4 t0 = lt[(int64_t)cy * (sc.env.w + 1) + cx + 1];
+            const float2 rs = sc.env.lrow[FIXED ? 1 : 0][cy], cs = sc.env.lcol[FIXED ? 1 : 0][cx + 1];
+            ldir = v3(cs.y * rs.x, rs.y, cs.x * rs.x);  // spherical_direction's products
             pdfl_x = t0.w;
-            Li_l = xyz(t1);
+            Li_l = xyz(t0);
         } else {
             if (light_id == 0) ldir = env_dir<FIXED>(sc.env, r);
             else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
@@ -1287,26 +1289,38 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #endif
 }
 
-// Light-sample table of an HRDI env light (EnvView::ltab): entry (y, x + 1) holds the
-// direction env_dir returns for cell (x, y), and env_L / env_pdf at that direction --
-// computed by the very functions the per-sample path calls, so the values are the same.
+// Light-sample table of an HRDI env light (EnvView::ltab / lrow / lcol): entry (y, x + 1)
+// holds env_L / env_pdf at the direction env_dir returns for cell (x, y) -- computed by the
+// very functions the per-sample path calls, so the values are the same -- and the row /
+// column tables the direction's two factors (spherical_theta / spherical_phi of the cell's
+// v / u, the arithmetic of spherical_direction).
 template <bool FIXED>
-__global__ void k_env_table(EnvView e, float4* out) {
+__global__ void k_env_table(EnvView e, float4* out, float2* row, float2* col) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int W1 = e.w + 1;
+    if (i < e.h) {
+        float st, ct;
+        spherical_theta(env_cell_v<FIXED>(e, i), st, ct);
+        row[i] = make_float2(st, ct);
+    }
+    if (i < W1) {
+        const int x = i - 1;
+        float sp, cp;
+        spherical_phi(env_cell_u<FIXED>(e, FIXED && x < 0 ? 0 : x), sp, cp);
+        col[i] = make_float2(sp, cp);
+    }
     if (i >= W1 * e.h) return;
     const int y = i / W1, x = i - y * W1 - 1;
     const V3 d = env_cell_dir<FIXED>(e, FIXED && x < 0 ? 0 : x, y);
     V3 L;
     float pdf;
     env_L_pdf<FIXED>(e, d, L, pdf);
-    out[2 * i] = make_float4(d.x, d.y, d.z, pdf);
-    out[2 * i + 1] = make_float4(L.x, L.y, L.z, 0.f);
+    out[i] = make_float4(L.x, L.y, L.z, pdf);
 }
-void launch_env_table(const EnvView& e, bool fixed_mode, float4* out, hipStream_t s) {
+void launch_env_table(const EnvView& e, bool fixed_mode, float4* out, float2* row, float2* col, hipStream_t s) {
     const int n = (e.w + 1) * e.h;
-    if (fixed_mode) hipLaunchKernelGGL(k_env_table<true>, dim3((n + 255) / 256), dim3(256), 0, s, e, out);
-    else hipLaunchKernelGGL(k_env_table<false>, dim3((n + 255) / 256), dim3(256), 0, s, e, out);
+    if (fixed_mode) hipLaunchKernelGGL(k_env_table<true>, dim3((n + 255) / 256), dim3(256), 0, s, e, out, row, col);
+    else hipLaunchKernelGGL(k_env_table<false>, dim3((n + 255) / 256), dim3(256), 0, s, e, out, row, col);
 }
 
 __global__ void k_hit_record(HitRecordArgs a) {  // stage_run(EXTEND) outputs

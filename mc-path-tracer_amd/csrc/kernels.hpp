@@ -168,7 +168,7 @@ int launch_geometry(int device, LaunchGeom& g);  // device must be current
 void launch_shade(const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fixed_mode, hipStream_t s);
 void launch_trace(const TraceArgs& a, const LaunchGeom& g, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
-void launch_env_table(const mcpt::EnvView& e, bool fixed_mode, float4* out, hipStream_t s);
+void launch_env_table(const mcpt::EnvView& e, bool fixed_mode, float4* out, float2* row, float2* col, hipStream_t s);
 // HRDI tables on the device (env_build.hip), bit-identical to the host build: scratch holds
 // env_build_scratch_floats(W, H) floats; W * H < 2^31.
 size_t env_build_scratch_floats(int W, int H);

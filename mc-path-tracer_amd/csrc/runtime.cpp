@@ -514,6 +514,8 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     s.env.tex = nullptr;
     s.env.guide_m = s.env.guide_c = nullptr;
     s.env.ltab[0] = s.env.ltab[1] = nullptr;
+    s.env.lrow[0] = s.env.lrow[1] = nullptr;
+    s.env.lcol[0] = s.env.lcol[1] = nullptr;
     if (d->env_mode == 1) {
         float4* tx;
         float *my, *cy, *pd;
@@ -577,15 +579,23 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         }
         // light-sample tables, reference and quality mode (k_env_table)
         if ((size_t)(d->env_w + 1) * d->env_h < ((size_t)1 << 28)) {
-            const size_t ne = 2 * (size_t)(d->env_w + 1) * d->env_h;
+            const size_t ne = (size_t)(d->env_w + 1) * d->env_h;
             float4 *lt0, *lt1;
-            if ((rc = dalloc(c, c->scene_bufs, &lt0, ne)) || (rc = dalloc(c, c->scene_bufs, &lt1, ne))) return rc;
-            launch_env_table(s.env, false, lt0, c->stream);
-            launch_env_table(s.env, true, lt1, c->stream);
+            float2 *rc0, *rc1;  // row table (h entries) then column table (w + 1)
+            const size_t nrc = (size_t)d->env_h + d->env_w + 1;
+            if ((rc = dalloc(c, c->scene_bufs, &lt0, ne)) || (rc = dalloc(c, c->scene_bufs, &lt1, ne)) ||
+                (rc = dalloc(c, c->scene_bufs, &rc0, nrc)) || (rc = dalloc(c, c->scene_bufs, &rc1, nrc)))
+                return rc;
+            launch_env_table(s.env, false, lt0, rc0, rc0 + d->env_h, c->stream);
+            launch_env_table(s.env, true, lt1, rc1, rc1 + d->env_h, c->stream);
             HIPCHK(c, hipGetLastError());
             HIPCHK(c, hipStreamSynchronize(c->stream));
             s.env.ltab[0] = lt0;
             s.env.ltab[1] = lt1;
+            s.env.lrow[0] = rc0;
+            s.env.lrow[1] = rc1;
+            s.env.lcol[0] = rc0 + d->env_h;
+            s.env.lcol[1] = rc1 + d->env_h;
         }
     }
     s.depth = width == 4 ? quad_push : c->pair_depth;
