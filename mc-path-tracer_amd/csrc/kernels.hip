@@ -448,10 +448,15 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         uint32_t samples = a.p.samples[pid];
         const int32_t htri = a.p.hit_tri[pid];
         const float4 b4 = a.p.beta[(((fl >> F_LEN_SHIFT) & 0xffu) > 1u) ? pid : 0u];  // len 1: beta is (1,1,1), not loaded
-        const V3 ld4 = ld3f4(a.p.Ld + pid);  // .w is always 0 (k_clear, k_resolve): xyz only
         const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
         const bool need_rd = len == 1 && htri < 0;
         const bool need_nee = len <= (uint32_t)a.max_depth && len > 1;
+        // The film is read only where the logic can add to it: a primary miss (background)
+        // or a vertex with MIS terms.  Elsewhere the update is film + 0 * beta, which leaves
+        // the film's bits unchanged (Ld is never -0: it starts at +0 and every update adds to
+        // it), so neither the load nor the store is needed.
+        const bool need_ld = !(fl & F_DEAD) && (need_rd || need_nee);
+        const V3 ld4 = ld3f4(a.p.Ld + (need_ld ? pid : 0u));  // .w is always 0 (k_clear, k_resolve): xyz only
         const V3 rd = ld3f4(a.p.ray_d + (need_rd ? pid : 0u));
         const float4 n0 = a.p.nee0[need_nee ? pid : 0u], n1 = a.p.nee1[need_nee ? pid : 0u];
         const uchar2 vv = reinterpret_cast<const uchar2*>(a.p.vis)[need_nee ? pid : 0u];
@@ -504,8 +509,9 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
                 }
             }
             // film unchanged bit for bit (a zero contribution): the store would rewrite the same bytes
-            if (__float_as_uint(film.x) != __float_as_uint(ld4.x) || __float_as_uint(film.y) != __float_as_uint(ld4.y) ||
-                __float_as_uint(film.z) != __float_as_uint(ld4.z))
+            if (need_ld && (__float_as_uint(film.x) != __float_as_uint(ld4.x) ||
+                            __float_as_uint(film.y) != __float_as_uint(ld4.y) ||
+                            __float_as_uint(film.z) != __float_as_uint(ld4.z)))
                 a.p.Ld[pid] = f4(film, 0.f);
             if (terminate) {  // :199-204
                 dead = true;

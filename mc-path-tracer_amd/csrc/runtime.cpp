@@ -776,6 +776,8 @@ static int check_ready(mcpt_ctx* c) {
     if (!c->has_scene) return set_err(c, MCPT_E_INVALID, "no scene uploaded");
     if (!c->has_cam) return set_err(c, MCPT_E_INVALID, "no camera set");
     if (!c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
+    if (!c->ext_q || !c->any_q || !c->mat_q || !c->any_ray)  // a failed (re)allocation left none
+        return set_err(c, MCPT_E_NOMEM, "ray queues not allocated");
     return MCPT_OK;
 }
 
