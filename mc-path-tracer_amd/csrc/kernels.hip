@@ -2,11 +2,13 @@
 //
 // One wavefront iteration (= one reference wavefront_pathtrace call,
 // wavefront_kernels.cu:377-442, widened from one 256x256 tile to a tile set):
-//   k_shade   fused wf_logic + wf_generate + wf_mat_mix  (wavefront_kernels.cu:90-251, 295-375)
-//   k_trace   one persistent launch for both ray sets: wf_extend closest hit
-//             (wavefront_kernels.cu:253-272, Triangle.cu:144-203) and wf_shadow + the BRDF
-//             visibility ray that the reference traces inline in wf_mat_mix
-//             (wavefront_kernels.cu:274-293, 334-336; Triangle.cu:204-243)
+//   k_shade     fused wf_logic + wf_generate, one thread per path (wavefront_kernels.cu:90-251);
+//               pushes the continuing paths as dense material records
+//   k_material  light choice + wf_mat_mix over the material records (:207-215, 295-375)
+//   k_trace     one persistent launch for both ray sets: wf_extend closest hit
+//               (wavefront_kernels.cu:253-272, Triangle.cu:144-203) and wf_shadow + the BRDF
+//               visibility ray that the reference traces inline in wf_mat_mix
+//               (wavefront_kernels.cu:274-293, 334-336; Triangle.cu:204-243)
 // The material stage evaluates the BRDF-sample terms unconditionally and the
 // visibility bit selects them in the next k_shade; this is exactly the
 // reference's result (f_brdf = Li_brdf = 0, pdf_brdf.x = pdf_light.y = 1 when
@@ -211,17 +213,16 @@ __device__ inline void hit_record(const DevScene& sc, V3 o, V3 d, int tri, V3& p
 }
 
 // ---------------------------------------------------------------------------
-// k_shade: one wavefront iteration's shading for one block of 256 pixels.
+// k_shade: the first half of one wavefront iteration's shading, for one block of
+// 256 pixels of a path slot.
 //   phase 1, one thread per pixel: wf_logic (MIS combine, throughput update,
 //     Russian roulette, termination, sample count) and wf_generate for pixels
 //     whose path ended (wavefront_kernels.cu:90-251);
-//   phase 2: the block's continuing paths are compacted through LDS (ballot +
-//     mbcnt + per-wave prefix) onto the first threads of the block, which run
-//     the light choice and wf_mat_mix (:207-215, 295-375).  Without the
-//     compaction the material code -- most of the kernel's instructions --
-//     ran with the terminating / regenerating lanes of each wave masked off.
-//   phase 3: one block-wide push of the extension rays (generated + continued)
-//     and the any-hit rays (light sample + BRDF visibility).
+//   phase 2: one block-wide push (ballot + mbcnt + per-wave LDS prefix, one atomic
+//     per queue) of the generated extension rays and of the continuing paths as
+//     material records, which k_material (below) runs densely: the light choice
+//     and wf_mat_mix are most of the shading instructions, and on the pixel-ordered
+//     threads they ran with the terminating / regenerating lanes masked off.
 // Per path the arithmetic is the reference's, so which thread evaluates a path
 // does not change any result.
 // ---------------------------------------------------------------------------
@@ -685,17 +686,17 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
 //
 // One persistent kernel traces both ray sets of an iteration: set 0 closest hit
 // (extension rays -> hit_tri), set 1 any hit (light and BRDF visibility rays ->
-// vis).  The grid is sized to the resident wave count; wave w of shard s owns
-// the shard's 64-ray chunks w, w + W, w + 2W, ... of set 0 followed by those of
-// set 1 (W waves per shard), read as one sequence, and whenever enough lanes
-// are idle at the top of the loop they take the next rays of that sequence.
-// Each loop trip a lane does one unit of work: one child-pair test, or (in the
-// wave-uniform triangle phase) one triangle of its parked leaf.  Reaching a
-// leaf parks it and traversal continues speculatively from the stack, so node
-// and triangle work are executed by full waves rather than interleaved per
-// lane.  No atomics: the split is static, balanced by the many chunks each
-// wave owns.  Stack: kLdsStack entries per lane in LDS ([entry][lane],
-// conflict-free), deeper entries in private scratch.
+// vis).  The grid is sized to the resident wave count.  The queue shards are
+// grouped into partitions (two per XCD); a partition's set-0 entries followed by
+// its set-1 entries are read as one sequence of rays, handed out by one atomic
+// counter per partition whenever enough lanes of a wave are idle at the top of
+// the loop (waves whose partition ran dry join another one; see below).  Each
+// loop trip a lane does up to kNodeSteps child-pair (or 4-wide) node tests, then
+// (in the wave-uniform triangle phase) one triangle of its parked leaf.  Reaching
+// a leaf parks it and traversal continues speculatively from the stack, so node
+// and triangle work are executed by full waves rather than interleaved per lane.
+// Stack: kLdsStack entries per lane in LDS ([entry][lane], conflict-free), deeper
+// entries in private scratch.
 // ---------------------------------------------------------------------------
 // Inclusive scan over the 64 lanes of a wave with DPP moves (no ds_bpermute address
 // registers): Hillis-Steele within each 16-lane row (row_shr 1/2/4/8; lanes shifted past
@@ -1510,7 +1511,7 @@ int launch_geometry(int dev, LaunchGeom& g) {
     }
     g.mat_blocks[0] = (uint32_t)std::max(1, cus * std::max(1, mat0) / kShards) * (uint32_t)kShards;
     g.mat_blocks[1] = (uint32_t)std::max(1, cus * std::max(1, mat1) / kShards) * (uint32_t)kShards;
-    g.refill_min = env_u32("MCPT_REFILL_MIN", 16, 1, 64);
+    g.refill_min = env_u32("MCPT_REFILL_MIN", 0, 0, 64);  // 0: per instantiation (launch_trace)
     g.tri_min = env_u32("MCPT_TRI_MIN", 16, 0, 64);
     return 0;
 }
@@ -1527,7 +1528,6 @@ void launch_shade(const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fix
 void launch_trace(const TraceArgs& args, const LaunchGeom& g, hipStream_t s) {
     if (args.nshards <= 0) return;
     TraceArgs a = args;
-    a.refill_min = g.refill_min;
     a.tri_min = g.tri_min;
     a.nparts = std::min<uint32_t>(kMaxParts, std::max<uint32_t>(1, g.trace_parts));
     a.ndies = g.ndies;
@@ -1537,6 +1537,10 @@ void launch_trace(const TraceArgs& args, const LaunchGeom& g, hipStream_t s) {
     // 16.5 ms per launch; config 2 (depth 16) 0.781 -> 0.815 ms with it, so shallow trees keep 8.
     // The node width is the scene's (DevScene::width, chosen at upload).
     const int w = a.scene.width == 4 ? 1 : 0, k = a.scene.depth > kDeepTree ? 1 : 0;
+    // Refill threshold (idle lanes before a wave takes new rays): 20 for the child-pair 8-entry
+    // instantiation (config 2, four interleaved rounds: k_trace 0.7267 -> 0.7237 ms; 8 / 12 /
+    // 24 / 28 / 32 measured 0.750 / 0.734 / 0.725 / 0.729 / 0.732), 16 for the others.
+    a.refill_min = g.refill_min ? g.refill_min : (w == 0 && k == 0 ? 20u : 16u);
     const uint32_t wps = std::max<uint32_t>(1, g.trace_waves[w][k] / nsh);
     const dim3 grid(wps * nsh), block(kTraceBlock);
     if (w == 0 && k == 0) hipLaunchKernelGGL((k_trace<2, kLdsStack>), grid, block, 0, s, a);

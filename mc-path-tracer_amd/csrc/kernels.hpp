@@ -6,8 +6,8 @@
 // here every field is a separate 16-B-aligned stream so a wave64 access is one
 // coalesced 1 KiB dwordx4 transaction:
 //   ray_o/ray_d   float4 [P]    extension ray (xyz, pad)
-//   hit_p         float4 [P]    isect.position, t
-//   hit_n         float4 [P]    isect.normal, material id (int bits, -1 = miss)
+//   hit_tri       i32    [P]    closest triangle of the extension ray (-1 = miss); the hit
+//                               record (isect) is rebuilt from it where it is consumed
 //   sray_o/sray_d float4 [2Q]   any-hit rays at their any-queue position (Q = queue entries,
 //                               allocated with the queues): written densely by k_material after
 //                               its block push, read densely by k_trace; the queue entry itself
