@@ -1537,10 +1537,20 @@ void launch_trace(const TraceArgs& args, const LaunchGeom& g, hipStream_t s) {
     // 16.5 ms per launch; config 2 (depth 16) 0.781 -> 0.815 ms with it, so shallow trees keep 8.
     // The node width is the scene's (DevScene::width, chosen at upload).
     const int w = a.scene.width == 4 ? 1 : 0, k = a.scene.depth > kDeepTree ? 1 : 0;
-    // Refill threshold (idle lanes before a wave takes new rays): 20 for the child-pair 8-entry
-    // instantiation (config 2, four interleaved rounds: k_trace 0.7267 -> 0.7237 ms; 8 / 12 /
-    // 24 / 28 / 32 measured 0.750 / 0.734 / 0.725 / 0.729 / 0.732), 16 for the others.
-    a.refill_min = g.refill_min ? g.refill_min : (w == 0 && k == 0 ? 20u : 16u);
+    // Refill threshold (idle lanes before a wave takes new rays), per instantiation, measured
+    // on the config that uses it (k_trace ms per launch, interleaved rounds on one box):
+    //   child pairs, 8-entry stack (config 2): 20 -- 0.7267 at 16, 0.7237 at 20; 8 / 12 / 24 /
+    //     28 / 32: 0.750 / 0.734 / 0.725 / 0.729 / 0.732;
+    //   child pairs, deep stack (config 4): 32 -- 16 / 24 / 28 / 32 / 40: 7.55 / 7.31 / 7.27 /
+    //     7.25 / 7.40;
+    //   4-wide, 8-entry (config 3): 24 -- 16 / 20 / 24 / 28 / 32: 1.110 / 1.105 / 1.109 / 1.106
+    //     / 1.114 (flat);
+    //   4-wide, deep stack (config 5): 24 -- 16 / 20 / 24 / 28 / 32 / 40: 15.16 / 15.14 / 14.87
+    //     / 14.88 / 14.99 / 15.61.
+    // Waves that refill less often spend fewer trips on the refill's dependent loads; too high
+    // a threshold leaves lanes idle (tools/gpu_knobs2.sh, tools/gpu_cfg_refill.sh).
+    static const uint32_t kRefill[2][2] = {{20u, 32u}, {24u, 24u}};  // [width 2/4][stack 8/deep]
+    a.refill_min = g.refill_min ? g.refill_min : kRefill[w][k];
     const uint32_t wps = std::max<uint32_t>(1, g.trace_waves[w][k] / nsh);
     const dim3 grid(wps * nsh), block(kTraceBlock);
     if (w == 0 && k == 0) hipLaunchKernelGGL((k_trace<2, kLdsStack>), grid, block, 0, s, a);
