@@ -1,5 +1,6 @@
 #!/bin/bash
-# Config-2 steady-state sweep of the refill / triangle-phase thresholds (env knobs), interleaved rounds.
+# Config-2 steady-state sweep of launch knobs (env), interleaved rounds.
+# KNOBS="label:VAR=value ..." (default: refill thresholds), ROUNDS (default 2); "base" runs with no knob.
 set -o pipefail
 mkdir -p gpurun_out
 run() {
@@ -9,7 +10,8 @@ run() {
   python -c "
 import json; d = json.load(open('gpurun_out/knob_$label.json')); print('$label', d['value'], d['stage_ms_per_step'])"
 }
-for r in 1 2; do
-  run base$r X=1
-  for k in ${REFILLS:-20 24 28 32}; do run r${k}_$r MCPT_REFILL_MIN=$k; done
+KNOBS=${KNOBS:-"r16:MCPT_REFILL_MIN=16 r24:MCPT_REFILL_MIN=24"}
+for r in $(seq ${ROUNDS:-2}); do
+  run base_$r X=1
+  for kv in $KNOBS; do run ${kv%%:*}_$r ${kv#*:}; done
 done
