@@ -626,6 +626,36 @@ def test_trace_partitions_trace_every_ray(mcpt_mod, oracle, scene_c2, nparts):
     ref.close()
 
 
+@pytest.mark.parametrize("knob", ["MCPT_REFILL_MIN=1", "MCPT_REFILL_MIN=64", "MCPT_TRI_MIN=0", "MCPT_TRI_MIN=64"])
+def test_trace_schedule_knobs_same_film(mcpt_mod, scene_c2, knob):
+    """k_trace's refill threshold (idle lanes before a wave takes new rays; per instantiation by
+    default, launch_trace) and triangle-phase threshold only schedule work: at their extremes
+    the film, sample counts and ray counts are bit-identical to the defaults'.  Both knobs are
+    read when the context is created."""
+    rc = mcpt_mod.CONFIGS[2]
+    W, H = 320, 180
+    cam = mcpt_mod.config_camera(rc, W, H)
+    ref = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 3, rc.max_depth)
+    st_ref = ref.render()
+    L_ref, s_ref = ref.film()
+    ref.close()
+    var, val = knob.split("=")
+    old = os.environ.get(var)
+    os.environ[var] = val
+    try:
+        pt = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 3, rc.max_depth)
+    finally:
+        if old is None:
+            os.environ.pop(var, None)
+        else:
+            os.environ[var] = old
+    st = pt.render()
+    L, s = pt.film()
+    assert np.array_equal(s, s_ref) and st.rays == st_ref.rays
+    assert np.array_equal(L.view(np.uint32), L_ref.view(np.uint32))
+    pt.close()
+
+
 def test_node_layouts_same_hits(mcpt_mod, oracle, scene_c2):
     """Pair-node numberings 0 (depth-first), 1 (sibling pairs, depth-first) and 2 (breadth-first)
     are layout only: bit-identical hits and visibility; out-of-range MCPT_SIBLING_LAYOUT values
