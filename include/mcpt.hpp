@@ -218,6 +218,7 @@ public:
     void make_proxy(int config_id, const std::string& asset_dir) {
         detail::check(mcpt_scene_make_proxy(s_, config_id, asset_dir.c_str()), nullptr, "Scene::make_proxy");
         proxy_env_ = true;
+        env_loaded_ = false;  // the proxy replaced the builder's environment arrays
         geometry_changed();
     }
     void add_light(std::shared_ptr<DirectionalLight> light) {  // Scene.h:53
@@ -262,14 +263,18 @@ public:
     // The returned desc points into this Scene and `dir_params`; valid until the next edit.
     mcpt_scene_desc desc(std::vector<float>& dir_params) {
         const EnvironmentLight& env = *environment_light;
-        const std::pair<const void*, uint64_t> env_key{&env, env.revision()};
-        if (!proxy_env_ && env.get_light_type() == HRDI && env_key != env_built_) {
+        // The .hdr is (re)read only when the texture path or the table source changed: the other
+        // env edits (set_ls, set_color, set_type) only change the fields desc() fills in below.
+        // The env arrays live beside the BVH in the builder, so an env reload never rebuilds
+        // the geometry (built_ stays tied to geometry and BVH-parameter edits).
+        const std::pair<std::string, bool> env_key{env.get_texture_filepath(), env.get_device_tables()};
+        if (!proxy_env_ && env.get_light_type() == HRDI && (!env_loaded_ || env_key != env_built_)) {
             if (env.get_texture_filepath().empty()) throw Error(MCPT_E_INVALID, "EnvironmentLight: HRDI without a texture");
             detail::check(mcpt_scene_set_env_hdr_ex(s_, env.get_texture_filepath().c_str(), 1,
                                                     env.get_device_tables() ? MCPT_ENV_DEVICE_TABLES : 0u),
                           nullptr, "EnvironmentLight");
             env_built_ = env_key;
-            built_ = false;
+            env_loaded_ = true;
         }
         if (!built_) {
             detail::check(mcpt_scene_build_ex(s_, &bvh_), nullptr, "Scene build");
@@ -306,7 +311,8 @@ private:
     mcpt_scene* s_;
     bool built_ = false;
     bool proxy_env_ = false;  // make_proxy set the environment (until set_environment_light)
-    std::pair<const void*, uint64_t> env_built_{nullptr, ~0ull};
+    std::pair<std::string, bool> env_built_{std::string(), false};  // texture path, device tables
+    bool env_loaded_ = false;
     mcpt_bvh_params bvh_{MCPT_BVH_SAH3, 8, 128, 0.5f, 1.0f};
 };
 

@@ -230,17 +230,17 @@ __device__ inline float union_area(float4 amn, float4 amx, float4 bmn, float4 bm
     return dx * dy + dy * dz + dz * dx;  // half the surface area (same order both ways)
 }
 
-// chgt: per cluster, tree height (low 8 bits) and interior nodes in its subtree (bits 8+)
+// chgt: per cluster, tree height and interior nodes in its subtree (ploc_pack, kernels.hpp)
 __global__ void k_ploc_init(int n, const uint32_t* __restrict__ idx, const float4* __restrict__ pmn,
                             const float4* __restrict__ pmx, int* __restrict__ cref, float4* __restrict__ cmn,
-                            float4* __restrict__ cmx, int* __restrict__ chgt) {
+                            float4* __restrict__ cmx, uint32_t* __restrict__ chgt) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t p = idx[i];
     cref[i] = (int)(0x80000000u | (uint32_t)i);  // leaf: one triangle at sorted position i
     cmn[i] = pmn[p];
     cmx[i] = pmx[p];
-    chgt[i] = 0;
+    chgt[i] = ploc_pack(0u, 0u);
 }
 
 // nearest neighbour of every cluster within +-r (boxes of the block's range + halo in LDS)
@@ -292,8 +292,8 @@ __global__ void k_ploc_mark(int nc, const int* __restrict__ nn, unsigned long lo
 __global__ void k_ploc_apply(int nc, int top, const int* __restrict__ nn, const unsigned long long* __restrict__ flag,
                              const unsigned long long* __restrict__ scan, const int* __restrict__ cref,
                              const float4* __restrict__ cmn, const float4* __restrict__ cmx,
-                             const int* __restrict__ chgt, int* __restrict__ oref, float4* __restrict__ omn,
-                             float4* __restrict__ omx, int* __restrict__ ohgt, float4* __restrict__ nodes,
+                             const uint32_t* __restrict__ chgt, int* __restrict__ oref, float4* __restrict__ omn,
+                             float4* __restrict__ omx, uint32_t* __restrict__ ohgt, float4* __restrict__ nodes,
                              int* __restrict__ ncnt) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nc) return;
@@ -313,9 +313,9 @@ __global__ void k_ploc_apply(int nc, int top, const int* __restrict__ nn, const 
         oref[pos] = k;
         omn[pos] = make_float4(fminf(amn.x, bmn.x), fminf(amn.y, bmn.y), fminf(amn.z, bmn.z), 0.f);
         omx[pos] = make_float4(fmaxf(amx.x, bmx.x), fmaxf(amx.y, bmx.y), fmaxf(amx.z, bmx.z), 0.f);
-        const int hi = chgt[i], hj = chgt[j];  // height: low 8 bits; interior count: bits 8+
-        ohgt[pos] = min(255, max(hi & 0xff, hj & 0xff) + 1) | (((hi >> 8) + (hj >> 8) + 1) << 8);
-        ncnt[k] = (hi >> 8) + (hj >> 8) + 1;
+        const uint32_t h = ploc_merge(chgt[i], chgt[j]);
+        ohgt[pos] = h;
+        ncnt[k] = (int)ploc_count(h);
     } else {
         oref[pos] = cref[i];
         omn[pos] = cmn[i];
@@ -436,7 +436,7 @@ int build_ploc(const LbvhInput& in, LbvhOutput& out, hipStream_t s) {
     if (rc) return rc;
     if (n == 1) return single_leaf(pmn, pmx, out, s);
     int* cref[2] = {tmp.get<int>(n), tmp.get<int>(n)};
-    int* chgt[2] = {tmp.get<int>(n), tmp.get<int>(n)};
+    uint32_t* chgt[2] = {tmp.get<uint32_t>(n), tmp.get<uint32_t>(n)};
     float4* cmn[2] = {tmp.get<float4>(n), tmp.get<float4>(n)};
     float4* cmx[2] = {tmp.get<float4>(n), tmp.get<float4>(n)};
     int* nn = tmp.get<int>(n);
@@ -477,15 +477,15 @@ int build_ploc(const LbvhInput& in, LbvhOutput& out, hipStream_t s) {
         cur ^= 1;
         rounds++;
     }
-    int root_h = 0;
+    uint32_t root_h = 0;
     std::vector<float4> pm(2);
-    if (hipMemcpyAsync(&root_h, chgt[cur], sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(&root_h, chgt[cur], sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(pm.data(), cmn[cur], sizeof(float4), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(pm.data() + 1, cmx[cur], sizeof(float4), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess)
         return -3;
     if (top != -1) return -5;
-    root_h &= 0xff;
+    root_h = ploc_height(root_h);
     // locality layout (as the host upload chooses: sibling pairs for trees that stay in L2)
     const int layout = (size_t)(n - 1) * 64 <= ((size_t)2 << 20) ? 1 : 0;
     const int zero = 0, one = 1;
@@ -499,7 +499,7 @@ int build_ploc(const LbvhInput& in, LbvhOutput& out, hipStream_t s) {
     }
     if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) return -3;
     out.root_ref = 0;
-    out.depth = root_h;
+    out.depth = (int)root_h;
     out.root_mn[0] = pm[0].x; out.root_mn[1] = pm[0].y; out.root_mn[2] = pm[0].z;
     out.root_mx[0] = pm[1].x; out.root_mx[1] = pm[1].y; out.root_mx[2] = pm[1].z;
     out.nnodes = n - 1;
@@ -549,7 +549,7 @@ int build_lbvh(const LbvhInput& in, LbvhOutput& out, hipStream_t s) {
             hipMemcpyAsync(pm.data() + 1, nmx, sizeof(float4), hipMemcpyDeviceToHost, s) != hipSuccess)
             return -3;
         out.root_ref = 0;
-        out.depth = root_h;  // interior levels = maximal stack pushes + 1
+        out.depth = (int)root_h;  // interior levels = maximal stack pushes + 1
     }
     if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) return -3;
     out.root_mn[0] = pm[0].x; out.root_mn[1] = pm[0].y; out.root_mn[2] = pm[0].z;

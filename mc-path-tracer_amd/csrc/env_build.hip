@@ -200,13 +200,16 @@ inline dim3 grid(size_t n) { return dim3((unsigned)((n + kB - 1) / kB)); }
 
 }  // namespace
 
-size_t env_build_scratch_floats(int W, int H) { return 2 * (size_t)W * H + 2 * (size_t)H + 4; }
+// The luminance region is rounded up to a multiple of 4 floats so that `prod` (read as float4
+// by k_env_denom) starts 16-B aligned whatever W * H is.
+static size_t env_lum_floats(int W, int H) { return ((size_t)W * H + 3) & ~(size_t)3; }
+size_t env_build_scratch_floats(int W, int H) { return env_lum_floats(W, H) + (size_t)W * H + 2 * (size_t)H + 4; }
 
 void launch_env_build(const float4* tex, int W, int H, float* scratch, float* marginal_y, float* conds_y,
                       float* pdf, hipStream_t s) {
     const size_t n = (size_t)W * H;
     float* lum = scratch;
-    float* prod = lum + n;
+    float* prod = lum + env_lum_floats(W, H);
     float* srow = prod + n;
     float* mp = srow + H;
     float* denom = mp + H;

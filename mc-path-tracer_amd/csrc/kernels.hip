@@ -193,14 +193,12 @@ __device__ inline void hit_record(const DevScene& sc, V3 o, V3 d, int tri, V3& p
     const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
     const float4* sp4 = sc.tri_sh + 3 * tri;
     const float4 s0 = sp4[0], s1 = sp4[1], s2 = sp4[2];
-#ifndef MCPT_X_LAZY_V0
     // All six loads in one round trip: the compiler otherwise issues the vertex load after
     // the determinant test and the shading record after the whole test (three serialised
     // fetches; the hit is known to exist, so every value is used).
     __asm__ volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w),
                      "v"(w2.x), "v"(s0.x), "v"(s0.y), "v"(s0.z), "v"(s0.w), "v"(s1.x), "v"(s1.y), "v"(s1.z),
                      "v"(s1.w), "v"(s2.x), "v"(s2.y));
-#endif
     float t, u, v;
     tri_test(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t, u, v);
     const V3 n0 = v3(s0.x, s0.y, s0.z), n1 = v3(s0.w, s1.x, s1.y), n2 = v3(s1.z, s1.w, s2.x);
@@ -341,13 +339,9 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
             a.p.vis[2 * pid] = 1;
             mo.trivial_any++;
         } else {
-#ifndef MCPT_SPARSE_ANY  // staged: stored at its any-queue position after the block push
+            // staged: stored at its any-queue position after the block push
             stage[0 * kBlock + threadIdx.x] = f4(so_l, 0.f);
             stage[1 * kBlock + threadIdx.x] = f4(ldir, 0.f);
-#else
-            a.p.sray_o[2 * pid] = f4(so_l, 0.f);
-            a.p.sray_d[2 * pid] = f4(ldir, 0.f);
-#endif
             mo.want_l = true;
         }
     }
@@ -372,13 +366,8 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
             a.p.vis[2 * pid + 1] = 1;
             mo.trivial_any++;
         } else {
-#ifndef MCPT_SPARSE_ANY
             stage[2 * kBlock + threadIdx.x] = f4(so_b, 0.f);
             stage[3 * kBlock + threadIdx.x] = f4(wi_b, 0.f);
-#else
-            a.p.sray_o[2 * pid + 1] = f4(so_b, 0.f);
-            a.p.sray_d[2 * pid + 1] = f4(wi_b, 0.f);
-#endif
             mo.want_b = true;
         }
     }
@@ -632,18 +621,14 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
         if (mo.want_l) {
             const uint32_t k = shard * a.any_cap + slot[1];
             a.any_q[k] = 2 * mpid;
-#ifndef MCPT_SPARSE_ANY
             a.p.sray_o[k] = s_any[0][threadIdx.x];
             a.p.sray_d[k] = s_any[1][threadIdx.x];
-#endif
         }
         if (mo.want_b) {
             const uint32_t k = shard * a.any_cap + slot[2];
             a.any_q[k] = 2 * mpid + 1;
-#ifndef MCPT_SPARSE_ANY
             a.p.sray_o[k] = s_any[2][threadIdx.x];
             a.p.sray_d[k] = s_any[3][threadIdx.x];
-#endif
         }
         n_ext += (mo.want_ext || mo.trivial_ext) ? 1u : 0u;  // queued + resolved-in-place rays
         n_any += (mo.want_l ? 1u : 0u) + (mo.want_b ? 1u : 0u) + mo.trivial_any;
@@ -884,9 +869,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     uint64_t prof[12] = {};  // see mcpt_debug_trace_profile
 #endif
     uint64_t drained = 0;  // partitions this wave saw run dry (by an atomic: never stale)
-#ifdef MCPT_X_PREFETCH
-    uint32_t pfx = 0;
-#endif
     for (;;) {  // one trip per partition joined
     // Per-lane ray state is declared per partition trip: when the trip ends no lane holds a
     // ray, so none of it is live across the partition scan below (VGPR budget).
@@ -901,25 +883,19 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     int ref = kEnd, leaf = kEnd, sp = 0, tri = -1;
     bool fin = true;  // inverse direction finite: pair_slab() is exact
     float best = K_HUGE, cut = K_HUGE;
-#ifndef MCPT_X_NOSPILL
     int2 spill[kMaxStack - kLdsStack];
-#endif
     // Pop the next entry still in front of the current cut (any-hit rays keep
     // cut = K_HUGE * (1 + 2^-8), so for them every entry is taken).
     auto pop = [&]() -> int {
         while (sp > 0) {
             sp--;
             int2 e;
-#ifndef MCPT_X_NOSPILL
             if (sp < kLdsStack) {
                 e = stk[sp][lane];
             } else {
                 e = spill[sp - kLdsStack];
                 __asm__ volatile("" : "+v"(e.x), "+v"(e.y));  // keep the LDS load an LDS load (no flat merge)
             }
-#else
-            e = stk[sp < kLdsStack ? sp : kLdsStack - 1][lane];
-#endif
             if (__int_as_float(e.y) > cut) continue;
             return e.x;
         }
@@ -1004,9 +980,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     // positions) issues its ray loads with the queue-entry load, not after it
                     const bool at_slot = kind ? a.set[1].ray_at_slot : a.set[0].ray_at_slot;
                     rid = at_slot ? qslot : (qp ? qp[qslot] : qslot);
-#ifdef MCPT_X_EXTRA_HOP  // experiment: one more dependent load before the ray loads (refill latency cost)
-                    rid += a.vis[rid] == 0x7bu ? 1u : 0u;
-#endif
                     const float4 o4 = rop[rid], d4 = rdp[rid];
                     if (at_slot && qp) rid = qp[qslot];  // the result index, needed only when the ray finishes
                     o = xyz(o4);
@@ -1068,9 +1041,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         if (act) {
 #pragma unroll 1
           for (int it = 0; it < kNodeSteps; it++) {
-#ifdef MCPT_X_ANYWAIT  // experiment: an any-hit lane with a parked leaf waits for its triangle test
-            if (kind != 0 && leaf != kEnd) break;
-#endif
             bool need_pop = false;
             if (ref >= 0) {
               RAY_STEP_NODE();
@@ -1121,12 +1091,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     for (int k = 3; k >= 1; k--) {
                         if (rr[k] != kEnd) {
                             const int2 e = make_int2(rr[k], __float_as_int(key[k]));
-#ifndef MCPT_X_NOSPILL
                             if (sp < kLdsStack) stk[sp][lane] = e;
                             else spill[sp - kLdsStack] = e;
-#else
-                            stk[sp < kLdsStack ? sp : kLdsStack - 1][lane] = e;
-#endif
                             sp++;
                         }
                     }
@@ -1135,21 +1101,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
               } else {
                 const float4* nd = sc.nodes + 4 * ref;
                 const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-#ifdef MCPT_X_PREFETCH  // experiment: touch both children (node line or triangle record) before the slab
-                {
-                    const int p0 = __float_as_int(q3.x), p1 = __float_as_int(q3.y);
-                    const uint32_t* w0 = p0 >= 0 ? (const uint32_t*)(sc.nodes + 4 * p0) : (const uint32_t*)(sc.tri + kTriF4 * (p0 & 0xffffff));
-                    const uint32_t* w1 = p1 >= 0 ? (const uint32_t*)(sc.nodes + 4 * p1) : (const uint32_t*)(sc.tri + kTriF4 * (p1 & 0xffffff));
-                    pfx ^= w0[0] ^ w1[0];
-                }
-#endif
-#ifdef MCPT_X_EXTRA_FETCH  // experiment: +50% node bytes (the neighbouring node's first half)
-                {
-                    const float4* xn = sc.nodes + 4 * (ref > 0 ? ref - 1 : ref);
-                    const float4 x0 = xn[0], x1 = xn[1];
-                    if (x0.x == 1234.5f && x1.w == 9876.5f) ref = kEnd;
-                }
-#endif
                 float a0, b0, a1, b1;
                 bool h0, h1;
                 // node layout (SoA pairs): q0 = (mn.x, mn.x', mx.x, mx.x'), q1 = y, q2 = z,
@@ -1169,12 +1120,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 if (h0 && h1) {
                     const bool first0 = !(a1 < a0);
                     const int2 e = make_int2(first0 ? c1 : c0, __float_as_int(first0 ? a1 : a0));
-#ifndef MCPT_X_NOSPILL
                     if (sp < kLdsStack) stk[sp][lane] = e;
                     else spill[sp - kLdsStack] = e;
-#else
-                    stk[sp < kLdsStack ? sp : kLdsStack - 1][lane] = e;
-#endif
                     sp++;
                     ref = first0 ? c0 : c1;
                 } else {
@@ -1210,13 +1157,11 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 const int id = leaf & 0xffffff;
                 const float4* tp = sc.tri + kTriF4 * id;
                 const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-#ifndef MCPT_X_LAZY_V0
                 // One memory round trip per test: without this the compiler sinks the vertex
                 // load (w0.xyz) below the determinant test, so every front-facing test waits
                 // for a second, dependent fetch of the same record.
                 __asm__ volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z),
                                  "v"(w1.w), "v"(w2.x), "v"(w2.y));
-#endif
                 RAY_STEP_TRI();
                 tot_t++;
                 float t;
@@ -1251,9 +1196,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #endif
         if (act && ref == kEnd && leaf == kEnd) finish();
     }
-#ifdef MCPT_X_NOSTEAL  // experiment: home partition only (round 1's scheme: needs a wave on every die)
-    break;
-#endif
     // ---- partition scan: read every counter (one lane each) and join the first
     // partition after the current one that still holds rays.  A stale read (this die's
     // L2 holding an old copy of a counter line) can only be lower than the true count, so
@@ -1266,25 +1208,17 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         if (cand) g = __hip_atomic_load(a.grab + lane * C_WORDS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t open = __ballot(cand && g < s_tot[lane]);
         if (open == 0) break;  // every partition drained
-#ifndef MCPT_X_PICK_NEXT
         // the open partition with the most rays left (lowest index on ties): waves that
         // run dry spread over the remaining work instead of queueing on one counter
         const uint32_t rem = min(s_tot[lane] - g, (1u << 25) - 1u);
         uint32_t key = (open >> lane) & 1ull ? (rem << 6) | (63u - (uint32_t)lane) : 0u;
         for (int off = 32; off > 0; off >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, off));
         enter(63u - (__builtin_amdgcn_readfirstlane(key) & 63u));
-#else  // experiment: the first open partition after the current one
-        const uint64_t after = open & ~((2ull << part) - 1ull);  // partitions past the current one
-        enter((uint32_t)__builtin_ctzll(after ? after : open));
-#endif
     }
     }
 #ifdef MCPT_TRACE_PROF
     if (lane == 0)
         for (int i = 0; i < 12; i++) atomicAdd(&g_trace_prof[i], (unsigned long long)prof[i]);
-#endif
-#ifdef MCPT_X_PREFETCH
-    if (a.refill_min == 1000u && pfx == 0x9e3779b9u) a.hit_tri[0] = 0;  // keeps the touches (never true)
 #endif
     wave_stats(a.set[0].stats, lane, tot_n - tot_n1, tot_t - tot_t1, tot_h - tot_h1);
     wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);

@@ -12,7 +12,6 @@
 //                               allocated with the queues): written densely by k_material after
 //                               its block push, read densely by k_trace; the queue entry itself
 //                               holds the result index 2p (light sample) / 2p+1 (BRDF visibility).
-//                               (MCPT_SPARSE_ANY: the previous layout, [2P] indexed 2p / 2p+1)
 //   beta          float4 [P]    throughput, (f_sample/pdf_sample).x
 //   nee0 / nee1   float4 [P]    precomputed light / BRDF MIS terms, ratio .y / .z
 //   flags         u32    [P]    dead, len, MIS condition bits
@@ -186,6 +185,19 @@ struct LbvhOutput {
     int nnodes = 0, root_ref = 0, depth = 0, rounds = 0;
     float root_mn[3], root_mx[3];
 };
+// PLOC cluster record: subtree height (low 8 bits, saturated at 255) and the subtree's
+// interior-node count (bits 8..31).  Unsigned with logical shifts: a count below 2^24 (every
+// scene mcpt_scene_upload accepts) packs and unpacks exactly (tests/native/core_identities.cpp).
+__host__ __device__ constexpr uint32_t ploc_pack(uint32_t height, uint32_t count) {
+    return (height < 255u ? height : 255u) | (count << 8);
+}
+__host__ __device__ constexpr uint32_t ploc_height(uint32_t h) { return h & 0xffu; }
+__host__ __device__ constexpr uint32_t ploc_count(uint32_t h) { return h >> 8; }
+// the record of a merge of clusters a and b
+__host__ __device__ constexpr uint32_t ploc_merge(uint32_t a, uint32_t b) {
+    return ploc_pack((ploc_height(a) > ploc_height(b) ? ploc_height(a) : ploc_height(b)) + 1u,
+                     ploc_count(a) + ploc_count(b) + 1u);
+}
 int build_lbvh(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
 int build_ploc(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
 int trace_profile(unsigned long long* out, int reset);

@@ -668,10 +668,8 @@ static int set_tiles_internal(mcpt_ctx* c, const std::vector<int2>& t) {
             return set_err(c, MCPT_E_NOMEM, "queue allocation failed");
         c->queue_alloc = need;
     }
-#ifndef MCPT_SPARSE_ANY
     c->p.sray_o = c->any_ray;  // indexed by any-queue position (kShards * any_cap = 2 * need entries)
     c->p.sray_d = c->any_ray + 2 * c->queue_alloc;
-#endif
     if (t.size() > c->tiles_cap) {
         if (c->tiles) HIPCHK(c, hipFree(c->tiles));
         c->tiles = nullptr;
@@ -720,9 +718,6 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
     int rc;
     if ((rc = dalloc(c, c->film_bufs, &p.ray_o, P)) || (rc = dalloc(c, c->film_bufs, &p.ray_d, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.hit_tri, P)) ||
-#ifdef MCPT_SPARSE_ANY
-        (rc = dalloc(c, c->film_bufs, &p.sray_o, 2 * P)) || (rc = dalloc(c, c->film_bufs, &p.sray_d, 2 * P)) ||
-#endif
         (rc = dalloc(c, c->film_bufs, &p.beta, P)) || (rc = dalloc(c, c->film_bufs, &p.nee0, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.nee1, P)) || (rc = dalloc(c, c->film_bufs, &p.Ld, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.flags, P)) || (rc = dalloc(c, c->film_bufs, &p.samples, P)) ||
@@ -830,9 +825,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     v.shard_cap = c->any_cap;
     v.stats = &c->cnt->shard[0][C_STATS + 3];
     v.prefiltered = 1;
-#ifndef MCPT_SPARSE_ANY
     v.ray_at_slot = 1;  // k_material stores the any-hit rays at their queue positions
-#endif
     ta.hit_tri = c->p.hit_tri;
     ta.vis = c->p.vis;
     ta.grab = &c->cnt->grab[0][0];  // reset by k_accumulate below

@@ -370,8 +370,11 @@ class PathTracer:
         mcpt_scene_upload_gpu_bvh (BVH built on the device, PLOC by default; same hits)."""
         d = scene.desc() if isinstance(scene, Scene) else scene
         if gpu_bvh:
-            if gpu_bvh in ("ploc", "lbvh"):
-                self._ck(lib().mcpt_set_gpu_bvh_builder(self.h, 1 if gpu_bvh == "ploc" else 0))
+            if gpu_bvh not in (True, "ploc", "lbvh"):
+                raise ValueError(f"unknown GPU BVH builder {gpu_bvh!r}")
+            # True is the documented default (PLOC), set explicitly: the builder is context state,
+            # so an earlier "lbvh" upload must not carry over
+            self._ck(lib().mcpt_set_gpu_bvh_builder(self.h, 0 if gpu_bvh == "lbvh" else 1))
             self._ck(lib().mcpt_scene_upload_gpu_bvh(self.h, C.byref(d)))
         else:
             self._ck(lib().mcpt_scene_upload(self.h, C.byref(d)))
@@ -411,7 +414,7 @@ class PathTracer:
         self._ck(lib().mcpt_set_path_slots(self.h, slots))
 
     def set_trace_partitions(self, nparts=0):
-        """k_trace work partitions (mcpt_set_trace_partitions); 0 = one per XCD of the device."""
+        """k_trace work partitions (mcpt_set_trace_partitions); 0 = the device default, two per XCD."""
         self._ck(lib().mcpt_set_trace_partitions(self.h, nparts))
 
     def set_tiles(self, tiles=None):

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "device/mcpt_core.hpp"
+#include "kernels.hpp"
 
 using namespace mcpt;
 
@@ -165,6 +166,24 @@ int main() {
     }
     std::printf("hard quotients %ld, broken by a 2^-45 reciprocal error %ld\n", hard, broken);
     if (hard < 100000 || broken == 0) { std::printf("hard-case generator ineffective\n"); bad++; }
+    // PLOC cluster records (bvh_build.hip): height and interior-node count round-trip for every
+    // subtree size of a scene mcpt_scene_upload accepts (< 2^24 triangles: at most 2^24 - 2
+    // interior nodes), including the merge of two halves of the largest tree
+    {
+        using namespace mcpt_dev;
+        const uint32_t nmax = (1u << 24) - 2u;
+        for (uint32_t c : {0u, 1u, 255u, 256u, (1u << 23) - 1u, 1u << 23, (1u << 23) + 7u, nmax - 1u, nmax}) {
+            for (uint32_t h : {0u, 1u, 17u, 254u, 255u, 300u}) {
+                const uint32_t p = ploc_pack(h, c);
+                if ((ploc_count(p) != c || ploc_height(p) != (h < 255u ? h : 255u)) && bad++ < 5)
+                    std::printf("ploc_pack(%u, %u) -> %u %u\n", h, c, ploc_height(p), ploc_count(p));
+            }
+        }
+        const uint32_t a = ploc_pack(30, (nmax - 1u) / 2u), b = ploc_pack(40, nmax - 1u - (nmax - 1u) / 2u);
+        const uint32_t m = ploc_merge(a, b);
+        if ((ploc_count(m) != nmax || ploc_height(m) != 41u) && bad++ < 5)
+            std::printf("ploc_merge: %u %u\n", ploc_height(m), ploc_count(m));
+    }
     std::printf("bad=%ld\n", bad);
     return bad != 0;
 }

@@ -852,7 +852,7 @@ def _env_only(a, tex):
     return b
 
 
-@pytest.mark.parametrize("shape", ["c2", (77, 300), (512, 1024), "zeros", "spike"])
+@pytest.mark.parametrize("shape", ["c2", (77, 300), (77, 301), (512, 1024), "zeros", "spike"])
 def test_env_tables_built_on_device_equal_oracle(mcpt_mod, oracle, scene_c2, shape):
     """build_environment_light (light_initialization_kernels.cu:3-161) on the device: marginal,
     conditional and pdf tables equal the oracle's or_env_build for the config-2 map and synthetic
