@@ -2,19 +2,24 @@
 
 Workload (BASELINE.json configs[1]): 1920x1080, 256 spp, depth 5, MIS on, env importance sampling,
 Cornell-box + 5 spheres proxy for the missing scene_show_off_spheres.glb lit by
-night_free_Env.hdr.  A *step* is one wavefront iteration (the reference's wavefront_pathtrace,
-wavefront_kernels.cu:377-442: logic+generate+material -> extend -> shadow) over every pixel the
-rank owns; paths are in steady state after the warmup.  Three paths are in flight per pixel
-(mcpt_set_path_slots: slot k renders samples k, k+3, ...; same per-sample results, films equal to
-fp32 summation order -- tests/test_gpu.py::test_path_slots_*): 6.2 M paths per iteration amortise
-each launch's ramp-up and drain (+15 % over one path per pixel, measured).  value = (extension + shadow + BRDF
-visibility rays of all ranks) / (max over ranks of the timed wall time).
+night_free_Env.hdr.  A *step* is one whole frame, the literal workload of the metric: the film is
+cleared (g_clear_dfilm, wavefront_kernels.cu:55-76) and every pixel the rank owns is rendered to
+256 spp by repeated wavefront iterations (wavefront_pathtrace, wavefront_kernels.cu:377-442:
+logic+generate+material -> extend -> shadow), startup and tail iterations included.  value =
+(extension + shadow + BRDF visibility rays of all ranks) / (max over ranks of the timed wall time).
+Three paths are in flight per pixel (mcpt_set_path_slots; BENCH_SLOTS per config); films equal
+the one-path-per-pixel oracle's within the north star's 1e-4 (tests/test_bench_layout.py runs
+this exact layout).  `--steady` reports the steady-state iteration rate beside it.
 
-Multi-GPU: one process per GPU (torch.distributed.run), weak scaling: the film is 1920 x 1080*N
-pixels of the same 16:9 view (the config-2 camera; N-fold vertical supersampling), and 256x256
-tiles are dealt to ranks by (tx + ty) mod N, so every rank owns ~one 1080p frame of pixels with
-the same image content (sky / geometry mix) as the 1-GPU run.  No collective runs inside the timed region (tiles are independent); the RCCL gather of
-the film is a separate, untimed step (mcpt/parallel.py).
+Multi-GPU: one process per GPU.  `--gpus N` without an external launcher starts
+the N ranks itself (torch.distributed.run, before anything touches the GPU); under a launcher
+WORLD_SIZE must equal N.  256x256 tiles are dealt to ranks by (tx + ty) mod N.
+  --scaling weak (default): the frame is 1920 x 1080*N pixels of the same view (N-fold vertical
+      supersampling), so every rank owns ~one 1080p frame of pixels with the same sky / geometry
+      mix as the 1-GPU run;
+  --scaling strong: the config's own frame (e.g. --config 4: 3840x2160) split over the ranks.
+No collective runs inside the timed region (tiles are independent); `--gather` sends every
+rank's tile pixels to rank 0's device film after timing (mcpt/parallel.py, RCCL send/recv).
 """
 from __future__ import annotations
 
@@ -22,6 +27,8 @@ import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,26 +45,39 @@ B_TRI = 36            # per ray/triangle test
 B_HIT = 40            # per closest hit: 3 normals + material id
 B_SHADE = 195 + 172   # logic + material per path-bounce
 B_GEN = 49            # generate per new sample
+# Path slots (paths in flight per pixel) per BASELINE config: the measured best of
+# tools/configs.py; the parity tests run the same layout.
+BENCH_SLOTS = {1: 16, 2: 3, 3: 3, 4: 4, 5: 4}
+STEP = "frame"  # what one step is; stamped into the PMC summaries (tools/pmc.py)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)
-    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=5, help="timed frames")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed frames before the timed ones")
     ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--spp", type=int, default=None, help="override the config's spp (not the BASELINE workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=12, help="spp of the full-frame CPU-oracle sample")
-    ap.add_argument("--gather", action="store_true", help="RCCL-gather the film after timing (N>1)")
-    ap.add_argument("--no-full-frame", action="store_true", help="skip the untimed-by-value full 256-spp frame")
-    ap.add_argument("--slots", type=int, default=int(os.environ.get("MCPT_BENCH_SLOTS", "3")),
-                    help="paths in flight per pixel (mcpt_set_path_slots)")
-    return ap.parse_args()
+    ap.add_argument("--gather", action="store_true", help="gather the film on rank 0 after timing (N>1)")
+    ap.add_argument("--steady", action="store_true",
+                    help="also time 60 steady-state iterations (outside value; off by default so that every "
+                         "k_trace launch of the process belongs to a timed or warmup frame, as rocprofv3 sees it)")
+    ap.add_argument("--slots", type=int, default=int(os.environ["MCPT_BENCH_SLOTS"]) if "MCPT_BENCH_SLOTS" in os.environ else None,
+                    help="paths in flight per pixel (mcpt_set_path_slots); default BENCH_SLOTS[config]")
+    return ap.parse_args(argv)
 
 
 def tiles_for(rank, world, W, H, tile):
     nx, ny = (W + tile - 1) // tile, (H + tile - 1) // tile
     return [(tx, ty) for ty in range(ny) for tx in range(nx) if (tx + ty) % world == rank]
+
+
+def frame_size(rc, world, scaling):
+    """The rendered frame: the config's view, N-fold taller under weak scaling."""
+    return (rc.width, rc.height * world) if scaling == "weak" else (rc.width, rc.height)
 
 
 KERNEL_SOURCES = ("mc-path-tracer_amd/csrc/kernels.hip", "mc-path-tracer_amd/csrc/kernels.hpp",
@@ -77,22 +97,26 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
-def pmc_summary(config, slots):
-    """The newest committed rocprofv3 PMC summary (profiles/pmc_*.json) and whether it was
-    measured on this code (source hash) and this workload (config, path slots)."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json")))
+def pmc_summary(config, slots, kind="pmc"):
+    """The newest committed rocprofv3 summary profiles/<kind>_*.json (kind "pmc": FETCH/WRITE
+    traffic, "pmcdetail": SQ/TCC counters) and whether it was measured on this code (source hash)
+    and this workload (config, path slots, step)."""
+    files = sorted(f for f in glob.glob(os.path.join(REPO, "profiles", f"{kind}_*.json"))
+                   if os.path.basename(f)[len(kind) + 1:][:1] == "r")
     if not files:
-        return None, "no PMC summary in profiles/"
+        return None, f"no {kind} summary in profiles/"
     try:
         d = json.load(open(files[-1]))
     except Exception as e:  # noqa: BLE001
-        return None, f"unreadable PMC summary: {e}"
+        return None, f"unreadable {kind} summary: {e}"
     stamp = d.get("stamp", {})
     why = []
     if stamp.get("source_hash") != source_hash():
         why.append("kernel sources changed since it was taken")
     if stamp.get("config") != config or stamp.get("slots") != slots:
         why.append(f"taken on config {stamp.get('config')} / {stamp.get('slots')} slots")
+    if stamp.get("step", "iteration") != STEP:
+        why.append(f"taken with {stamp.get('step', 'iteration')} steps")
     return d, ("; ".join(why) or None)
 
 
@@ -106,31 +130,164 @@ def pmc_traffic(summary, kernel_prefix):
     return int(sum(got)) if got and None not in got else None
 
 
+def pmc_detail(summary, kernel_prefix):
+    """Counter ratios of one kernel from a fresh pmcdetail summary (tools/pmc_detail.py)."""
+    if not summary:
+        return None
+    for k, v in summary.get("kernels", {}).items():
+        if any(k.startswith(p) or k.startswith("void " + p) for p in kernel_prefix):
+            return v.get("ratios")
+    return None
+
+
+def cpu_threads():
+    """Host threads for the CPU baseline: the cores this process may run on, capped at the GPU
+    box's per-GPU CPU share (OMP_NUM_THREADS, 16 there; os.cpu_count() shows the whole host)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
+
+
 def cpu_baseline(scene_arrays, cam, W, H, spp, max_depth):
     """Oracle (scalar C port of the reference kernels) on the host cores: the full frame at a few spp."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_py  # checker/baseline only
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     t = time.perf_counter()
     _, _, cnt = oracle_py.render(scene_arrays, cam, W, H, spp=spp, max_depth=max_depth, nthreads=threads)
     dt = time.perf_counter() - t
     rays = cnt["extend_rays"] + cnt["shadow_rays"] + cnt["vis_rays"]
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(),
             "sample": f"oracle/ (scalar C restatement of the reference kernels, -O2, literal stack traversal, "
-                      f"{threads} std threads over 256x256 tiles): the full {W}x{H} frame at {spp} spp, "
-                      f"{rays} rays in {dt:.1f} s"}
+                      f"{threads} std threads over 256x256 tiles = every core this process may use, capped at "
+                      f"the box's per-GPU share OMP_NUM_THREADS; host has {os.cpu_count()} CPUs): the full "
+                      f"{W}x{H} frame at {spp} spp, {rays} rays in {dt:.1f} s"}
+
+
+def spawn_ranks(args):
+    """`--gpus N` without a launcher: start N ranks with torch.distributed.run as a child process
+    (nothing has touched the GPU yet) and exit with its status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+class Acc:
+    """Sum of StageStats over frames."""
+    KEYS = ("extend_rays", "shadow_rays", "vis_rays", "iterations", "ms_shade", "ms_extend",
+            "ext_nodes", "ext_tests", "ext_hits", "any_nodes", "any_tests", "any_hits")
+
+    def __init__(self):
+        for k in self.KEYS:
+            setattr(self, k, 0)
+
+    def add(self, st):
+        for k in self.KEYS:
+            setattr(self, k, getattr(self, k) + getattr(st, k))
+
+    @property
+    def rays(self):
+        return int(self.extend_rays + self.shadow_rays + self.vis_rays)
+
+
+def roofline(st, ms_trace, ms_shade, config, slots):
+    """roofline object of the dominant kernel (k_trace) and of the shading stages.
+
+    achieved = SURVEY.md 8(d)'s algorithmic bytes that live in HBM: the per-ray state (65 B per
+    extension ray, 33 B per any-hit ray) times the rays of a launch, over the launch time.  The
+    traversal's node and triangle bytes (8(d)'s B_bvh) are reported separately as cache-served
+    bytes: they run at several times the HBM peak, so they come from L1 / L2 / MALL (their own
+    roof is the L2's).  traffic = measured HBM bytes per launch from the committed rocprofv3 PMC
+    summary (profiles/pmc_r*.json) when it was taken on this code and workload.  bound = the
+    resource with the highest measured utilisation (HBM traffic, L2 bytes, VALU issue), or
+    "latency" when none reaches 0.5."""
+    n = max(1, st.iterations)
+    avg_s = ms_trace / n * 1e-3
+    ext_q = st.extend_rays
+    any_q = st.shadow_rays + st.vis_rays
+    state = (B_EXT_STATE * ext_q + B_ANY_STATE * any_q) / n
+    bvh = (2 * B_NODE * (st.ext_nodes + st.any_nodes) + B_TRI * (st.ext_tests + st.any_tests) + B_HIT * st.ext_hits) / n
+    achieved = state / avg_s
+    names = {"k_trace": ("mcpt_dev::k_trace<",), "shade": ("mcpt_dev::k_shade<", "mcpt_dev::k_material<")}
+    summary, stale = pmc_summary(config, slots)
+    fresh = summary if stale is None else None
+    detail, dstale = pmc_summary(config, slots, "pmcdetail")
+    dfresh = detail if dstale is None else None
+    traffic = pmc_traffic(fresh, names["k_trace"])
+    roof = {"bound": None, "kernel": "k_trace", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
+            "avg_launch_ms": round(ms_trace / n, 4), "launches": int(n),
+            "algorithmic_bytes_per_launch": int(state),
+            "algorithmic": "SURVEY 8(d) per-ray state bytes (65 B extension, 33 B any-hit) x rays per launch",
+            "cache_served": {"bytes_per_launch": int(bvh), "GBps": round(bvh / avg_s / 1e9, 1),
+                             "l2_peak_GBps": L2_PEAK / 1e9, "l2_frac": round(bvh / avg_s / L2_PEAK, 4),
+                             "what": "SURVEY 8(d) B_bvh: 64 B per child-pair node step, 36 B per triangle "
+                                     "test, 40 B per closest hit (logical; served by L1/L2/MALL)"},
+            "per_ray": {"ext_pair_nodes": round(st.ext_nodes / max(1, ext_q), 2),
+                        "ext_tri_tests": round(st.ext_tests / max(1, ext_q), 2),
+                        "any_pair_nodes": round(st.any_nodes / max(1, any_q), 2),
+                        "any_tri_tests": round(st.any_tests / max(1, any_q), 2)}}
+    util = {"l2": roof["cache_served"]["l2_frac"]}
+    if traffic is not None:
+        roof["traffic_GBps"] = round(traffic / avg_s / 1e9, 1)
+        roof["traffic_frac"] = round(traffic / avg_s / HBM_PEAK, 4)
+        util["hbm"] = roof["traffic_frac"]
+    else:
+        roof["pmc_stale"] = stale
+        util["hbm"] = roof["frac"]
+    r = pmc_detail(dfresh, names["k_trace"])
+    if r:
+        roof["counters"] = r
+        if "valu_busy" in r:
+            util["valu"] = r["valu_busy"]
+    elif dstale:
+        roof["counters_stale"] = dstale
+    roof["utilisation"] = util
+    top = max(util, key=util.get)
+    roof["bound"] = top if util[top] >= 0.5 else "latency"
+    why = [f"{k} {v:.2f}" for k, v in sorted(util.items(), key=lambda kv: -kv[1])]
+    roof["binding"] = (f"utilisation {', '.join(why)}" +
+                       (f"; waves wait on memory {r['wait_frac']:.2f} of their cycles, VALU lane "
+                        f"utilisation {r['lane_util']:.2f}" if r and "wait_frac" in r else ""))
+    # the streaming stages (logic + generate + material: k_shade and k_material) on their own
+    t_shd = ms_shade / n * 1e-3
+    b_shd = (B_SHADE * st.shadow_rays + B_GEN * max(0, st.extend_rays - st.shadow_rays)) / n
+    shade = {"ms_per_iteration": round(ms_shade / n, 4), "state_bytes_per_iteration": int(b_shd),
+             "state_frac": round(b_shd / t_shd / HBM_PEAK, 4) if t_shd > 0 else None}
+    shd_traffic = pmc_traffic(fresh, names["shade"])
+    if shd_traffic is not None and t_shd > 0:
+        shade["traffic"] = shd_traffic
+        shade["traffic_frac"] = round(shd_traffic / t_shd / HBM_PEAK, 4)
+    roof["shade_stages"] = shade
+    return roof
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+              f"(or run without a launcher and let --gpus start the ranks)", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1 and os.environ.get("MCPT_BENCH_NO_TORCH") == "1":
-        torch = None
-    else:
-        import torch
+    import torch
 
     dist = None
     # MCPT_BENCH_BACKEND=gloo + MCPT_BENCH_SHARE_GPU=1: rehearse the N-rank path on a 1-GPU box
@@ -146,66 +303,74 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    import numpy as np
 
     import mcpt
 
     rc = mcpt.CONFIGS[args.config]
-    W, H = rc.width, rc.height * world
+    slots = args.slots or BENCH_SLOTS[args.config]
+    spp = args.spp or rc.spp
+    W, H = frame_size(rc, world, args.scaling)
     scene = mcpt.build_config_scene(args.config)
-    cam = mcpt.config_camera(rc, rc.width, rc.height)  # the 1080p view at any N (see docstring)
-    pt = mcpt.PathTracer(local, mcpt.default_config(spp=rc.spp, max_depth=rc.max_depth))
+    cam = mcpt.config_camera(rc, rc.width, rc.height)  # the config's view at any N (see docstring)
+    pt = mcpt.PathTracer(local, mcpt.default_config(spp=spp, max_depth=rc.max_depth))
     pt.upload_scene(scene)
     pt.set_camera(cam)
-    pt.set_path_slots(args.slots)
+    pt.set_path_slots(slots)
     pt.resize(W, H)
     my_tiles = tiles_for(rank, world, W, H, 256)
     pt.set_tiles(my_tiles)
 
-    pt.iterate(args.warmup)
+    def frame():
+        pt.clear()
+        return pt.render()  # returns after its stream has drained
+
+    for _ in range(args.warmup):
+        frame()
     if dist:
         dist.barrier()
-    if torch:
-        torch.cuda.synchronize()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    st = pt.iterate(args.steps)  # returns after its stream has drained
-    if torch:
-        torch.cuda.synchronize()
+    st = Acc()
+    for _ in range(args.steps):
+        st.add(frame())
+    torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
 
-    rays = st.rays
-    # The literal workload once through, outside `value`: clear the film and render every
-    # pixel the rank owns to spp completion (startup and tail iterations included).
-    full = None
-    if not args.no_full_frame:
+    # steady state (outside `value`): iterations with every pixel's paths in flight
+    steady = None
+    if args.steady:
         pt.clear()
-        if torch:
-            torch.cuda.synchronize()
+        pt.iterate(30)
         t1 = time.perf_counter()
-        fs = pt.render()
-        dt_full = time.perf_counter() - t1
-        full = [dt_full, float(fs.rays), float(fs.iterations)]
+        ss = pt.iterate(60)
+        steady = [time.perf_counter() - t1, float(ss.rays), float(ss.ms_extend), float(ss.ms_shade)]
     if dist:
-        v = torch.tensor([dt, float(rays)], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dev = "cuda" if backend == "nccl" else "cpu"
+        v = torch.tensor([dt, float(st.rays)], dtype=torch.float64, device=dev)
         mx = v.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(v, op=dist.ReduceOp.SUM)
         dt_all, rays_all = float(mx[0]), float(v[1])
-        if full:
-            f = torch.tensor(full, dtype=torch.float64, device=v.device)
+        if steady:
+            f = torch.tensor(steady, dtype=torch.float64, device=dev)
             fmax = f.clone()
             dist.all_reduce(fmax, op=dist.ReduceOp.MAX)
             dist.all_reduce(f, op=dist.ReduceOp.SUM)
-            full = [float(fmax[0]), float(f[1]), float(fmax[2])]
+            steady = [float(fmax[0]), float(f[1]), float(steady[2]), float(steady[3])]
     else:
-        dt_all, rays_all = dt, float(rays)
+        dt_all, rays_all = dt, float(st.rays)
 
+    gathered = None
     if args.gather and dist:
         from mcpt import parallel
 
-        parallel.gather_film(pt, rank, world)
+        pt.clear()
+        pt.render()  # the film the gather moves: one whole frame
+        tg = time.perf_counter()
+        parallel.gather_film_to_root(pt, rank, world)
+        gathered = round(time.perf_counter() - tg, 4)
 
     if rank != 0:
         if dist:
@@ -214,76 +379,17 @@ def main():
         return
 
     K = args.steps
-    # logical bytes per SURVEY.md 8(d): state bytes per ray/path-bounce + BVH bytes per visit
-    b_ext = B_EXT_STATE * st.extend_rays + 2 * B_NODE * st.ext_nodes + B_TRI * st.ext_tests + B_HIT * st.ext_hits
-    b_any = B_ANY_STATE * (st.shadow_rays + st.vis_rays) + 2 * B_NODE * st.any_nodes + B_TRI * st.any_tests
-    b_shd = B_SHADE * st.shadow_rays + B_GEN * (st.extend_rays - st.shadow_rays)
-    # dominant kernel by summed HIP-event time over the timed region (same stream as the kernels);
-    # k_trace traces the extension (closest-hit) and any-hit rays of an iteration in one launch
-    kern = {"k_trace": st.ms_extend + st.ms_shadow, "k_shade": st.ms_shade}
-    names = {"k_trace": ("mcpt_dev::k_trace(", "mcpt_dev::k_trace<"), "k_shade": ("mcpt_dev::k_shade<", "mcpt_dev::k_material<")}
-    dom = max(kern, key=kern.get)
-    byts = b_ext + b_any if dom == "k_trace" else b_shd
-    state = (B_EXT_STATE * st.extend_rays + B_ANY_STATE * (st.shadow_rays + st.vis_rays)) if dom == "k_trace" else b_shd
-    per_launch = byts / K
-    avg_ms = kern[dom] / K
-    achieved = per_launch / (avg_ms * 1e-3)
-    # measured HBM bytes per launch from the committed PMC summary, used only when it was taken
-    # on this code and workload (tools/pmc.py stamps it)
-    summary, stale = pmc_summary(args.config, args.slots)
-    fresh = summary if stale is None else None
-    traffic = pmc_traffic(fresh, names[dom])
-    frac = achieved / HBM_PEAK
-    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": round(frac, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
-            "algorithmic_bytes_per_launch": int(per_launch),
-            "state_only_frac": round(state / K / (avg_ms * 1e-3) / HBM_PEAK, 4),
-            "per_ray": {"ext_pair_nodes": round(st.ext_nodes / max(1, st.extend_rays), 2),
-                        "ext_tri_tests": round(st.ext_tests / max(1, st.extend_rays), 2),
-                        "any_pair_nodes": round(st.any_nodes / max(1, st.shadow_rays + st.vis_rays), 2),
-                        "any_tri_tests": round(st.any_tests / max(1, st.shadow_rays + st.vis_rays), 2)}}
-    # What binds, from the numbers: SURVEY 8(d)'s logical bytes count every BVH node and triangle
-    # fetch; above the HBM peak they can only have come from the caches (L2 / MALL)
-    binding = []
-    if frac > 1.0:
-        binding.append(f"not HBM: the logical bytes run at {frac:.2f}x the HBM peak, so the node and triangle "
-                       f"fetches are cache-served ({achieved / L2_PEAK:.2f} of the 34.5 TB/s aggregate L2 rate)")
-        roof["l2_frac"] = round(achieved / L2_PEAK, 4)
-    if traffic is not None:
-        tf = traffic / (avg_ms * 1e-3) / HBM_PEAK
-        roof["traffic_GBps"] = round(traffic / (avg_ms * 1e-3) / 1e9, 1)
-        roof["traffic_frac"] = round(tf, 4)
-        binding.append(f"measured HBM traffic {tf:.2f} of peak")
-        if tf > 0.6:
-            binding.append("HBM-bound by measured traffic")
-    elif stale:
-        roof["pmc_stale"] = stale
-    if frac > 1.0 and (traffic is None or traffic / (avg_ms * 1e-3) / HBM_PEAK < 0.6):
-        binding.append("the traversal is bound by its divergent issue / gather-latency mix (DESIGN.md section 4)")
-    roof["binding"] = "; ".join(binding) if binding else "hbm"
-    # the streaming stages (logic + generate + material: k_shade and k_material) on their own,
-    # by SURVEY 8(d) state bytes and by the PMC traffic
-    t_shd = st.ms_shade / K * 1e-3
-    roof["shade_stages"] = {"ms_per_iteration": round(st.ms_shade / K, 4),
-                            "state_bytes_per_iteration": int(b_shd / K),
-                            "state_frac": round(b_shd / K / t_shd / HBM_PEAK, 4)}
-    shd_traffic = pmc_traffic(fresh, names["k_shade"])
-    if shd_traffic is not None:
-        roof["shade_stages"]["traffic"] = shd_traffic
-        roof["shade_stages"]["traffic_frac"] = round(shd_traffic / t_shd / HBM_PEAK, 4)
-    # measured HBM ceiling on this device (hand-written dwordx4 copy) beside the spec peak
-    copy = pt.hbm_copy_gbps(1 << 30, 20)
-    roof["measured_copy_GBps"] = round(copy, 1)
-    # whole-pipeline form: all logical bytes of both kernels over their summed time
-    t_pipe = (st.ms_extend + st.ms_shadow + st.ms_shade) * 1e-3
-    roof["pipeline_frac"] = round((b_ext + b_any + b_shd) / t_pipe / HBM_PEAK, 4)
-    hbm_meas = [pmc_traffic(fresh, p) for p in names.values()]
-    if all(h is not None for h in hbm_meas):  # measured HBM bytes per iteration (fresh PMC summary)
-        roof["pipeline_hbm_frac_measured"] = round(sum(hbm_meas) * K / t_pipe / HBM_PEAK, 4)
+    roof = roofline(st, st.ms_extend, st.ms_shade, args.config, slots)
+    roof["measured_copy_GBps"] = round(pt.hbm_copy_gbps(1 << 30, 20), 1)  # one-pass dwordx4 copy ceiling
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(scene.arrays(), cam, W, H, args.cpu_spp, rc.max_depth)
     value = rays_all / dt_all / 1e6
+    names = {2: "Cornell-box + 5 spheres proxy (scene_show_off_spheres.glb missing), night_free_Env.hdr",
+             3: "deep-BVH proxy, 871,416 tris (scene_show_off_dragon.glb missing), night_free_Env.hdr",
+             4: "Suzanne x2 Loop-subdivided, 251,904 tris (scene_show_off_head.glb missing), HDR_029",
+             5: "2 M-tri displaced-icosphere proxy (greek_sculpture.glb missing), night_free_Env.hdr",
+             1: "sphere.glb, HDR_029"}
     out = {
         "metric": "Mray/s (extend+shade) at 1080p x256spp depth5; fraction of HBM roofline",
         "value": round(value, 2),
@@ -291,34 +397,39 @@ def main():
         "n_gpus": world,
         "steps": K,
         "warmup": args.warmup,
-        "ms_per_step": round(dt_all * 1e3 / K, 4),
+        "ms_per_step": round(dt_all * 1e3 / K, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": "BASELINE config 2: Cornell-box + 5 spheres proxy (scene_show_off_spheres.glb missing), "
-                        f"night_free_Env.hdr env IS, {rc.width}x{rc.height} per GPU, {rc.spp} spp, depth {rc.max_depth}, MIS",
+            "workload": f"BASELINE config {args.config}: {names[args.config]}, env IS, "
+                        f"{W}x{H} frame, {spp} spp, depth {rc.max_depth}, MIS"
+                        + (" (spp overridden: not the BASELINE workload)" if args.spp else ""),
             "frame": [W, H],
+            "spp": spp,
             "tiles": "256x256, rank = (tx+ty) mod N",
-            "step": "one wavefront iteration (shade+extend+shadow) over the rank's pixels x path slots, steady state",
+            "step": "one whole frame: film cleared, every pixel the rank owns rendered to spp "
+                    "(all wavefront iterations: shade + extend + shadow)",
             "rays_per_step": int(rays_all / K),
-            "rays_per_step_rank0": {"extend": round(st.extend_rays / K), "shadow": round(st.shadow_rays / K),
-                                    "visibility": round(st.vis_rays / K)},
+            "iterations_per_step_rank0": round(st.iterations / K, 1),
             "parallelism": f"tiles{world}",
-            "path_slots": args.slots,
+            "path_slots": slots,
             "device": pt.device_name,
         },
-        "stage_ms_per_step": {k: round(v / K, 4) for k, v in kern.items()},
+        "stage_ms_per_step": {"k_trace": round(st.ms_extend / K, 3), "k_shade+k_material": round(st.ms_shade / K, 3)},
         "roofline": roof,
         "cpu_baseline": cpu,
     }
-    if full:
-        out["full_frame"] = {"seconds": round(full[0], 4), "rays": int(full[1]), "iterations": int(full[2]),
-                             "mray_s": round(full[1] / full[0] / 1e6, 2),
-                             "what": f"film cleared, every pixel rendered to {rc.spp} spp (max over ranks; host "
-                                     "syncs every 32 iterations, startup and tail included)"}
+    if steady:
+        out["steady_state"] = {"mray_s": round(steady[1] / steady[0] / 1e6, 2),
+                               "ms_per_iteration": round(steady[0] * 1e3 / 60, 4),
+                               "k_trace_ms": round(steady[2] / 60, 4), "shade_ms": round(steady[3] / 60, 4),
+                               "what": "60 wavefront iterations after 30, every pixel's path slots in flight "
+                                       "(rank 0's kernel times; rays and time over all ranks)"}
+    if gathered is not None:
+        out["gather_s"] = gathered
     print(json.dumps(out), flush=True)
     pt.close()
     if dist:

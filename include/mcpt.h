@@ -176,13 +176,18 @@ int mcpt_stage_run(mcpt_ctx *ctx, int stage, const mcpt_soa_view *in, mcpt_soa_v
 int mcpt_film_read(mcpt_ctx *ctx, float *Ld_rgb, uint32_t *samples);         /* host copies, 3*W*H / W*H */
 int mcpt_film_read_device(mcpt_ctx *ctx, void *d_Ld_rgb, void *d_samples);  /* device-to-device */
 int mcpt_film_pack_tiles(mcpt_ctx *ctx, void *d_out, uint32_t *npix);       /* tile-set pixels -> packed 16 B/px (rgb f32, samples u32) */
+/* The inverse on the gathering rank: scatter another rank's packed tile pixels (device memory on
+ * ctx's GPU, 16 B/px in the order mcpt_film_pack_tiles wrote them for tiles tile_xy[0..ntiles))
+ * into ctx's film accumulators.  The tiles must not be ctx's own (their other path slots would
+ * be added in).  Synchronous. */
+int mcpt_film_unpack_tiles(mcpt_ctx *ctx, const void *d_in, const uint32_t *tile_xy, uint32_t ntiles);
 int mcpt_film_tonemap_rgba8(mcpt_ctx *ctx, float exposure, uint8_t *out);   /* == draw_to_surface */
 int mcpt_film_size(const mcpt_ctx *ctx, uint32_t *w, uint32_t *h);
 /* Frame-end gather of a multi-GPU render in one process: the tile-set pixels of
  * every context (one per GPU, same film and tile size, tile sets disjoint from the root's) are
  * copied device-to-device over xGMI into ctxs[root]'s film, whose readers then return the whole
- * frame.  Processes with one GPU each use one RCCL all_gather of mcpt_film_pack_tiles buffers
- * instead (mcpt/parallel.py).  Synchronous. */
+ * frame.  Processes with one GPU each send their mcpt_film_pack_tiles buffer to the root over
+ * RCCL, which scatters it with mcpt_film_unpack_tiles (mcpt/parallel.py).  Synchronous. */
 int mcpt_gather(mcpt_ctx *const *ctxs, int32_t n, int32_t root);
 /* Film output (replaces stbi_write_png of the display buffer, RenderingContext.cpp:114-118):
  * PNG = tonemapped 8-bit RGB, row 0 = top; PFM = float RGB radiance Ld/samples (0 where no sample). */

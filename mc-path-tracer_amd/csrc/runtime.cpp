@@ -1134,13 +1134,42 @@ int mcpt_film_pack_tiles(mcpt_ctx* c, void* d_out, uint32_t* npix) {
     return MCPT_OK;
 }
 
+int mcpt_film_unpack_tiles(mcpt_ctx* c, const void* d_in, const uint32_t* xy, uint32_t n) {
+    if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
+    if (n == 0) return MCPT_OK;
+    if (!d_in || !xy) return set_err(c, MCPT_E_INVALID, "null argument");
+    const uint32_t nx = (c->W + c->tile_w - 1) / c->tile_w, ny = (c->H + c->tile_h - 1) / c->tile_h;
+    std::vector<int2> t(n);
+    for (uint32_t i = 0; i < n; i++) {
+        if (xy[2 * i] >= nx || xy[2 * i + 1] >= ny) return set_err(c, MCPT_E_INVALID, "tile out of range");
+        t[i] = make_int2((int)xy[2 * i], (int)xy[2 * i + 1]);
+        for (const int2& o : c->tiles_h)  // the context's own pixels would mix with its other slots
+            if (o.x == t[i].x && o.y == t[i].y) return set_err(c, MCPT_E_INVALID, "unpack into one of the context's own tiles");
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    int2* dt = nullptr;
+    HIPCHK(c, hipMalloc(&dt, n * sizeof(int2)));
+    hipError_t e = hipMemcpyAsync(dt, t.data(), n * sizeof(int2), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+        // scattered into slot 0 of the path state (its other slots of a pixel the context never
+        // renders stay zero, so the film view's slot sum returns these values)
+        UnpackArgs ua{(const float4*)d_in, dt, (int)n, (int)c->tile_w, (int)c->tile_h, (int)c->W, (int)c->H, c->p.Ld, c->p.samples};
+        launch_unpack(ua, c->stream);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(dt);
+    if (e != hipSuccess) return set_err(c, MCPT_E_HIP, std::string("unpack: ") + hipGetErrorString(e));
+    return MCPT_OK;
+}
+
 // Frame-end gather of a multi-GPU render inside one process (SURVEY.md 8(b) mcpt_gather, 8(e)):
 // every context's tile-set pixels, resolved over its path slots and packed 16 B/px, are copied
 // device-to-device onto the root's device (hipMemcpyPeerAsync: SDMA over xGMI between MI355X
 // dies of a node) and scattered into the root's film accumulators, so the root's film readers
 // return the whole frame.  Tile sets must not overlap the root's own tiles (the interleaved
-// partition of mcpt/parallel.py); the multi-process form is one RCCL all_gather of the same
-// packed buffers (mcpt/parallel.py).
+// partition of mcpt/parallel.py); the multi-process form sends the same packed buffers to the
+// root over RCCL and scatters them with mcpt_film_unpack_tiles (mcpt/parallel.py).
 int mcpt_gather(mcpt_ctx* const* ctxs, int32_t n, int32_t root) {
     if (!ctxs || n < 1 || root < 0 || root >= n || !ctxs[root]) return set_err(nullptr, MCPT_E_INVALID, "bad gather arguments");
     mcpt_ctx* R = ctxs[root];

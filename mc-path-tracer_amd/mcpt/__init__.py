@@ -99,6 +99,7 @@ ABI = {
     "mcpt_film_read": (C.c_int, [C.c_void_p, _f, _u]),
     "mcpt_film_read_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "mcpt_film_pack_tiles": (C.c_int, [C.c_void_p, C.c_void_p, _u]),
+    "mcpt_film_unpack_tiles": (C.c_int, [C.c_void_p, C.c_void_p, _u, C.c_uint32]),
     "mcpt_film_tonemap_rgba8": (C.c_int, [C.c_void_p, C.c_float, C.POINTER(C.c_uint8)]),
     "mcpt_sync": (C.c_int, [C.c_void_p]),
     "mcpt_device_name": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),

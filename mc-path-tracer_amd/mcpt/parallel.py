@@ -1,10 +1,14 @@
-"""Multi-GPU frame tiling and the film gather.
+"""Multi-GPU frame tiling and the frame-end film gather.
 
 Tiles are independent (keyed RNG: a pixel's result does not depend on who renders it), so the
-only collective is one gather of the per-rank tile pixels at frame end: every rank packs its
-tiles' pixels into a contiguous 16 B/px buffer (Ld rgb f32 + samples u32, mcpt_film_pack_tiles)
-and one all_gather over RCCL/xGMI (torch.distributed, backend "nccl") brings them to every rank;
-rank 0 scatters them into the full film.  No exchange happens while rendering.
+only collective is one gather of the per-rank tile pixels at frame end, to rank 0.  Every rank
+packs its tiles' pixels into a contiguous 16 B/px buffer (Ld rgb f32 + samples u32 bits,
+mcpt_film_pack_tiles) and sends it to rank 0 over RCCL (torch.distributed send/recv, backend
+"nccl": point-to-point over xGMI, each peer on its own link to rank 0 -- no ring, no N-fold
+all_gather payload).  Rank 0 receives every buffer into device memory and scatters it into its
+device film with mcpt_film_unpack_tiles, so its film readers return the whole frame.  The film's
+home stays device memory, as in the reference (Film.cu:121-172).  Buffer sizes follow from the
+deterministic tile partition, so no size exchange is needed.  No exchange happens while rendering.
 """
 from __future__ import annotations
 
@@ -22,8 +26,22 @@ def tiles_for_rank(rank, world, W, H, tile=256):
     return [(tx, ty) for ty in range(ny) for tx in range(nx) if (tx + ty) % world == rank]
 
 
+def pack(Ld: np.ndarray, samples: np.ndarray, tiles, W, H, tile=256) -> np.ndarray:
+    """Host restatement of mcpt_film_pack_tiles: a film's tile pixels as [n, 4] float32 (.w =
+    samples bits), tile by tile, rows of tile_w pixels; pixels past the frame edge are zero."""
+    out = np.zeros((len(tiles) * tile * tile, 4), np.float32)
+    for k, (tx, ty) in enumerate(tiles):
+        blk = np.zeros((tile, tile, 4), np.float32)
+        x0, y0 = tx * tile, ty * tile
+        w, h = min(tile, W - x0), min(tile, H - y0)
+        blk[:h, :w, :3] = Ld[y0:y0 + h, x0:x0 + w]
+        blk[:h, :w, 3] = np.ascontiguousarray(samples[y0:y0 + h, x0:x0 + w], np.uint32).view(np.float32)
+        out[k * tile * tile:(k + 1) * tile * tile] = blk.reshape(-1, 4)
+    return out
+
+
 def unpack(packed: np.ndarray, tiles, W, H, tile=256, Ld=None, samples=None):
-    """Scatter a rank's packed tile pixels ([n,4] float32, .w = samples bits) into a full film."""
+    """Scatter a rank's packed tile pixels ([n,4] float32, .w = samples bits) into a host film."""
     if Ld is None:
         Ld = np.zeros((H, W, 3), np.float32)
         samples = np.zeros((H, W), np.uint32)
@@ -33,47 +51,58 @@ def unpack(packed: np.ndarray, tiles, W, H, tile=256, Ld=None, samples=None):
         x0, y0 = tx * tile, ty * tile
         w, h = min(tile, W - x0), min(tile, H - y0)
         Ld[y0:y0 + h, x0:x0 + w] = blk[:h, :w, :3]
-        samples[y0:y0 + h, x0:x0 + w] = blk[:h, :w, 3].view(np.uint32)
+        samples[y0:y0 + h, x0:x0 + w] = np.ascontiguousarray(blk[:h, :w, 3]).view(np.uint32)
     return Ld, samples
 
 
-def gather_packed(local: "torch.Tensor", rank, world, dist):
-    """all_gather of variable-length [n,4] float32 tensors (padded to the max); returns the list
-    of per-rank tensors (trimmed).  Works with nccl (device tensors) and gloo (CPU tensors)."""
+def gather_packed_to_root(local, rank, world, dist, W, H, tile=256):
+    """Send every rank's packed [n, 4] float32 tensor to rank 0 (point-to-point send / recv,
+    nccl with device tensors or gloo with host tensors).  Rank 0 gets the list of per-rank
+    tensors (its own first) on local's device; the other ranks get None.  Sizes come from the
+    tile partition (tiles_for_rank), which every rank computes identically."""
     import torch
 
-    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    sizes = [int(s.item()) for s in sizes]
-    mx = max(sizes)
-    buf = torch.zeros((mx, 4), dtype=local.dtype, device=local.device)
-    buf[: local.shape[0]] = local
-    outs = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(outs, buf)
-    return [o[:s] for o, s in zip(outs, sizes)]
+    if rank != 0:
+        dist.send(local.contiguous(), dst=0)
+        return None
+    parts = [local]
+    for r in range(1, world):
+        n = len(tiles_for_rank(r, world, W, H, tile)) * tile * tile
+        buf = torch.empty((n, 4), dtype=local.dtype, device=local.device)
+        if n:
+            dist.recv(buf, src=r)
+        parts.append(buf)
+    return parts
 
 
-def gather_film(pt, rank, world, tile=256):
-    """Gather the film of a tiled multi-GPU render onto every rank; returns (Ld, samples) on rank 0."""
+def gather_film_to_root(pt, rank, world, tile=256):
+    """Frame-end gather of a tiled multi-GPU render into rank 0's device film: pack on every rank,
+    send to rank 0 (RCCL over xGMI), scatter there with mcpt_film_unpack_tiles.  Afterwards
+    pt.film() / write_png() on rank 0 return the whole frame."""
     import ctypes as C
 
     import torch
     import torch.distributed as dist
 
-    from . import lib, _check
+    from . import _check, lib
 
     n = C.c_uint32()
     _check(lib().mcpt_film_pack_tiles(pt.h, None, C.byref(n)), pt.h)
     local = torch.empty((n.value, 4), dtype=torch.float32, device="cuda")
     _check(lib().mcpt_film_pack_tiles(pt.h, C.c_void_p(local.data_ptr()), C.byref(n)), pt.h)
-    if dist.get_backend() != "nccl":  # gloo rehearsal: host-side collective
-        torch.cuda.synchronize()
+    host = dist.get_backend() != "nccl"  # gloo rehearsal: host-side point-to-point
+    if host:
         local = local.cpu()
-    parts = gather_packed(local, rank, world, dist)
+    parts = gather_packed_to_root(local, rank, world, dist, pt.W, pt.H, tile)
     if rank != 0:
         return None
-    Ld = samples = None
-    for r, part in enumerate(parts):
-        Ld, samples = unpack(part.cpu().numpy(), tiles_for_rank(r, world, pt.W, pt.H, tile), pt.W, pt.H, tile, Ld, samples)
-    return Ld, samples
+    for r, part in enumerate(parts[1:], start=1):
+        rt = tiles_for_rank(r, world, pt.W, pt.H, tile)
+        if not rt:
+            continue
+        dev = part.cuda() if host else part
+        xy = np.ascontiguousarray(rt, np.uint32).reshape(-1, 2)
+        torch.cuda.synchronize()  # the received buffer is complete before the library's stream reads it
+        _check(lib().mcpt_film_unpack_tiles(pt.h, C.c_void_p(dev.data_ptr()), xy.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                            len(rt)), pt.h)
+    return True

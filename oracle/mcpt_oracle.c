@@ -1094,6 +1094,8 @@ static void *worker_main(void *arg) {
         int t = (*w->next_tile)++;
         pthread_mutex_unlock(w->mu);
         if (t >= w->ntx * w->nty) break;
+        const or_config *cf = w->c->cfg;
+        if (cf->tile_mod > 0 && ((t % w->ntx) + (t / w->ntx)) % cf->tile_mod != cf->tile_rank) continue;
         render_tile(w->c, &q, t % w->ntx, t / w->ntx);
     }
     for (int i = 0; i < 6; i++) w->cnt[i] = q.cnt[i];

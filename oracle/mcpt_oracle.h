@@ -72,6 +72,8 @@ typedef struct or_config {
     int32_t traversal;    /* 0 = reference stack traversal, 1 = brute force   */
     int32_t row_begin, row_end;  /* restrict to rows [begin,end); 0,0 = all */
     int32_t fixed;        /* 1 = quality mode (product MCPT_FLAG_FIXED) */
+    int32_t tile_mod, tile_rank;  /* tile_mod > 0: only tiles with (tx+ty) % tile_mod == tile_rank
+                                     (one rank's share of the multi-GPU partition) */
 } or_config;
 
 /* counters[0]=extension rays, [1]=shadow rays, [2]=BRDF visibility rays,

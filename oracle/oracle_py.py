@@ -36,7 +36,8 @@ class OrCamera(C.Structure):
 class OrConfig(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("spp", C.c_int32), ("max_depth", C.c_int32), ("rr_depth", C.c_int32),
                 ("tile_w", C.c_int32), ("tile_h", C.c_int32), ("nthreads", C.c_int32), ("traversal", C.c_int32),
-                ("row_begin", C.c_int32), ("row_end", C.c_int32), ("fixed", C.c_int32)]
+                ("row_begin", C.c_int32), ("row_end", C.c_int32), ("fixed", C.c_int32),
+                ("tile_mod", C.c_int32), ("tile_rank", C.c_int32)]
 
 
 _lib = None
@@ -127,14 +128,25 @@ def camera_struct(cam) -> OrCamera:
     return c
 
 
+def default_threads():
+    """Oracle threads: the cores this process may use, at most 16 (the GPU box's per-GPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def render(arrays: dict, cam, W, H, spp, max_depth=5, rr_depth=3, seed=0x5EED2026, nthreads=None, traversal=0,
-           tile=256, rows=None, fixed=False):
-    """Full CPU re-execution of the reference wavefront loop.  Returns (Ld[H,W,3], samples[H,W], counters)."""
+           tile=256, rows=None, fixed=False, part=None):
+    """Full CPU re-execution of the reference wavefront loop.  Returns (Ld[H,W,3], samples[H,W], counters).
+    part=(rank, world) renders only that rank's tiles of the (tx + ty) mod world partition."""
     s = scene_struct(arrays)
     c = camera_struct(cam)
-    nthreads = nthreads or min(8, os.cpu_count() or 1)
+    nthreads = nthreads or default_threads()
     rb, re = rows if rows else (0, 0)
-    cfg = OrConfig(seed, spp, max_depth, rr_depth, tile, tile, nthreads, traversal, rb, re, int(fixed))
+    tr, tm = part if part else (0, 0)
+    cfg = OrConfig(seed, spp, max_depth, rr_depth, tile, tile, nthreads, traversal, rb, re, int(fixed), tm, tr)
     Ld = np.zeros(3 * W * H, np.float32)
     samples = np.zeros(W * H, np.uint32)
     cnt = (C.c_uint64 * 6)()

@@ -1,5 +1,7 @@
-"""bench.py's PMC-summary staleness check (CPU only): traffic figures from profiles/pmc_*.json are
-used only when the summary's stamp matches the current kernel sources and the benched workload."""
+"""bench.py host logic (CPU only): the PMC-summary staleness check, the roofline derivation, the
+frame / slot layout and the CPU-baseline thread count.  Traffic and counter figures from
+profiles/pmc*_r*.json are used only when the summary's stamp matches the current kernel sources
+and the benched workload (config, path slots, step kind)."""
 import json
 import os
 import sys
@@ -13,20 +15,88 @@ def test_source_hash_stable():
     assert bench.source_hash() == bench.source_hash() and len(bench.source_hash()) == 16
 
 
+def _stamp(h="abc", config=2, slots=3, step="frame"):
+    return {"source_hash": h, "config": config, "slots": slots, "step": step}
+
+
 def test_pmc_summary_stale_detection(tmp_path, monkeypatch):
     prof = tmp_path / "profiles"
     prof.mkdir()
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
     monkeypatch.setattr(bench, "source_hash", lambda: "abc")
-    assert bench.pmc_summary(2, 3) == (None, "no PMC summary in profiles/")
-    kern = {"mcpt_dev::k_trace(mcpt_dev::TraceArgs)": {"hbm_bytes_per_launch": 1000}}
-    (prof / "pmc_r09.json").write_text(json.dumps({"stamp": {"source_hash": "abc", "config": 2, "slots": 3},
-                                                   "kernels": kern}))
+    assert bench.pmc_summary(2, 3) == (None, "no pmc summary in profiles/")
+    kern = {"void mcpt_dev::k_trace<2, 8>(mcpt_dev::TraceArgs)": {"hbm_bytes_per_launch": 1000}}
+    (prof / "pmc_r09.json").write_text(json.dumps({"stamp": _stamp(), "kernels": kern}))
     d, why = bench.pmc_summary(2, 3)
-    assert why is None and bench.pmc_traffic(d, ("mcpt_dev::k_trace(",)) == 1000
+    assert why is None and bench.pmc_traffic(d, ("mcpt_dev::k_trace<",)) == 1000
     assert "3 slots" in bench.pmc_summary(2, 4)[1]
+    # a summary of the round-2 per-iteration steps is stale for the per-frame bench
+    (prof / "pmc_r10.json").write_text(json.dumps({"stamp": _stamp(step="iteration"), "kernels": kern}))
+    assert "iteration steps" in bench.pmc_summary(2, 3)[1]
+    (prof / "pmc_r11.json").write_text(json.dumps({"stamp": _stamp(), "kernels": kern}))
     monkeypatch.setattr(bench, "source_hash", lambda: "def")
     d, why = bench.pmc_summary(2, 3)
     assert "sources changed" in why
-    (prof / "pmc_r10.json").write_text(json.dumps({"kernels": kern}))  # unstamped (round-1 format)
+    (prof / "pmc_r12.json").write_text(json.dumps({"kernels": kern}))  # unstamped (round-1 format)
     assert bench.pmc_summary(2, 3)[1] is not None
+    # pmcdetail summaries are looked up separately (not mistaken for pmc_r*.json)
+    (prof / "pmcdetail_r12.json").write_text(json.dumps({"stamp": _stamp(h="def"), "kernels": {
+        "void mcpt_dev::k_trace<2, 8>(mcpt_dev::TraceArgs)": {"ratios": {"valu_busy": 0.7}}}}))
+    d, why = bench.pmc_summary(2, 3, "pmcdetail")
+    assert why is None and bench.pmc_detail(d, ("mcpt_dev::k_trace<",)) == {"valu_busy": 0.7}
+
+
+class _St:
+    def __init__(self, **kw):
+        for k in bench.Acc.KEYS:
+            setattr(self, k, 0)
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+
+def test_roofline_fields_never_exceed_one_and_bound_is_derived(tmp_path, monkeypatch):
+    """achieved = HBM-resident algorithmic bytes (per-ray state), cache-served BVH bytes apart;
+    bound = the most utilised resource, 'latency' when nothing reaches half its roof."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    monkeypatch.setattr(bench, "source_hash", lambda: "abc")
+    # config-2-like frame: 10 launches of 6 M extension + 4.6 M any-hit rays at 0.72 ms
+    st = _St(iterations=10, extend_rays=60_000_000, shadow_rays=23_000_000, vis_rays=23_000_000,
+             ext_nodes=550_000_000, ext_tests=115_000_000, ext_hits=50_000_000,
+             any_nodes=600_000_000, any_tests=110_000_000)
+    r = bench.roofline(st, 7.2, 4.4, 2, 3)
+    assert r["frac"] <= 1 and r["cache_served"]["l2_frac"] <= 1
+    assert r["algorithmic_bytes_per_launch"] == (65 * 6_000_000 + 33 * 4_600_000)
+    assert r["bound"] == "latency" and r["pmc_stale"]  # no PMC summary: HBM judged by the state bytes
+    kern = {"void mcpt_dev::k_trace<2, 8>(mcpt_dev::TraceArgs)": {"hbm_bytes_per_launch": 420_000_000},
+            "void mcpt_dev::k_shade<false>(mcpt_dev::ShadeArgs)": {"hbm_bytes_per_launch": 700_000_000},
+            "void mcpt_dev::k_material<false>(mcpt_dev::ShadeArgs)": {"hbm_bytes_per_launch": 900_000_000}}
+    (prof / "pmc_r03.json").write_text(json.dumps({"stamp": _stamp(), "kernels": kern}))
+    (prof / "pmcdetail_r03.json").write_text(json.dumps({"stamp": _stamp(), "kernels": {
+        "void mcpt_dev::k_trace<2, 8>(mcpt_dev::TraceArgs)": {
+            "ratios": {"valu_busy": 0.78, "wait_frac": 0.57, "lane_util": 0.5}}}}))
+    r = bench.roofline(st, 7.2, 4.4, 2, 3)
+    assert r["traffic"] == 420_000_000 and abs(r["traffic_frac"] - 420e6 / 0.72e-3 / 8e12) < 1e-4
+    assert r["bound"] == "valu" and r["utilisation"]["valu"] == 0.78 and "wait on memory 0.57" in r["binding"]
+    assert r["shade_stages"]["traffic"] == 1_600_000_000
+    for k in ("frac", "traffic_frac"):
+        assert r[k] <= 1
+
+
+def test_frame_and_slots_layout():
+    import mcpt
+
+    rc2, rc4 = mcpt.CONFIGS[2], mcpt.CONFIGS[4]
+    assert bench.frame_size(rc2, 1, "weak") == (1920, 1080) and bench.frame_size(rc2, 8, "weak") == (1920, 8640)
+    assert bench.frame_size(rc4, 8, "strong") == (3840, 2160)
+    assert bench.BENCH_SLOTS[2] == 3 and set(bench.BENCH_SLOTS) == set(mcpt.CONFIGS)
+    a = bench.parse(["--gpus", "4", "--config", "4", "--scaling", "strong"])
+    assert (a.gpus, a.config, a.scaling, a.slots, a.steps) == (4, 4, "strong", None, 5)
+
+
+def test_cpu_baseline_threads(monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.cpu_threads() == min(3, len(os.sched_getaffinity(0)))
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.cpu_threads() == len(os.sched_getaffinity(0))

@@ -1,0 +1,69 @@
+"""Parity at the bench's own layout, for every GPU BASELINE config.
+
+bench.py renders each config's full frame with BENCH_SLOTS path slots per pixel (several paths
+in flight per pixel, each slot accumulating its own samples).  Here the GPU renders exactly that
+layout -- full resolution, the bench's slot count, the config's depth -- to high sample counts
+(256 spp for configs 2 and 3, as benched; 16 spp for configs 4 and 5, whose full 1024 / 4096 spp
+would take minutes), and a band of rows re-executed by the oracle (one path per pixel, the
+reference's layout: wavefront_kernels.cu:90-375) must agree: sample counts exactly, radiance within
+the north star's 1e-4 relative (the slots only change the film's summation order).  High sample
+indices, Russian roulette at depth and the slots' interleaved sample chains are all exercised.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+sys.path.insert(0, REPO)
+import bench  # noqa: E402  (BENCH_SLOTS: the layout under test is the bench's)
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+
+
+def film_close(g, c):
+    tol = RTOL * np.maximum(np.abs(g), np.abs(c)) + 1e-7
+    ok = (np.abs(g - c) <= tol) | (np.isnan(g) & np.isnan(c))
+    return bool(ok.all()), int((~ok).sum())
+
+
+@pytest.mark.parametrize("cid,spp,rows", [(2, 256, (536, 540)), (3, 256, (600, 604)), (4, 16, (1078, 1082)),
+                                          (5, 16, (2046, 2049))], ids=["config2", "config3", "config4", "config5"])
+def test_bench_layout_band_parity(request, mcpt_mod, oracle, cid, spp, rows):
+    rc = mcpt_mod.CONFIGS[cid]
+    slots = bench.BENCH_SLOTS[cid]
+    if cid in (2, 3):
+        scene, arrays = request.getfixturevalue(f"scene_c{cid}")
+    else:
+        scene = mcpt_mod.build_config_scene(cid)
+        arrays = scene.arrays()
+    cam = mcpt_mod.config_camera(rc)
+    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=spp, max_depth=rc.max_depth))
+    pt.upload_scene(scene)
+    pt.set_camera(cam)
+    pt.set_path_slots(slots)
+    pt.resize(rc.width, rc.height)
+    t0 = time.perf_counter()
+    st = pt.render()
+    t_gpu = time.perf_counter() - t0
+    assert st.live_paths == 0
+    Ld, smp = pt.film()
+    pt.close()
+    # every rendered pixel has all its samples (last row / column never rendered: :110)
+    assert np.all(smp[:-1, :-1] == spp) and not smp[-1].any() and not smp[:, -1].any()
+    r0, r1 = rows
+    t0 = time.perf_counter()
+    rL, rs, cnt = oracle.render(arrays, cam, rc.width, rc.height, spp, rc.max_depth, rows=(r0, r1))
+    t_cpu = time.perf_counter() - t0
+    assert np.array_equal(smp[r0:r1], rs[r0:r1])
+    ok, nbad = film_close(Ld[r0:r1], rL[r0:r1])
+    assert ok, f"{nbad} radiance values differ"
+    assert np.isfinite(Ld[r0:r1]).all() and Ld[r0:r1].max() > 0
+    # RR and the deepest vertices were reached in the band (the oracle counts the rays it traced)
+    assert cnt["extend_rays"] > (r1 - r0) * (rc.width - 1) * spp
+    print(f"config {cid}: {rc.width}x{rc.height} {spp} spp {slots} slots: GPU frame {t_gpu:.2f} s "
+          f"({st.rays / t_gpu / 1e6:.0f} Mray/s), oracle rows {r0}-{r1} {t_cpu:.1f} s")

@@ -1,10 +1,20 @@
-"""Multi-rank path on CPU (gloo, world_size 2): tile partition and the film gather/unpack."""
+"""Multi-rank path on CPU (gloo, world_size 2): the tile partition and the frame-end gather to rank 0.
+
+The rendering rank is played by the oracle (scalar C restatement of the reference kernels) so the
+test runs without a GPU: every rank renders only its own tiles of the (tx + ty) mod N partition,
+packs them as mcpt_film_pack_tiles does, sends them to rank 0 (mcpt/parallel.py, point-to-point
+send / recv, the same calls the RCCL path makes), and rank 0's assembled film must equal the
+one-process render bit for bit (the keyed RNG makes a pixel's result independent of its rank).
+"""
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import torch.multiprocessing as mp
 
+from conftest import REPO
 from mcpt import parallel
 
 
@@ -33,44 +43,69 @@ def test_partition_balance_weak_scaling():
         assert max(counts) / (W * H / world) < 1.12
 
 
-def fake_film(W, H):
+def test_partition_balance_strong_scaling_config4():
+    """bench.py --config 4 --scaling strong: the fixed 3840x2160 frame split over 2/4/8 ranks."""
+    for world in (2, 4, 8):
+        W, H = 3840, 2160
+        counts = [sum(min(256, W - tx * 256) * min(256, H - ty * 256) for tx, ty in
+                      parallel.tiles_for_rank(r, world, W, H)) for r in range(world)]
+        assert sum(counts) == W * H and max(counts) / (W * H / world) < 1.15
+
+
+def test_pack_unpack_roundtrip():
     rng = np.random.default_rng(0)
-    return rng.random((H, W, 3), dtype=np.float32), rng.integers(0, 300, (H, W)).astype(np.uint32)
+    W, H, T = 300, 170, 64
+    Ld = rng.random((H, W, 3), dtype=np.float32)
+    smp = rng.integers(0, 1 << 31, (H, W)).astype(np.uint32)
+    tiles = parallel.tiles_for_rank(1, 3, W, H, T)
+    L2, S2 = parallel.unpack(parallel.pack(Ld, smp, tiles, W, H, T), tiles, W, H, T)
+    mask = np.zeros((H, W), bool)
+    for tx, ty in tiles:
+        mask[ty * T:(ty + 1) * T, tx * T:(tx + 1) * T] = True
+    assert np.array_equal(L2[mask], Ld[mask]) and np.array_equal(S2[mask], smp[mask])
+    assert not L2[~mask].any() and not S2[~mask].any()
 
 
-def pack(Ld, samples, tiles, W, H, tile=256):
-    out = np.zeros((len(tiles) * tile * tile, 4), np.float32)
-    for k, (tx, ty) in enumerate(tiles):
-        blk = np.zeros((tile, tile, 4), np.float32)
-        x0, y0 = tx * tile, ty * tile
-        w, h = min(tile, W - x0), min(tile, H - y0)
-        blk[:h, :w, :3] = Ld[y0:y0 + h, x0:x0 + w]
-        blk[:h, :w, 3] = samples[y0:y0 + h, x0:x0 + w].view(np.float32)
-        out[k * tile * tile:(k + 1) * tile * tile] = blk.reshape(-1, 4)
-    return out
+W_, H_, T_, SPP_ = 300, 200, 64, 2
+
+
+def _scene_and_camera():
+    import mcpt
+
+    s = mcpt.build_config_scene(2)
+    rc = mcpt.CONFIGS[2]
+    return s.arrays(), mcpt.config_camera(rc, W_, H_)
 
 
 def _worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
 
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_py
+
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    W, H = 700, 530
-    Ld, smp = fake_film(W, H)
-    tiles = parallel.tiles_for_rank(rank, world, W, H)
-    local = torch.from_numpy(pack(Ld, smp, tiles, W, H))
-    parts = parallel.gather_packed(local, rank, world, dist)
-    if rank == 0:
-        L2 = S2 = None
-        for r, p in enumerate(parts):
-            L2, S2 = parallel.unpack(p.numpy(), parallel.tiles_for_rank(r, world, W, H), W, H, 256, L2, S2)
-        q.put(bool(np.array_equal(L2, Ld) and np.array_equal(S2, smp)))
-    dist.barrier()
-    dist.destroy_process_group()
+    try:
+        arrays, cam = _scene_and_camera()
+        # this rank's partition only, rendered as a rank would (the oracle stands in for the GPU)
+        Ld, smp, _ = oracle_py.render(arrays, cam, W_, H_, SPP_, 5, tile=T_, nthreads=2, part=(rank, world))
+        tiles = parallel.tiles_for_rank(rank, world, W_, H_, T_)
+        local = torch.from_numpy(parallel.pack(Ld, smp, tiles, W_, H_, T_))
+        parts = parallel.gather_packed_to_root(local, rank, world, dist, W_, H_, T_)
+        if rank == 0:
+            L2 = S2 = None
+            for r, p in enumerate(parts):
+                L2, S2 = parallel.unpack(p.numpy(), parallel.tiles_for_rank(r, world, W_, H_, T_), W_, H_, T_, L2, S2)
+            fL, fs, _ = oracle_py.render(arrays, cam, W_, H_, SPP_, 5, tile=T_, nthreads=4)
+            q.put((bool(np.array_equal(L2.view(np.uint32), fL.view(np.uint32)) and np.array_equal(S2, fs)),
+                   int(fs.sum()), int(S2.sum())))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
 
 
-def test_gather_roundtrip_gloo_world2():
+def test_rendered_partition_gathered_to_root_gloo_world2():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -80,7 +115,17 @@ def test_gather_roundtrip_gloo_world2():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    ok = q.get(timeout=120)
+    ok, n_full, n_gathered = q.get(timeout=240)
     for p in procs:
         p.join(60)
-    assert ok
+    assert n_full == (W_ - 1) * (H_ - 1) * SPP_  # every rendered pixel (last row / column never: :110)
+    assert ok and n_gathered == n_full
+
+
+def test_bench_gpus_flag_refuses_mismatched_world(tmp_path):
+    """bench.py --gpus N under a launcher whose WORLD_SIZE differs exits non-zero before any GPU
+    work (without a launcher it starts the N ranks itself)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr

@@ -763,32 +763,6 @@ def test_native_gather_equals_one_pass(mcpt_mod, scene_c2, slots):
         pt.close()
 
 
-@pytest.mark.parametrize("cid,rows,slots", [(4, (1078, 1082), 4), (5, (2046, 2049), 4)])
-def test_config45_full_frame_band_parity(mcpt_mod, oracle, cid, rows, slots):
-    """BASELINE configs 4 (Suzanne x2 subdivided, 251,904 tris, 3840x2160, depth 8) and 5 (2 M-tri
-    proxy, 4096x4096, depth 12) at their full resolution, 4 spp over 4 path slots (the bench's
-    layout: one sample per slot) on the GPU; a band of rows re-executed by the oracle agrees
-    (samples exactly, radiance within the north star's 1e-4)."""
-    rc = mcpt_mod.CONFIGS[cid]
-    s = mcpt_mod.build_config_scene(cid)
-    a = s.arrays()
-    cam = mcpt_mod.config_camera(rc)
-    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=4, max_depth=rc.max_depth))
-    pt.upload_scene(s)
-    pt.set_camera(cam)
-    pt.set_path_slots(slots)
-    pt.resize(rc.width, rc.height)
-    st = pt.render()
-    assert st.live_paths == 0
-    Ld, smp = pt.film()
-    r0, r1 = rows
-    rL, rs, _ = oracle.render(a, cam, rc.width, rc.height, 4, rc.max_depth, rows=(r0, r1))
-    assert np.array_equal(smp[r0:r1], rs[r0:r1])
-    ok, nbad = film_close(Ld[r0:r1], rL[r0:r1])
-    assert ok, f"{nbad} radiance values differ"
-    pt.close()
-
-
 @pytest.mark.parametrize("gpu_bvh", [False, "ploc"])
 @pytest.mark.parametrize("which", ["scene_c1", "scene_c2", "scene_cube", "scene_c3"])
 def test_quad_nodes_same_hits(request, mcpt_mod, oracle, which, gpu_bvh):

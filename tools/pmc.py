@@ -30,7 +30,7 @@ def find(sub, suffix):
 
 stats = find("prof_kt", "kernel_stats.csv")
 if stats:
-    shutil.copy(stats, os.path.join(dst, f"kernel_stats_{tag}.csv"))
+    shutil.copy(stats, os.path.join(dst, os.environ.get("STATS_NAME", f"kernel_stats_{tag}") + ".csv"))
 pmc = collections.defaultdict(dict)
 for sub, ctr in (("prof_fetch", "FETCH_SIZE"), ("prof_write", "WRITE_SIZE")):
     f = find(sub, "counter_collection.csv")
@@ -50,13 +50,14 @@ if stats:
 sys.path.insert(0, REPO)
 import bench  # noqa: E402  (source_hash only)
 
-# The profiled commands run bench.py's defaults (config 2, 3 path slots) unless PMC_CONFIG /
-# PMC_SLOTS say otherwise; bench.py uses the traffic only when this stamp matches its run.
-stamp = {"source_hash": bench.source_hash(), "config": int(os.environ.get("PMC_CONFIG", "2")),
-         "slots": int(os.environ.get("PMC_SLOTS", "3"))}
+# The profiled commands run bench.py's defaults (config 2, BENCH_SLOTS, whole-frame steps) unless
+# PMC_CONFIG / PMC_SLOTS say otherwise; bench.py uses the traffic only when this stamp matches its run.
+cfg = int(os.environ.get("PMC_CONFIG", "2"))
+stamp = {"source_hash": bench.source_hash(), "config": cfg,
+         "slots": int(os.environ.get("PMC_SLOTS", str(bench.BENCH_SLOTS[cfg]))), "step": bench.STEP}
 out = {"round": tag, "stamp": stamp,
        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on "
-       "'python3 bench.py --no-cpu-baseline --steps 20 --warmup 10'; durations from --kernel-trace --stats",
+       f"'python3 bench.py {os.environ.get('PMC_ARGS', '--no-cpu-baseline')}'; durations from --kernel-trace --stats",
        "correction": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE reads half of 16 B/lane streams)",
        "kernels": {}}
 for k, v in pmc.items():
@@ -67,5 +68,6 @@ for k, v in pmc.items():
             v["avg_ns"] = dur[k]
             v["hbm_GBps"] = round(b / dur[k], 1)
     out["kernels"][k] = v
-json.dump(out, open(os.path.join(dst, f"pmc_{tag}.json"), "w"), indent=1)
+name = os.environ.get("PMC_NAME", f"pmc_{tag}")  # e.g. pmc_c5_r03 for another config's evidence
+json.dump(out, open(os.path.join(dst, f"{name}.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
