@@ -62,6 +62,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=12, help="spp of the full-frame CPU-oracle sample")
     ap.add_argument("--gather", action="store_true", help="gather the film on rank 0 after timing (N>1)")
+    ap.add_argument("--verify-gather", action="store_true",
+                    help="with --gather: rank 0 then renders the whole frame alone and checks the gathered film "
+                         "equals it bit for bit")
     ap.add_argument("--steady", action="store_true",
                     help="also time 60 steady-state iterations (outside value; off by default so that every "
                          "k_trace launch of the process belongs to a timed or warmup frame, as rocprofv3 sees it)")
@@ -362,15 +365,25 @@ def main():
     else:
         dt_all, rays_all = dt, float(st.rays)
 
-    gathered = None
+    gathered = verified = None
     if args.gather and dist:
         from mcpt import parallel
 
         pt.clear()
         pt.render()  # the film the gather moves: one whole frame
+        dist.barrier()
         tg = time.perf_counter()
         parallel.gather_film_to_root(pt, rank, world)
         gathered = round(time.perf_counter() - tg, 4)
+        if args.verify_gather and rank == 0:
+            import numpy as np
+
+            Lg, sg = pt.film()  # the gathered frame
+            pt.set_tiles(None)  # every tile, one rank: the reference film
+            pt.clear()
+            pt.render()
+            Lr, sr = pt.film()
+            verified = bool(np.array_equal(Lg.view(np.uint32), Lr.view(np.uint32)) and np.array_equal(sg, sr))
 
     if rank != 0:
         if dist:
@@ -430,6 +443,8 @@ def main():
                                        "(rank 0's kernel times; rays and time over all ranks)"}
     if gathered is not None:
         out["gather_s"] = gathered
+    if verified is not None:
+        out["gather_equals_one_rank_frame"] = verified
     print(json.dumps(out), flush=True)
     pt.close()
     if dist:

@@ -38,7 +38,7 @@ enum {
  * wavefront_kernels.cu: max_depth 5 (:142), rr_depth 3 (:189), spp <= 250 (:124). */
 typedef struct mcpt_config {
     uint64_t seed;       /* keyed RNG seed; default 0x5EED2026 */
-    int32_t spp;         /* samples per pixel: gates processing and new samples */
+    int32_t spp;         /* samples per pixel (< 2^19): gates processing and new samples */
     int32_t max_depth;   /* 'path_length > max_depth' terminates */
     int32_t rr_depth;    /* Russian roulette when 'path_length > rr_depth' */
     int32_t tile_w;      /* film tile (Film.cu:17: 256x256) */
@@ -122,15 +122,57 @@ typedef struct mcpt_stage_stats {
 enum { MCPT_STAGE_LOGIC = 0, MCPT_STAGE_GENERATE = 1, MCPT_STAGE_MATERIAL = 2,
        MCPT_STAGE_EXTEND = 3, MCPT_STAGE_SHADOW = 4 };
 
+/* Path state at the shading stages' boundary, for mcpt_stage_run(LOGIC | GENERATE | MATERIAL)
+ * (host SoA, n paths; SURVEY.md 8(b) per-stage parity harness).  Field meaning against the
+ * reference's Paths (Wavefront.cuh:8-26):
+ *   flags     bit 0 dead; bits 1..8 len (path_length); bits 9..12 the MIS conditions of the
+ *             previous vertex (9 light term w > 0 && pdf > 0, 10 BRDF term, 11 f_sample == 0 or
+ *             pdf_sample == 0, 12 a BRDF visibility ray was drawn: non-delta light); bits 13..31
+ *             the sample index the path renders (keys its RNG draws)
+ *   samples   dFilm.samples of the pixel (completed samples)
+ *   hit_tri   the closest hit of `ray` (index into the uploaded scene's triangle arrays, -1 none)
+ *   ray_o/_d  Paths.ray (3n each)
+ *   beta      Paths.beta in xyz, (f_sample / pdf_sample).x in w (4n)
+ *   nee0/1    the light-sample / BRDF-sample MIS terms f * Li * w / pdf (wavefront_kernels.cu:
+ *             168-179) in xyz, (f_sample / pdf_sample).y / .z in w (4n)
+ *   vis       light-sample / BRDF-sample visibility (Paths.visible; the BRDF one is the
+ *             reference's inline visibility ray, :334-336) (2n)
+ *   Ld        dFilm.Ld of the pixel (3n)
+ *   light_o/_d, bvis_o/_d   MATERIAL out: the light-sample shadow ray (ray_light, :212-213) and the
+ *             BRDF visibility ray (:334) it queued for the trace stage; NaN where none was
+ *             queued (a delta light, or a ray resolved in place because it cannot hit the scene:
+ *             its vis byte is then set to 1) (3n each)
+ *   queued    out: bit 0 extension ray queued, bit 1 path continues into MATERIAL (LOGIC),
+ *             bit 2 light ray queued, bit 3 BRDF visibility ray queued (n)
+ * LOGIC (k_shade): wf_logic + wf_generate of a film of film_w x film_h pixels, path i = pixel
+ * (i % film_w, i / film_w), one path per pixel, the context's camera and config.  In: flags,
+ * samples, hit_tri, ray_d, beta, nee0, nee1, vis, Ld.  Out: flags, samples, Ld, ray_o/_d of new
+ * paths, beta (the updated throughput of continuing paths), hit_tri, queued.
+ * GENERATE: LOGIC with every path dead (wf_generate for sample index `samples`).
+ * MATERIAL (k_material): the light choice (:207-213) and wf_mat_mix (:295-375) of continuing path
+ * i at pixel i.  In: flags (len, sample index), hit_tri, ray_o/_d, beta.  Out: flags, ray_o/_d
+ * (the next extension ray), beta, nee0, nee1, hit_tri, vis, light/bvis rays, queued. */
+typedef struct mcpt_path_view {
+    uint32_t film_w, film_h;
+    uint32_t *flags, *samples;
+    int32_t *hit_tri;
+    float *ray_o, *ray_d, *beta, *nee0, *nee1;
+    uint8_t *vis;
+    float *Ld;
+    float *light_o, *light_d, *bvis_o, *bvis_d;
+    uint8_t *queued;
+} mcpt_path_view;
+
 /* Caller SoA buffers for mcpt_stage_run (host memory). */
 typedef struct mcpt_soa_view {
-    const float *ray_o;     /* 3*n */
-    const float *ray_d;     /* 3*n */
+    const float *ray_o;     /* EXTEND / SHADOW in: 3*n */
+    const float *ray_d;     /* EXTEND / SHADOW in: 3*n */
     float *hit_pos_t;       /* EXTEND out: 4*n pos.xyz, t */
     float *hit_nrm_mat;     /* EXTEND out: 4*n normal.xyz, (float)material (-1 miss) */
     int32_t *hit_tri;       /* EXTEND out: n triangle index or -1 */
     uint8_t *visible;       /* SHADOW out: n */
     uint32_t *steps;        /* optional out: per-ray child-pair node fetches + triangle tests */
+    mcpt_path_view *paths;  /* LOGIC / GENERATE / MATERIAL: in->paths inputs, out->paths outputs */
 } mcpt_soa_view;
 
 typedef struct mcpt_ctx mcpt_ctx;     /* device context: one per GPU, not thread-safe */

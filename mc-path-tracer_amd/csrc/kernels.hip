@@ -390,6 +390,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
 #endif
 template <bool FIXED>
 __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
+    if (a.cnt->idle) return;  // the tile set is complete (an earlier iteration of the call traced no ray)
     const DevScene& sc = a.scene;
     const int tile_px = a.tile_w * a.tile_h;
     const int bpt = (tile_px + kBlock - 1) / kBlock;
@@ -419,7 +420,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     }
     // ---- phase 1: logic + generate (one thread per pixel)
     bool gen_ext = false, gen_trivial = false, cont = false;
-    uint32_t cont_len = 0, cont_samples = 0;
+    uint32_t cont_len = 0, cont_sidx = 0;
     int32_t cont_htri = -1;
     V3 beta_store = v3(0.f, 0.f, 0.f);
     // A primary ray that missed adds the background (env_L of its direction) to the film.
@@ -452,7 +453,8 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         const uchar2 vv = reinterpret_cast<const uchar2*>(a.p.vis)[need_nee ? pid : 0u];
         bool dead = (fl & F_DEAD) != 0;
         const uint32_t spp = (uint32_t)a.spp;
-        // this slot's sample index (slot k runs samples k, k + S, ...; S = 1: the count itself)
+        // this slot's sample index (slot k runs samples k, k + S, ...; S = 1: the count itself),
+        // kept in the flags word from generation on (k_material keys its draws with it)
         uint32_t sidx = (uint32_t)slot + (uint32_t)a.slots * samples;
         if (!dead && sidx < spp) {  // wavefront_kernels.cu:124
             const Rng r{rng_key(a.seed, pix, sidx), len};
@@ -511,7 +513,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             } else {
                 cont = true;
                 cont_len = len;
-                cont_samples = samples;
+                cont_sidx = sidx;
                 cont_htri = htri;
             }
         }
@@ -523,7 +525,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             V3 new_o, new_d;
             gen_ray(a.cam, a.W, a.H, x, y, r0, new_o, new_d);
             // beta = (1,1,1) (:245) is implied by len 1: k_shade does not load it for len-1 paths
-            nflags = 1u << F_LEN_SHIFT;
+            nflags = (1u << F_LEN_SHIFT) | (sidx << F_SIDX_SHIFT);
             a.p.ray_o[pid] = f4(new_o, 0.f);
             a.p.ray_d[pid] = f4(new_d, 0.f);
             gen_ext = true;
@@ -549,7 +551,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         if (gen_ext) a.ext_q[shard * a.ext_cap + slot[0]] = pid;
         if (cont) {
             const uint32_t qi = shard * a.ext_cap + slot[1];
-            a.mat_rec[qi] = make_uint4(pid, cont_len, cont_samples, (uint32_t)cont_htri);
+            a.mat_rec[qi] = make_uint4(pid, cont_len, cont_sidx, (uint32_t)cont_htri);
             a.mat_beta[qi] = f4(beta_store, 0.f);
         }
     }
@@ -588,6 +590,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
 // ---------------------------------------------------------------------------
 template <bool FIXED>
 __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) {
+    if (a.cnt->idle) return;  // the tile set is complete
     const uint32_t shard = blockIdx.x % kShards, w_in = blockIdx.x / kShards, bps = gridDim.x / kShards;
     uint32_t* sc_ctr = a.cnt->shard[shard];
     const uint32_t n = sc_ctr[C_MAT];
@@ -608,7 +611,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
         MatOut mo{false, false, false, false, false, 0u};
         uint32_t mpid = 0;
         if (i < n) {
-            const uint4 q = a.mat_rec[shard * a.ext_cap + i];  // {pid, len, samples, hit_tri}
+            const uint4 q = a.mat_rec[shard * a.ext_cap + i];  // {pid, len, sample index, hit_tri}
             const float4 b4 = a.mat_beta[shard * a.ext_cap + i];
             mpid = q.x;
             mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w, &s_any[0][0]);
@@ -652,7 +655,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
         __syncthreads();
         if (threadIdx.x < 12) {
             unsigned long long v = 0;
-            for (int w = 0; w < kBlock / 64; w++) v += s_sprof[w][threadIdx.x];
+            for (int w = 0; w < (int)(blockDim.x >> 6); w++) v += s_sprof[w][threadIdx.x];
             atomicAdd(&g_trace_prof[(blockIdx.x % 64) * 12 + threadIdx.x], v);
         }
     }
@@ -766,6 +769,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #ifdef MCPT_WAVE_TIMES
     if (threadIdx.x == 0 && blockIdx.x < 16384) g_wave_t[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
+    if (a.idle && *a.idle) return;  // the tile set is complete
     __shared__ int2 stk[kLdsStack][kTraceBlock];
     const int lane = threadIdx.x;
     // ---- work distribution.  The queue shards are split into nparts partitions
@@ -1325,6 +1329,7 @@ __global__ void k_tonemap(TonemapArgs a) {  // draw_to_surface (wavefront_kernel
 }
 
 __global__ void k_accumulate(CounterBlock* c, uint32_t nparts) {  // fold per-iteration shard counts into 64-bit totals
+    if (c->idle) return;  // nothing ran since the iteration that set it; every counter is zero
     const int t = threadIdx.x;  // one lane per shard
     uint32_t v[C_STATS + 6];
 #pragma unroll
@@ -1362,6 +1367,7 @@ __global__ void k_accumulate(CounterBlock* c, uint32_t nparts) {  // fold per-it
         c->tot_vis += v[C_VIS];
         c->last_ext = v[C_EXT];
         c->last_live = er;
+        if (er == 0) c->idle = 1;  // no path alive and none generated: every later iteration is a no-op
         for (int k = 0; k < 6; k++) c->tot_stats[k] += v[C_STATS + k];
     }
 }
@@ -1456,6 +1462,17 @@ void launch_shade(const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fix
     } else {
         hipLaunchKernelGGL(k_shade<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
         hipLaunchKernelGGL(k_material<false>, dim3(g.mat_blocks[0]), dim3(kBlock), 0, s, a);
+    }
+}
+// One of the two shading kernels alone (mcpt_stage_run's LOGIC / GENERATE and MATERIAL stages).
+void launch_shade_stage(bool material_stage, const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fixed_mode,
+                        hipStream_t s) {
+    if (!material_stage) {
+        if (fixed_mode) hipLaunchKernelGGL(k_shade<true>, dim3(nblocks), dim3(kBlock), 0, s, a);
+        else hipLaunchKernelGGL(k_shade<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
+    } else {
+        if (fixed_mode) hipLaunchKernelGGL(k_material<true>, dim3(g.mat_blocks[1]), dim3(kBlock), 0, s, a);
+        else hipLaunchKernelGGL(k_material<false>, dim3(g.mat_blocks[0]), dim3(kBlock), 0, s, a);
     }
 }
 // Persistent grid: the device's resident waves rounded to a multiple of the shard count.

@@ -1,10 +1,12 @@
 // kernels.hpp -- device data layout shared by kernels.hip and runtime.hip.
 //
-// HBM layout (P = W*H paths, one per pixel as in the reference, path_id ==
-// pixel_id, wavefront_kernels.cu:108,114).  The reference's Paths is an
-// array-of-structs with 128-B Isect and 32-B dRay per path (Wavefront.cuh:8-26);
-// here every field is a separate 16-B-aligned stream so a wave64 access is one
-// coalesced 1 KiB dwordx4 transaction:
+// HBM layout (P = slots * W*H paths; slot 0 is the reference's one path per pixel, path_id ==
+// pixel_id, wavefront_kernels.cu:108,114).  The reference's Paths is an array-of-structs with a
+// 128-B Isect and a 32-B dRay per path (Wavefront.cuh:8-26); here every field is a separate
+// 16-B-aligned stream so a wave64 access is one coalesced 1 KiB dwordx4 transaction.  (Records
+// that pack a path's fields together -- 32-B rays, 64-B {beta, nee0, nee1, Ld} -- move fewer HBM
+// bytes on the sparse accesses but cost more lines per wave instruction, and measured slower:
+// k_material 248 -> 302 ms, k_shade 139 -> 193 ms per three config-2 frames)
 //   ray_o/ray_d   float4 [P]    extension ray (xyz, pad)
 //   hit_tri       i32    [P]    closest triangle of the extension ray (-1 = miss); the hit
 //                               record (isect) is rebuilt from it where it is consumed
@@ -14,7 +16,7 @@
 //                               holds the result index 2p (light sample) / 2p+1 (BRDF visibility).
 //   beta          float4 [P]    throughput, (f_sample/pdf_sample).x
 //   nee0 / nee1   float4 [P]    precomputed light / BRDF MIS terms, ratio .y / .z
-//   flags         u32    [P]    dead, len, MIS condition bits
+//   flags         u32    [P]    dead, len, MIS condition bits, the path's sample index (bits 13..31)
 //   vis           u8     [2P]   any-hit results
 //   samples       u32    [P]    film sample count (dFilm.samples)
 //   Ld            float4 [P]    film radiance (dFilm.Ld)
@@ -48,8 +50,15 @@ enum : uint32_t {
     F_CONDL = 1u << 9,      // light-sample MIS term valid (w > 0 && pdf > 0)
     F_CONDB = 1u << 10,     // BRDF-sample MIS term valid when visible
     F_FZERO = 1u << 11,     // f_sample == 0 || pdf_sample == 0
-    F_HASVIS = 1u << 12     // non-delta light: a BRDF visibility ray was traced
+    F_HASVIS = 1u << 12,    // non-delta light: a BRDF visibility ray was traced
+    F_SIDX_SHIFT = 13       // bits 13..31: the sample index the path renders (RNG key)
 };
+constexpr uint32_t kMaxSpp = 1u << (32 - F_SIDX_SHIFT);  // sample indices must fit the flags word
+
+// k_shade blocks: kBlock consecutive pixels of one path slot; slot k's blocks follow slot k-1's
+__host__ __device__ constexpr int shade_blocks_per_tile(int tile_px, int slots) {
+    return (tile_px + kBlock - 1) / kBlock * slots;
+}
 
 // BVH node width of the traversal, per scene (DevScene::width): width 2, child-pair
 // nodes, 4 x float4 (per axis (mn0, mn1, mx0, mx1), then refs); width 4, 8 x float4:
@@ -93,7 +102,9 @@ struct CounterBlock {
     uint32_t shard[kShards][C_WORDS];  // [0] ext pushes [1] any-hit pushes [2] vis rays [3..8] traversal stats [9,10] rays [11] material pushes
     uint32_t last_ext, last_live;
     uint32_t trace_short;  // k_trace launches that left a partition's rays untraced (k_accumulate; must stay 0)
-    uint32_t pad[29];
+    uint32_t idle;         // set by k_accumulate after an iteration with no ray: the tile set is complete, so
+                           // the remaining iterations of the call skip their kernels (run_iterations resets it)
+    uint32_t pad[28];
     uint32_t last_ext_shard[kShards];  // per-shard extension pushes of the last iteration
     uint32_t grab[kMaxParts][C_WORDS];  // k_trace ray hand-out, one counter line per partition
     unsigned long long tot_ext, tot_any, tot_vis, pad2;
@@ -111,7 +122,7 @@ struct ShadeArgs {
     uint64_t seed;
     uint32_t *ext_q, *any_q;
     // material queue (continuing paths, k_shade -> k_material, ext_cap per shard): dense records
-    // {pid, len, samples, hit_tri} + the updated throughput, so k_material reads its per-path
+    // {pid, len, sample index, hit_tri} + the updated throughput, so k_material reads its per-path
     // inputs from k_shade's coalesced loads instead of gathering them again at pid
     uint4* mat_rec;
     float4* mat_beta;
@@ -144,6 +155,7 @@ struct TraceArgs {
     uint32_t nparts;            // work partitions (default: the device's XCDs; set by launch_trace)
     uint32_t ndies;             // XCDs of the device (set by launch_trace)
     uint32_t* grab;             // nparts chunk counters, C_WORDS apart, zero at launch (k_accumulate resets)
+    const uint32_t* idle;       // optional: nonzero = the tile set is complete, exit at once (CounterBlock::idle)
 };
 
 struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; int32_t* scene_tri; uint32_t n; };
@@ -165,6 +177,8 @@ struct LaunchGeom {
 };
 int launch_geometry(int device, LaunchGeom& g);  // device must be current
 void launch_shade(const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fixed_mode, hipStream_t s);
+void launch_shade_stage(bool material_stage, const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fixed_mode,
+                        hipStream_t s);
 void launch_trace(const TraceArgs& a, const LaunchGeom& g, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
 void launch_env_table(const mcpt::EnvView& e, bool fixed_mode, float4* out, float2* row, float2* col, hipStream_t s);

@@ -40,6 +40,7 @@ struct mcpt_ctx {
     DevScene scene{};
     bool has_scene = false;
     bool has_scene_before = false;  // set at the start of a re-upload
+    int32_t ntri = 0;               // triangles of the uploaded scene
     int pair_depth = 0;
     int node_layout = 0;  // pair-node numbering the last upload used (mcpt_debug_node_layout)
     // camera
@@ -138,7 +139,10 @@ int mcpt_create(int device, const mcpt_config* cfg, mcpt_ctx** out) {
     snprintf(c->devname, sizeof(c->devname), "%s (%s, %d CUs)", prop.name, prop.gcnArchName, prop.multiProcessorCount);
     if (cfg) c->cfg = *cfg;
     else { c->cfg.seed = 0x5EED2026ull; c->cfg.spp = 16; c->cfg.max_depth = 5; c->cfg.rr_depth = 3; c->cfg.tile_w = 256; c->cfg.tile_h = 256; }
-    if (c->cfg.max_depth < 1 || c->cfg.max_depth > 200 || c->cfg.spp < 0) { delete c; return set_err(nullptr, MCPT_E_INVALID, "bad config"); }
+    if (c->cfg.max_depth < 1 || c->cfg.max_depth > 200 || c->cfg.spp < 0 || (uint32_t)c->cfg.spp >= kMaxSpp) {
+        delete c;
+        return set_err(nullptr, MCPT_E_INVALID, "bad config (max_depth 1..200, spp 0..2^19-1)");
+    }
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return set_err(nullptr, MCPT_E_HIP, "stream creation failed");
@@ -601,6 +605,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     s.depth = width == 4 ? quad_push : c->pair_depth;
     s.width = width;
     c->scene = s;
+    c->ntri = d->ntri;
     if (c->has_scene_before) c->film_stale = true;  // a re-upload notifies the film
     c->has_scene = true;
     return MCPT_OK;
@@ -646,9 +651,8 @@ int mcpt_camera_set(mcpt_ctx* c, const mcpt_camera* cam) {
 }
 
 static int set_tiles_internal(mcpt_ctx* c, const std::vector<int2>& t) {
-    // per-shard queue capacity: shard = k_shade block mod kShards
-    const uint32_t bpt = (c->tile_w * c->tile_h + kBlock - 1) / kBlock;
-    const uint32_t nblocks = (uint32_t)t.size() * bpt * c->slots;
+    // per-shard queue capacity: shard = k_shade block mod kShards (a block pushes <= one ray per thread)
+    const uint32_t nblocks = (uint32_t)t.size() * (uint32_t)shade_blocks_per_tile((int)(c->tile_w * c->tile_h), (int)c->slots);
     c->ext_cap = std::max<uint32_t>(1, (nblocks + kShards - 1) / kShards) * kBlock;
     c->any_cap = 2 * c->ext_cap;
     const size_t need = (size_t)kShards * c->ext_cap;
@@ -800,10 +804,10 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     sa.ext_cap = c->ext_cap;
     sa.any_cap = c->any_cap;
     sa.cnt = c->cnt;
-    int bpt = (int)((c->tile_w * c->tile_h + kBlock - 1) / kBlock);
+    const int bpt = shade_blocks_per_tile((int)(c->tile_w * c->tile_h), (int)c->slots);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 0), c->stream));
     if (sa.ntiles > 0)
-        launch_shade(sa, sa.ntiles * bpt * (int)c->slots, c->geom, (c->cfg.flags & MCPT_FLAG_FIXED) != 0, c->stream);
+        launch_shade(sa, sa.ntiles * bpt, c->geom, (c->cfg.flags & MCPT_FLAG_FIXED) != 0, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 1), c->stream));
     // extension (closest hit) and any-hit rays in one persistent launch
     TraceArgs ta{};
@@ -829,6 +833,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     ta.hit_tri = c->p.hit_tri;
     ta.vis = c->p.vis;
     ta.grab = &c->cnt->grab[0][0];  // reset by k_accumulate below
+    ta.idle = &c->cnt->idle;
     launch_trace(ta, c->geom, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
     launch_accumulate(c->cnt, c->geom.trace_parts, c->stream);
@@ -855,6 +860,9 @@ static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st, const i
         c->totals_ok = true;
     }
     const CounterBlock before = c->totals;
+    // iterations after one that traced no ray skip their kernels (k_accumulate sets the flag):
+    // mcpt_render's last batch of 32 no longer pays full launches for the finished film
+    HIPCHK(c, hipMemsetAsync(&c->cnt->idle, 0, sizeof(uint32_t), c->stream));
     for (uint32_t i = 0; i < n; i++) {
         // events for at most the first 4096 iterations of a call
         bool timing = i < 4096;
@@ -908,8 +916,8 @@ int mcpt_wavefront_step(mcpt_ctx* c, uint32_t tx, uint32_t ty, mcpt_stage_stats*
     // The one-tile set goes through its own small buffer (pinned staging, stream-ordered
     // copy): the context's tile set and queues stay as they are when their per-shard queue
     // capacity covers one tile, which it does unless the tile set is empty.
-    const uint32_t bpt = (c->tile_w * c->tile_h + kBlock - 1) / kBlock;
-    const uint32_t need = std::max<uint32_t>(1, (bpt * c->slots + kShards - 1) / kShards) * kBlock;
+    const uint32_t bpt = (uint32_t)shade_blocks_per_tile((int)(c->tile_w * c->tile_h), (int)c->slots);
+    const uint32_t need = std::max<uint32_t>(1, (bpt + kShards - 1) / kShards) * kBlock;
     if (c->ext_cap >= need) {
         if (!c->step_tile) {
             HIPCHK(c, hipSetDevice(c->device));
@@ -961,12 +969,210 @@ int mcpt_sync(mcpt_ctx* c) {
     return MCPT_OK;
 }
 
+// mcpt_stage_run(LOGIC | GENERATE | MATERIAL): the product's shading kernels (k_shade: wf_logic
+// + wf_generate; k_material: light choice + wf_mat_mix) over caller path state of n paths in
+// scratch device buffers -- the per-stage parity harness of SURVEY.md 8(b) / section 4 item 2.
+// The context's film, queues and counters are not touched.
+static int stage_run_paths(mcpt_ctx* c, int stage, const mcpt_path_view* in, mcpt_path_view* out, uint32_t n) {
+    const bool mat = stage == MCPT_STAGE_MATERIAL, gen = stage == MCPT_STAGE_GENERATE;
+    if (!in || !out) return set_err(c, MCPT_E_INVALID, "stage needs in->paths and out->paths");
+    uint32_t W = n, H = 1;
+    if (!mat) {
+        W = in->film_w;
+        H = in->film_h;
+        if (!c->has_cam) return set_err(c, MCPT_E_INVALID, "no camera set");
+        if ((uint64_t)W * H != n || W < 2 || H < 2) return set_err(c, MCPT_E_INVALID, "film_w * film_h must equal n (>= 2 x 2)");
+    }
+    if (n >= (1u << 26)) return set_err(c, MCPT_E_INVALID, "too many paths for one stage call");
+    if (mat && in->hit_tri)  // k_material rebuilds the hit record from the triangle: it must exist
+        for (uint32_t i = 0; i < n; i++)
+            if (in->hit_tri[i] < 0 || in->hit_tri[i] >= c->ntri)
+                return set_err(c, MCPT_E_INVALID, "MATERIAL: every path needs a hit (0 <= hit_tri < ntri)");
+    if (!in->hit_tri || !in->flags || (!gen && (!in->ray_d || !in->beta)) || (!mat && !in->samples) ||
+        (mat && !in->ray_o) || (stage == MCPT_STAGE_LOGIC && (!in->nee0 || !in->nee1 || !in->vis || !in->Ld)))
+        return set_err(c, MCPT_E_INVALID, "missing path-state input");
+    HIPCHK(c, hipSetDevice(c->device));
+    free_list(c->tmp_bufs);
+    auto& L = c->tmp_bufs;
+    // shard capacity: LOGIC blocks of 256 paths push into shard block mod 64; MATERIAL records are
+    // dealt to shards i mod 64
+    const uint32_t nblocks = (uint32_t)shade_blocks_per_tile((int)n, 1);
+    const uint32_t per_shard = mat ? (n + kShards - 1) / kShards : ((nblocks + kShards - 1) / kShards) * kBlock;
+    const uint32_t ext_cap = std::max<uint32_t>(kBlock, (per_shard + kBlock - 1) / kBlock * kBlock), any_cap = 2 * ext_cap;
+    const size_t qn = (size_t)kShards * ext_cap;
+    DevPaths p{};
+    uint32_t *ext_q, *any_q;
+    uint4* mrec;
+    float4* mbeta;
+    CounterBlock* cnt;
+    int2* tl;
+    int rc;
+    if ((rc = dalloc(c, L, &p.ray_o, n)) || (rc = dalloc(c, L, &p.ray_d, n)) || (rc = dalloc(c, L, &p.beta, n)) ||
+        (rc = dalloc(c, L, &p.nee0, n)) || (rc = dalloc(c, L, &p.nee1, n)) || (rc = dalloc(c, L, &p.Ld, n)) ||
+        (rc = dalloc(c, L, &p.hit_tri, n)) || (rc = dalloc(c, L, &p.flags, n)) || (rc = dalloc(c, L, &p.samples, n)) ||
+        (rc = dalloc(c, L, &p.vis, 2 * (size_t)n)) ||
+        (rc = dalloc(c, L, &p.sray_o, 2 * qn)) || (rc = dalloc(c, L, &p.sray_d, 2 * qn)) ||
+        (rc = dalloc(c, L, &ext_q, qn)) || (rc = dalloc(c, L, &any_q, 2 * qn)) || (rc = dalloc(c, L, &mrec, qn)) ||
+        (rc = dalloc(c, L, &mbeta, qn)) || (rc = dalloc(c, L, &cnt, 1)) || (rc = dalloc(c, L, &tl, 1)))
+        return rc;
+    auto f4v = [n](const float* a, int k, float w) {  // host k-float SoA -> float4 (w pad)
+        std::vector<float4> v(n, make_float4(0.f, 0.f, 0.f, w));
+        if (a)
+            for (uint32_t i = 0; i < n; i++)
+                v[i] = make_float4(a[k * i], a[k * i + 1], a[k * i + 2], k == 4 ? a[4 * i + 3] : w);
+        return v;
+    };
+    auto up = [&](void* d, const void* h, size_t bytes) -> hipError_t {
+        return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->stream);
+    };
+    std::vector<float4> ro = f4v(in->ray_o, 3, 0.f), rd = f4v(in->ray_d, 3, 0.f), be = f4v(in->beta, 4, 0.f),
+                        n0 = f4v(in->nee0, 4, 0.f), n1 = f4v(in->nee1, 4, 0.f), ld = f4v(in->Ld, 3, 0.f);
+    std::vector<uint32_t> fl(in->flags, in->flags + n), sm(n, 0u);
+    if (in->samples) sm.assign(in->samples, in->samples + n);
+    if (gen) std::fill(fl.begin(), fl.end(), (uint32_t)F_DEAD);
+    std::vector<uint8_t> vis(2 * (size_t)n, 0);
+    if (in->vis) vis.assign(in->vis, in->vis + 2 * (size_t)n);
+    CounterBlock* hc = c->cnt_host;  // pinned staging (the context's counters stay on the device)
+    memset(hc, 0, sizeof(CounterBlock));
+    std::vector<uint4> rec;
+    std::vector<float4> rbeta;
+    if (mat) {  // records {pid, len, sample index, hit_tri} + throughput, path i in shard i mod 64
+        rec.assign(qn, make_uint4(0, 0, 0, 0));
+        rbeta.assign(qn, make_float4(0.f, 0.f, 0.f, 0.f));
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t sh = i % kShards, k = i / kShards;
+            rec[(size_t)sh * ext_cap + k] = make_uint4(i, (fl[i] >> F_LEN_SHIFT) & 0xffu, fl[i] >> F_SIDX_SHIFT, (uint32_t)in->hit_tri[i]);
+            rbeta[(size_t)sh * ext_cap + k] = make_float4(be[i].x, be[i].y, be[i].z, 0.f);
+            hc->shard[sh][C_MAT]++;
+        }
+    }
+    const int2 tile0 = make_int2(0, 0);
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = up(p.ray_o, ro.data(), n * sizeof(float4));
+    if (e == hipSuccess) e = up(p.ray_d, rd.data(), n * sizeof(float4));
+    if (e == hipSuccess) e = up(p.beta, be.data(), n * sizeof(float4));
+    if (e == hipSuccess) e = up(p.nee0, n0.data(), n * sizeof(float4));
+    if (e == hipSuccess) e = up(p.nee1, n1.data(), n * sizeof(float4));
+    if (e == hipSuccess) e = up(p.Ld, ld.data(), n * sizeof(float4));
+    if (e == hipSuccess) e = up(p.hit_tri, in->hit_tri, n * sizeof(int32_t));
+    if (e == hipSuccess) e = up(p.flags, fl.data(), n * sizeof(uint32_t));
+    if (e == hipSuccess) e = up(p.samples, sm.data(), n * sizeof(uint32_t));
+    if (e == hipSuccess) e = up(p.vis, vis.data(), 2 * (size_t)n);
+    if (e == hipSuccess) e = up(cnt, hc, sizeof(CounterBlock));
+    if (e == hipSuccess) e = up(tl, &tile0, sizeof(int2));
+    if (e == hipSuccess && mat) e = up(mrec, rec.data(), qn * sizeof(uint4));
+    if (e == hipSuccess && mat) e = up(mbeta, rbeta.data(), qn * sizeof(float4));
+    if (e != hipSuccess) return set_err(c, MCPT_E_HIP, std::string("stage upload: ") + hipGetErrorString(e));
+    ShadeArgs sa{};
+    sa.scene = c->scene;
+    sa.cam = c->cam;
+    sa.p = p;
+    sa.tiles = tl;
+    sa.ntiles = 1;
+    sa.tile_w = (int)W;
+    sa.tile_h = (int)H;
+    sa.W = (int)W;
+    sa.H = (int)H;
+    sa.spp = c->cfg.spp;
+    sa.max_depth = c->cfg.max_depth;
+    sa.rr_depth = c->cfg.rr_depth;
+    sa.seed = c->cfg.seed;
+    sa.slots = 1;
+    sa.ext_q = ext_q;
+    sa.any_q = any_q;
+    sa.mat_rec = mrec;
+    sa.mat_beta = mbeta;
+    sa.ext_cap = ext_cap;
+    sa.any_cap = any_cap;
+    sa.cnt = cnt;
+    HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
+    launch_shade_stage(mat, sa, (int)nblocks, c->geom, (c->cfg.flags & MCPT_FLAG_FIXED) != 0, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
+    HIPCHK(c, hipMemcpyAsync(hc, cnt, sizeof(CounterBlock), hipMemcpyDeviceToHost, c->stream));
+    std::vector<float4> o_ro(n), o_rd(n), o_be(n), o_n0(n), o_n1(n), o_ld(n);
+    std::vector<uint32_t> o_fl(n), o_sm(n), o_eq(qn), o_aq(2 * qn);
+    std::vector<int32_t> o_ht(n);
+    std::vector<uint8_t> o_vis(2 * (size_t)n);
+    std::vector<uint4> o_rec(qn);
+    std::vector<float4> o_rb(qn), o_so(2 * qn), o_sd(2 * qn);
+    auto dn = [&](void* h, const void* d, size_t bytes) -> hipError_t {
+        return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream);
+    };
+    if (e == hipSuccess) e = dn(o_ro.data(), p.ray_o, n * sizeof(float4));
+    if (e == hipSuccess) e = dn(o_rd.data(), p.ray_d, n * sizeof(float4));
+    if (e == hipSuccess) e = dn(o_be.data(), p.beta, n * sizeof(float4));
+    if (e == hipSuccess) e = dn(o_n0.data(), p.nee0, n * sizeof(float4));
+    if (e == hipSuccess) e = dn(o_n1.data(), p.nee1, n * sizeof(float4));
+    if (e == hipSuccess) e = dn(o_ld.data(), p.Ld, n * sizeof(float4));
+    if (e == hipSuccess) e = dn(o_fl.data(), p.flags, n * sizeof(uint32_t));
+    if (e == hipSuccess) e = dn(o_sm.data(), p.samples, n * sizeof(uint32_t));
+    if (e == hipSuccess) e = dn(o_ht.data(), p.hit_tri, n * sizeof(int32_t));
+    if (e == hipSuccess) e = dn(o_vis.data(), p.vis, 2 * (size_t)n);
+    if (e == hipSuccess) e = dn(o_eq.data(), ext_q, qn * sizeof(uint32_t));
+    if (e == hipSuccess) e = dn(o_aq.data(), any_q, 2 * qn * sizeof(uint32_t));
+    if (e == hipSuccess) e = dn(o_rec.data(), mrec, qn * sizeof(uint4));
+    if (e == hipSuccess) e = dn(o_rb.data(), mbeta, qn * sizeof(float4));
+    if (e == hipSuccess) e = dn(o_so.data(), p.sray_o, 2 * qn * sizeof(float4));
+    if (e == hipSuccess) e = dn(o_sd.data(), p.sray_d, 2 * qn * sizeof(float4));
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return set_err(c, MCPT_E_HIP, std::string("stage run: ") + hipGetErrorString(e));
+    HIPCHK(c, hipEventElapsedTime(&c->last_stage_ms, c->events[0], c->events[1]));
+    const float qnan = __builtin_nanf("");
+    std::vector<uint8_t> queued(n, 0);
+    std::vector<float> lo(3 * (size_t)n, qnan), ldr(3 * (size_t)n, qnan), bo(3 * (size_t)n, qnan), bd(3 * (size_t)n, qnan);
+    for (int sh = 0; sh < kShards; sh++) {
+        for (uint32_t k = 0; k < hc->shard[sh][C_EXT]; k++) queued[o_eq[(size_t)sh * ext_cap + k]] |= 1;
+        if (!mat)
+            for (uint32_t k = 0; k < hc->shard[sh][C_MAT]; k++) {  // continuing paths: their updated throughput
+                const size_t q = (size_t)sh * ext_cap + k;
+                const uint32_t pid = o_rec[q].x;
+                queued[pid] |= 2;
+                o_be[pid] = make_float4(o_rb[q].x, o_rb[q].y, o_rb[q].z, o_be[pid].w);
+            }
+        for (uint32_t k = 0; k < hc->shard[sh][C_ANY]; k++) {
+            const size_t q = (size_t)sh * any_cap + k;
+            const uint32_t r = o_aq[q], pid = r >> 1;
+            float* so = (r & 1) ? bo.data() : lo.data();
+            float* sd = (r & 1) ? bd.data() : ldr.data();
+            queued[pid] |= (r & 1) ? 8 : 4;
+            so[3 * pid] = o_so[q].x; so[3 * pid + 1] = o_so[q].y; so[3 * pid + 2] = o_so[q].z;
+            sd[3 * pid] = o_sd[q].x; sd[3 * pid + 1] = o_sd[q].y; sd[3 * pid + 2] = o_sd[q].z;
+        }
+    }
+    auto put3 = [n](float* dst, const std::vector<float4>& v) {
+        if (dst)
+            for (uint32_t i = 0; i < n; i++) { dst[3 * i] = v[i].x; dst[3 * i + 1] = v[i].y; dst[3 * i + 2] = v[i].z; }
+    };
+    auto put4 = [n](float* dst, const std::vector<float4>& v) {
+        if (dst) memcpy(dst, v.data(), n * sizeof(float4));
+    };
+    if (out->flags) memcpy(out->flags, o_fl.data(), n * sizeof(uint32_t));
+    if (out->samples) memcpy(out->samples, o_sm.data(), n * sizeof(uint32_t));
+    if (out->hit_tri) memcpy(out->hit_tri, o_ht.data(), n * sizeof(int32_t));
+    put3(out->ray_o, o_ro);
+    put3(out->ray_d, o_rd);
+    put4(out->beta, o_be);
+    put4(out->nee0, o_n0);
+    put4(out->nee1, o_n1);
+    if (out->vis) memcpy(out->vis, o_vis.data(), 2 * (size_t)n);
+    put3(out->Ld, o_ld);
+    if (out->light_o) memcpy(out->light_o, lo.data(), 3 * (size_t)n * sizeof(float));
+    if (out->light_d) memcpy(out->light_d, ldr.data(), 3 * (size_t)n * sizeof(float));
+    if (out->bvis_o) memcpy(out->bvis_o, bo.data(), 3 * (size_t)n * sizeof(float));
+    if (out->bvis_d) memcpy(out->bvis_d, bd.data(), 3 * (size_t)n * sizeof(float));
+    if (out->queued) memcpy(out->queued, queued.data(), n);
+    free_list(c->tmp_bufs);
+    return MCPT_OK;
+}
+
 int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_view* out, uint32_t n) {
     if (!c || !in || !out) return set_err(c, MCPT_E_INVALID, "null argument");
     if (!c->has_scene) return set_err(c, MCPT_E_INVALID, "no scene uploaded");
-    if (stage != MCPT_STAGE_EXTEND && stage != MCPT_STAGE_SHADOW)
-        return set_err(c, MCPT_E_INVALID, "stage not separately exposed: logic/generate/material are fused into k_shade");
+    if (stage < MCPT_STAGE_LOGIC || stage > MCPT_STAGE_SHADOW) return set_err(c, MCPT_E_INVALID, "unknown stage");
     if (n == 0) return MCPT_OK;
+    if (stage == MCPT_STAGE_LOGIC || stage == MCPT_STAGE_GENERATE || stage == MCPT_STAGE_MATERIAL)
+        return stage_run_paths(c, stage, in->paths, out->paths, n);
     if (!in->ray_o || !in->ray_d) return set_err(c, MCPT_E_INVALID, "null rays");
     if (stage == MCPT_STAGE_EXTEND && (!out->hit_pos_t || !out->hit_nrm_mat)) return set_err(c, MCPT_E_INVALID, "null outputs");
     if (stage == MCPT_STAGE_SHADOW && !out->visible) return set_err(c, MCPT_E_INVALID, "null outputs");

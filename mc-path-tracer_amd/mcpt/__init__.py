@@ -74,9 +74,38 @@ class StageStats(C.Structure):
         return int(self.extend_rays + self.shadow_rays + self.vis_rays)
 
 
+class PathView(C.Structure):  # mcpt_path_view: path state at the shading stages' boundary
+    _fields_ = [("film_w", C.c_uint32), ("film_h", C.c_uint32), ("flags", _u), ("samples", _u), ("hit_tri", _i),
+                ("ray_o", _f), ("ray_d", _f), ("beta", _f), ("nee0", _f), ("nee1", _f),
+                ("vis", C.POINTER(C.c_uint8)), ("Ld", _f), ("light_o", _f), ("light_d", _f), ("bvis_o", _f),
+                ("bvis_d", _f), ("queued", C.POINTER(C.c_uint8))]
+
+
 class SoaView(C.Structure):
     _fields_ = [("ray_o", _f), ("ray_d", _f), ("hit_pos_t", _f), ("hit_nrm_mat", _f), ("hit_tri", _i),
-                ("visible", C.POINTER(C.c_uint8)), ("steps", _u)]
+                ("visible", C.POINTER(C.c_uint8)), ("steps", _u), ("paths", C.POINTER(PathView))]
+
+
+# mcpt_path_view fields as numpy: (dtype, values per path)
+PATH_FIELDS = {"flags": (np.uint32, 1), "samples": (np.uint32, 1), "hit_tri": (np.int32, 1), "ray_o": (np.float32, 3),
+               "ray_d": (np.float32, 3), "beta": (np.float32, 4), "nee0": (np.float32, 4), "nee1": (np.float32, 4),
+               "vis": (np.uint8, 2), "Ld": (np.float32, 3), "light_o": (np.float32, 3), "light_d": (np.float32, 3),
+               "bvis_o": (np.float32, 3), "bvis_d": (np.float32, 3), "queued": (np.uint8, 1)}
+STAGE_BY_NAME = {"logic": STAGE_LOGIC, "generate": STAGE_GENERATE, "material": STAGE_MATERIAL}
+
+
+def path_view(arrs: dict, n, film=(0, 0)):
+    """PathView over numpy arrays (missing fields stay NULL); the arrays are kept on the view."""
+    v = PathView()
+    v.film_w, v.film_h = film
+    keep = {}
+    for k, (dt, m) in PATH_FIELDS.items():
+        if k in arrs and arrs[k] is not None:
+            a = np.ascontiguousarray(arrs[k], dt).reshape(n * m)
+            keep[k] = a
+            setattr(v, k, a.ctypes.data_as(C.POINTER(np.ctypeslib.as_ctypes_type(dt))))
+    v._keep = keep
+    return v
 
 
 # Every symbol declared in include/mcpt.h with its ctypes signature.
@@ -477,6 +506,22 @@ class PathTracer:
                        st.ctypes.data_as(_u) if steps else None)
         self._ck(lib().mcpt_stage_run(self.h, STAGE_SHADOW, C.byref(vin), C.byref(vout), n))
         return (vis, st) if steps else vis
+
+    def stage(self, name, state: dict, film=None) -> dict:
+        """mcpt_stage_run of one shading stage ("logic", "generate", "material") over caller path
+        state (numpy arrays keyed as mcpt_path_view's fields, n paths); returns every output
+        field.  film=(W, H) for logic / generate: path i is pixel (i % W, i // W)."""
+        n = len(state["flags"])
+        film = film or (0, 0)
+        vin = SoaView()
+        pin = path_view(state, n, film)
+        vin.paths = C.pointer(pin)
+        outs = {k: np.zeros((n, m) if m > 1 else n, dt) for k, (dt, m) in PATH_FIELDS.items()}
+        vout = SoaView()
+        pout = path_view(outs, n, film)
+        vout.paths = C.pointer(pout)
+        self._ck(lib().mcpt_stage_run(self.h, STAGE_BY_NAME[name], C.byref(vin), C.byref(vout), n))
+        return {k: pout._keep[k].reshape(outs[k].shape) for k in outs}
 
     @property
     def last_stage_ms(self) -> float:

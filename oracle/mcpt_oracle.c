@@ -625,7 +625,9 @@ typedef struct { uint64_t nodes, tris; } trav_stats;
  * a triangle's hit counts only if the line also passes its own bounding box (the vertex union,
  * g_init_BVH_triangle_info, mesh_initialization_kernels.cu:63-83) under the same slab test --
  * exactly the leaf test of BVHAccel's one-triangle leaves, so results do not depend on how a
- * builder grouped triangles. */
+ * builder grouped triangles.  traversal == 2 is the literal reference rule instead (every leaf
+ * primitive tested, no own-box check, exact-t ties to the first visited, Triangle.cu:170-179):
+ * tests/test_oracle.py::test_literal_leaf_rule_deviation counts the pixels it changes. */
 static int own_box_hit(const or_scene *sc, int id, const ray_t *ray, v3 inv, const int neg[3]) {
     const float *a = sc->v0 + 3 * (int64_t)id, *b = sc->v1 + 3 * (int64_t)id, *c = sc->v2 + 3 * (int64_t)id;
     float mn[3], mx[3];
@@ -682,8 +684,10 @@ static int closest_hit(const or_scene *sc, const ray_t *ray, int traversal, floa
                     float u, v, t;
                     st->tris++;
                     if (tri_intersect(sc, id, ray, &u, &v, &t) && !(t < 0.f)) {
-                        if ((t < tmin || (t == tmin && best >= 0 && tri_key(sc, id) < tri_key(sc, best))) &&
-                            (np == 1 || own_box_hit(sc, id, ray, inv, neg))) { tmin = t; best = id; }
+                        if (traversal == 2) {  /* literal reference leaf rule: first visited wins */
+                            if (t < tmin) { tmin = t; best = id; }
+                        } else if ((t < tmin || (t == tmin && best >= 0 && tri_key(sc, id) < tri_key(sc, best))) &&
+                                   (np == 1 || own_box_hit(sc, id, ray, inv, neg))) { tmin = t; best = id; }
                     }
                 }
                 if (sp == 0) break;
@@ -727,7 +731,7 @@ static int any_hit(const or_scene *sc, const ray_t *ray, int traversal, trav_sta
                     float u, v, t;
                     st->tris++;
                     if (tri_intersect(sc, id, ray, &u, &v, &t) && !(t < 0.f) && t < K_HUGE &&
-                        (np == 1 || own_box_hit(sc, id, ray, inv, neg)))
+                        (traversal == 2 || np == 1 || own_box_hit(sc, id, ray, inv, neg)))
                         return 1;
                 }
                 if (sp == 0) break;
@@ -881,6 +885,98 @@ static rng_t path_rng(const ctx_t *c, uint32_t pid, uint32_t len) {
     return r;
 }
 
+/* wf_logic's MIS combination of the previous vertex's two samples (wavefront_kernels.cu:165-180)
+ * as four terms: the light-sample and BRDF-sample contributions f*Li*w/pdf and their conditions
+ * (w > 0 && pdf > 0), evaluated exactly as the reference evaluates them, plus the throughput
+ * factor f_sample / pdf_sample (:187) and its zero test (:182-185).  The product's material stage
+ * stores these terms (nee0 / nee1 / flags, mcpt_path_view) and its logic stage sums them; the
+ * stage harness (or_stage_*) is checked field by field against the same functions. */
+typedef struct {
+    v3 cL, cB, ratio;
+    int condL, condB, hasvis, fzero;
+} mis_t;
+
+static mis_t mis_terms(const path_t *p, int hasvis) {
+    mis_t m;
+    float w = or_power_heuristic(p->pdf_light[0], p->pdf_brdf[1]);
+    m.cL = vdivs(vscale(vmul(p->f_light, p->Li_light), w), p->pdf_light[0]);
+    m.condL = w > 0.f && p->pdf_light[0] > 0.f;
+    w = or_power_heuristic(p->pdf_brdf[0], p->pdf_light[1]);
+    m.cB = vdivs(vscale(vmul(p->f_brdf, p->Li_brdf), w), p->pdf_brdf[0]);
+    m.condB = w > 0.f && p->pdf_brdf[0] > 0.f;
+    m.hasvis = hasvis;
+    m.ratio = vdivs(p->f_sample, p->pdf_sample);
+    m.fzero = (p->f_sample.x == 0.f && p->f_sample.y == 0.f && p->f_sample.z == 0.f) || p->pdf_sample == 0.f;
+    return m;
+}
+
+/* :168-179.  vl / vb: light-sample / BRDF-sample visibility.  An occluded BRDF sample (or a
+ * delta light's absent one) adds +0: the reference's f_brdf = Li_brdf = 0 with pdfs 1 (:311). */
+static v3 mis_accumulate(const mis_t *m, int vl, int vb) {
+    v3 acc = V(0.f, 0.f, 0.f);
+    if (m->condL && vl) acc = vadd(acc, m->cL);
+    if (m->hasvis && vb) {
+        if (m->condB) acc = vadd(acc, m->cB);
+    } else {
+        acc = vadd(acc, V(0.f, 0.f, 0.f));
+    }
+    return acc;
+}
+
+/* wf_logic (wavefront_kernels.cu:124-205) for one live path: background at len 1, termination,
+ * the MIS sum, throughput update and Russian roulette.  Updates *beta and the film Ld; returns
+ * 1 if the path continues. */
+static int logic_core(const or_scene *sc, const or_config *cfg, const rng_t *r, uint32_t len, int found, v3 ray_d,
+                      v3 *beta_io, const mis_t *m, int vl, int vb, float *Ld) {
+    int nmb_lights = 1 + sc->ndir;
+    int D = cfg->max_depth;
+    v3 beta = *beta_io;
+    int terminate = 0;
+    if (len == 1 && found) {                                   /* :131-133: Vec3f(0)*beta */
+        v3 z = vmul(V(0.f, 0.f, 0.f), beta);
+        Ld[0] = Ld[0] + z.x; Ld[1] = Ld[1] + z.y; Ld[2] = Ld[2] + z.z;
+    }
+    if (len == 1 && !found) {                                  /* :134-139 */
+        int nbg = cfg->fixed ? 1 : nmb_lights;                  /* fixed: background once */
+        for (int i = 0; i < nbg; i++) {
+            v3 Le = vmul(env_L(sc, ray_d), beta);
+            Ld[0] = Ld[0] + Le.x; Ld[1] = Ld[1] + Le.y; Ld[2] = Ld[2] + Le.z;
+        }
+    }
+    if (len > (uint32_t)D || !found) terminate = 1;            /* :142-146 */
+    if (len > (uint32_t)D) return 0;                           /* :148 */
+    if (len > 1) {                                             /* :150-197 */
+        v3 acc = mis_accumulate(m, vl, vb);
+        v3 add = vmul(acc, beta);
+        Ld[0] = Ld[0] + add.x; Ld[1] = Ld[1] + add.y; Ld[2] = Ld[2] + add.z;
+        if (m->fzero) return 0;
+        *beta_io = vmul(*beta_io, m->ratio);
+        if (len > (uint32_t)cfg->rr_depth) {
+            if (cfg->fixed) { /* fixed: q from the updated throughput, survivors reweighted */
+                float qq = fmx(0.05f, 1.f - beta_io->y);
+                if (rnd(r, SL_RR) < qq) return 0;
+                *beta_io = vdivs(*beta_io, 1.f - qq);
+            } else {
+                float qq = fmx(0.05f, 1.f - beta.y);
+                if (rnd(r, SL_RR) < qq) return 0;
+                /* beta /= 1-q applies to a local and is never stored (:195) */
+            }
+        }
+    }
+    return !terminate;
+}
+
+/* :207-213: the light choice and the shadow ray of a continuing path. */
+static void pick_light(const or_scene *sc, int fixed, const rng_t *r, path_t *p) {
+    int nmb_lights = 1 + sc->ndir;
+    int l_id = (int)(rnd(r, SL_LIGHT) * (float)(nmb_lights - 0) + (float)0); /* rand_int :48-51 */
+    p->light_id = (uint32_t)((l_id == nmb_lights) ? 0 : l_id);
+    v3 ldir;
+    light_dir(sc, (int)p->light_id, r, &ldir, fixed);
+    p->ray_light.o = vadd(p->isect.position, vscale(p->isect.normal, 0.01f));
+    p->ray_light.d = ldir;
+}
+
 /* wf_logic (wavefront_kernels.cu:90-223) for one pixel. */
 static void wf_logic(ctx_t *c, queues_t *q, int x, int y) {
     const or_scene *sc = c->sc;
@@ -888,65 +984,17 @@ static void wf_logic(ctx_t *c, queues_t *q, int x, int y) {
     if (x >= W - 1 || y >= c->H - 1) return;                   /* :110 */
     uint32_t pid = (uint32_t)y * (uint32_t)W + (uint32_t)x;
     path_t *p = &c->paths[pid];
-    int nmb_lights = 1 + sc->ndir;
-    int D = c->cfg->max_depth, spp = c->cfg->spp;
-    v3 beta = p->beta;
-    uint32_t len = p->len;
+    int spp = c->cfg->spp;
     float *Ld = c->Ld + 3 * (int64_t)pid;
     if (!p->dead && c->samples[pid] < (uint32_t)spp) {        /* :124 */
-        int terminate = 0;
-        rng_t r = path_rng(c, pid, len);
-        if (len == 1 && p->isect.was_found) {                  /* :131-133: Vec3f(0)*beta */
-            v3 z = vmul(V(0.f, 0.f, 0.f), beta);
-            Ld[0] = Ld[0] + z.x; Ld[1] = Ld[1] + z.y; Ld[2] = Ld[2] + z.z;
-        }
-        if (len == 1 && !p->isect.was_found) {                 /* :134-139 */
-            int nbg = c->cfg->fixed ? 1 : nmb_lights;           /* fixed: background once */
-            for (int i = 0; i < nbg; i++) {
-                v3 Le = vmul(env_L(sc, p->ray.d), beta);
-                Ld[0] = Ld[0] + Le.x; Ld[1] = Ld[1] + Le.y; Ld[2] = Ld[2] + Le.z;
-            }
-        }
-        if (len > (uint32_t)D || !p->isect.was_found) terminate = 1;  /* :142-146 */
-        if (len > (uint32_t)D) goto TERMINATE;                 /* :148 */
-        if (len > 1) {                                         /* :150-197 */
-            v3 acc = V(0.f, 0.f, 0.f);
-            float w = or_power_heuristic(p->pdf_light[0], p->pdf_brdf[1]);
-            if (w > 0.f && p->visible && p->pdf_light[0] > 0.f)
-                acc = vadd(acc, vdivs(vscale(vmul(p->f_light, p->Li_light), w), p->pdf_light[0]));
-            w = or_power_heuristic(p->pdf_brdf[0], p->pdf_light[1]);
-            if (w > 0.f && p->pdf_brdf[0] > 0.f)
-                acc = vadd(acc, vdivs(vscale(vmul(p->f_brdf, p->Li_brdf), w), p->pdf_brdf[0]));
-            v3 add = vmul(acc, beta);
-            Ld[0] = Ld[0] + add.x; Ld[1] = Ld[1] + add.y; Ld[2] = Ld[2] + add.z;
-            if ((p->f_sample.x == 0.f && p->f_sample.y == 0.f && p->f_sample.z == 0.f) || p->pdf_sample == 0.f) {
-                terminate = 1;
-                goto TERMINATE;
-            }
-            p->beta = vmul(p->beta, vdivs(p->f_sample, p->pdf_sample));
-            if (len > (uint32_t)c->cfg->rr_depth) {
-                if (c->cfg->fixed) { /* fixed: q from the updated throughput, survivors reweighted */
-                    float qq = fmx(0.05f, 1.f - p->beta.y);
-                    if (rnd(&r, SL_RR) < qq) { terminate = 1; goto TERMINATE; }
-                    p->beta = vdivs(p->beta, 1.f - qq);
-                } else {
-                    float qq = fmx(0.05f, 1.f - beta.y);
-                    if (rnd(&r, SL_RR) < qq) { terminate = 1; goto TERMINATE; }
-                    /* beta /= 1-q applies to a local and is never stored (:195) */
-                }
-            }
-        }
-TERMINATE:
-        if (terminate) {
-            p->dead = 1;
+        rng_t r = path_rng(c, pid, p->len);
+        /* the previous vertex's terms; an occluded BRDF sample already zeroed f_brdf (:311) */
+        mis_t m = mis_terms(p, 1);
+        if (!logic_core(sc, c->cfg, &r, p->len, p->isect.was_found, p->ray.d, &p->beta, &m, p->visible, 1, Ld)) {
+            p->dead = 1;                                       /* :199-204 */
             c->samples[pid]++;
         } else {
-            int l_id = (int)(rnd(&r, SL_LIGHT) * (float)(nmb_lights - 0) + (float)0); /* rand_int :48-51 */
-            p->light_id = (uint32_t)((l_id == nmb_lights) ? 0 : l_id);
-            v3 ldir;
-            light_dir(sc, (int)p->light_id, &r, &ldir, c->cfg->fixed);
-            p->ray_light.o = vadd(p->isect.position, vscale(p->isect.normal, 0.01f));
-            p->ray_light.d = ldir;
+            pick_light(sc, c->cfg->fixed, &r, p);
             q->matq[q->nmat++] = (int32_t)pid;
         }
     }
@@ -987,12 +1035,20 @@ static void wf_shadow(ctx_t *c, queues_t *q, uint32_t id) {
     q->cnt[5] += st.tris;
 }
 
-/* wf_mat_mix (wavefront_kernels.cu:295-375) with the inline visibility ray. */
-static void wf_mat_mix(ctx_t *c, queues_t *q, uint32_t id) {
-    const or_scene *sc = c->sc;
-    path_t *p = &c->paths[id];
-    rng_t r = path_rng(c, id, p->len);
-    v3 f_light, Li_light, f_brdf = V(0.f, 0.f, 0.f), Li_brdf = V(0.f, 0.f, 0.f);
+/* The BRDF sample of wf_mat_mix (:331-345) as if it were visible: its direction, visibility ray
+ * and terms.  has = 0 for a delta light (no BRDF sample is drawn). */
+typedef struct {
+    int has;
+    ray_t vis;
+    v3 f_brdf, Li_brdf;
+    float pdf_brdf0, pdf_light1;
+} brdf_sample_t;
+
+/* wf_mat_mix (wavefront_kernels.cu:295-375) without the inline visibility trace: writes the light
+ * sample, the continuation and the next ray into p (BRDF-sample fields at the reference's
+ * occluded defaults f = Li = 0, pdfs 1, :311) and returns the BRDF sample in *bs. */
+static void mat_mix_core(const or_scene *sc, int fixed, const rng_t *r, path_t *p, brdf_sample_t *bs) {
+    v3 f_light, Li_light;
     float pdf_light[2] = {1.f, 1.f}, pdf_brdf[2] = {1.f, 1.f};
     const isect_t *is = &p->isect;
     int light_id = (int)p->light_id;
@@ -1004,44 +1060,149 @@ static void wf_mat_mix(ctx_t *c, queues_t *q, uint32_t id) {
 
     f_light = vadd(spec_get_f(&m, n, light_wi, wo), diff_get_f(&m, n, light_wi, wo)); /* :326 */
     Li_light = light_L(sc, light_id, light_wi);
-    int fixed = c->cfg->fixed;
     float sel = fixed ? 1.f / (float)(1 + sc->ndir) : 1.f;   /* fixed: light-selection pdf 1/N */
     pdf_light[0] = light_pdf(sc, light_id, light_wi, fixed);
     if (fixed) pdf_light[0] = pdf_light[0] * sel;
     pdf_brdf[1] = !delta ? (diff_get_pdf() + spec_get_pdf(&m, n, light_wi, wo)) * 0.5f
                          : (fixed ? 0.f : 1.f);               /* fixed: delta-light MIS weight 1 */
+    bs->has = !delta;
     if (!delta) {                                              /* :332-345 */
-        v3 wi_brdf = (rnd(&r, SL_MAT_LOBE) < 0.5f) ? spec_get_wi(&m, n, wo, &r, SL_MAT_E0, fixed)
-                                                   : diff_get_wi(n, &r, SL_MAT_E0, fixed);
-        ray_t vis;
-        vis.o = vadd(is->position, vscale(wi_brdf, 0.001f));
-        vis.d = wi_brdf;
-        trav_stats st = {0, 0};
-        int occluded = any_hit(sc, &vis, c->cfg->traversal, &st);
-        q->cnt[4] += st.nodes;
-        q->cnt[5] += st.tris;
-        q->cnt[2]++;
-        if (!occluded) {
-            f_brdf = vadd(spec_get_f(&m, n, wi_brdf, wo), diff_get_f(&m, n, wi_brdf, wo));
-            Li_brdf = light_L(sc, light_id, wi_brdf);
-            pdf_brdf[0] = (diff_get_pdf() + spec_get_pdf(&m, n, wi_brdf, wo)) * 0.5f;
-            pdf_light[1] = light_pdf(sc, light_id, wi_brdf, fixed);
-            if (fixed) pdf_light[1] = pdf_light[1] * sel;
-        }
+        v3 wi_brdf = (rnd(r, SL_MAT_LOBE) < 0.5f) ? spec_get_wi(&m, n, wo, r, SL_MAT_E0, fixed)
+                                                  : diff_get_wi(n, r, SL_MAT_E0, fixed);
+        bs->vis.o = vadd(is->position, vscale(wi_brdf, 0.001f));
+        bs->vis.d = wi_brdf;
+        bs->f_brdf = vadd(spec_get_f(&m, n, wi_brdf, wo), diff_get_f(&m, n, wi_brdf, wo));
+        bs->Li_brdf = light_L(sc, light_id, wi_brdf);
+        bs->pdf_brdf0 = (diff_get_pdf() + spec_get_pdf(&m, n, wi_brdf, wo)) * 0.5f;
+        bs->pdf_light1 = light_pdf(sc, light_id, wi_brdf, fixed);
+        if (fixed) bs->pdf_light1 = bs->pdf_light1 * sel;
     }
-    v3 wi_s = (rnd(&r, SL_CONT_LOBE) < 0.5f) ? spec_get_wi(&m, n, wo, &r, SL_CONT_E0, fixed)  /* :353 */
-                                             : diff_get_wi(n, &r, SL_CONT_E0, fixed);
+    v3 wi_s = (rnd(r, SL_CONT_LOBE) < 0.5f) ? spec_get_wi(&m, n, wo, r, SL_CONT_E0, fixed)  /* :353 */
+                                            : diff_get_wi(n, r, SL_CONT_E0, fixed);
     float pdf_s = (diff_get_pdf() + spec_get_pdf(&m, n, wi_s, wo)) * 0.5f;
     v3 f_s = vadd(spec_get_f(&m, n, wi_s, wo), diff_get_f(&m, n, wi_s, wo));
-    p->Li_light = Li_light; p->Li_brdf = Li_brdf;
-    p->f_light = f_light; p->f_brdf = f_brdf; p->f_sample = f_s;
+    p->Li_light = Li_light; p->Li_brdf = V(0.f, 0.f, 0.f);
+    p->f_light = f_light; p->f_brdf = V(0.f, 0.f, 0.f); p->f_sample = f_s;
     p->pdf_light[0] = pdf_light[0]; p->pdf_light[1] = pdf_light[1];
     p->pdf_brdf[0] = pdf_brdf[0]; p->pdf_brdf[1] = pdf_brdf[1];
     p->pdf_sample = pdf_s;
     p->ray.o = vadd(is->position, vscale(n, 0.001f));         /* :358 */
     p->ray.d = wi_s;
+}
+
+/* a visible BRDF sample's terms (:340-343) */
+static void apply_brdf_sample(path_t *p, const brdf_sample_t *bs) {
+    p->f_brdf = bs->f_brdf;
+    p->Li_brdf = bs->Li_brdf;
+    p->pdf_brdf[0] = bs->pdf_brdf0;
+    p->pdf_light[1] = bs->pdf_light1;
+}
+
+/* wf_mat_mix (wavefront_kernels.cu:295-375) with the inline visibility ray. */
+static void wf_mat_mix(ctx_t *c, queues_t *q, uint32_t id) {
+    path_t *p = &c->paths[id];
+    rng_t r = path_rng(c, id, p->len);
+    brdf_sample_t bs;
+    mat_mix_core(c->sc, c->cfg->fixed, &r, p, &bs);
+    if (bs.has) {                                              /* :334-345 */
+        trav_stats st = {0, 0};
+        int occluded = any_hit(c->sc, &bs.vis, c->cfg->traversal, &st);
+        q->cnt[4] += st.nodes;
+        q->cnt[5] += st.tris;
+        q->cnt[2]++;
+        if (!occluded) apply_brdf_sample(p, &bs);
+    }
     q->extq[q->next++] = (int32_t)id;
     q->shq[q->nsh++] = (int32_t)id;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Stage restatements at the product's stage boundary (mcpt_path_view).       */
+/* ------------------------------------------------------------------------- */
+enum { PF_DEAD = 1u, PF_LEN_SHIFT = 1, PF_CONDL = 1u << 9, PF_CONDB = 1u << 10, PF_FZERO = 1u << 11,
+       PF_HASVIS = 1u << 12, PF_SIDX_SHIFT = 13 };
+
+void or_stage_logic(const or_scene *sc, const or_camera *cam, const or_config *cfg, int32_t W, int32_t H,
+                    uint32_t *flags, uint32_t *samples, const int32_t *hit_tri, float *ray_o, float *ray_d,
+                    float *beta, const float *nee0, const float *nee1, const uint8_t *vis, float *Ld,
+                    uint8_t *queued) {
+    uint32_t spp = (uint32_t)cfg->spp;
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            uint32_t i = (uint32_t)y * (uint32_t)W + (uint32_t)x;
+            queued[i] = 0;
+            if (x >= W - 1 || y >= H - 1) continue;            /* :110 */
+            uint32_t fl = flags[i];
+            int dead = (fl & PF_DEAD) != 0;
+            uint32_t len = (fl >> PF_LEN_SHIFT) & 0xffu, sidx = fl >> PF_SIDX_SHIFT;
+            if (!dead && sidx < spp) {                         /* :124 */
+                rng_t r = {rng_key(cfg->seed, i, sidx), len};
+                mis_t m;
+                m.cL = V(nee0[4 * i], nee0[4 * i + 1], nee0[4 * i + 2]);
+                m.cB = V(nee1[4 * i], nee1[4 * i + 1], nee1[4 * i + 2]);
+                m.ratio = V(beta[4 * i + 3], nee0[4 * i + 3], nee1[4 * i + 3]);
+                m.condL = (fl & PF_CONDL) != 0;
+                m.condB = (fl & PF_CONDB) != 0;
+                m.hasvis = (fl & PF_HASVIS) != 0;
+                m.fzero = (fl & PF_FZERO) != 0;
+                v3 b = V(beta[4 * i], beta[4 * i + 1], beta[4 * i + 2]);
+                if (len == 1) b = V(1.f, 1.f, 1.f);           /* wf_generate's beta (:245) */
+                v3 rd = V(ray_d[3 * i], ray_d[3 * i + 1], ray_d[3 * i + 2]);
+                if (!logic_core(sc, cfg, &r, len, hit_tri[i] >= 0, rd, &b, &m, vis[2 * i], vis[2 * i + 1], Ld + 3 * (size_t)i)) {
+                    dead = 1;                                  /* :199-204 */
+                    samples[i]++;
+                } else {
+                    beta[4 * i] = b.x; beta[4 * i + 1] = b.y; beta[4 * i + 2] = b.z;
+                    queued[i] |= 2;
+                }
+            }
+            if (dead) {
+                flags[i] = PF_DEAD;
+                if (samples[i] < spp) {                        /* :219-222 + wf_generate (:225-251) */
+                    rng_t r0 = {rng_key(cfg->seed, i, samples[i]), 0};
+                    ray_t ray = gen_ray(cam, W, H, x, y, &r0);
+                    ray_o[3 * i] = ray.o.x; ray_o[3 * i + 1] = ray.o.y; ray_o[3 * i + 2] = ray.o.z;
+                    ray_d[3 * i] = ray.d.x; ray_d[3 * i + 1] = ray.d.y; ray_d[3 * i + 2] = ray.d.z;
+                    flags[i] = (1u << PF_LEN_SHIFT) | (samples[i] << PF_SIDX_SHIFT);
+                    queued[i] |= 1;
+                }
+            }
+        }
+}
+
+void or_stage_material(const or_scene *sc, const or_config *cfg, int32_t n, uint32_t *flags, const int32_t *hit_tri,
+                       float *ray_o, float *ray_d, float *beta, float *nee0, float *nee1, float *light_o,
+                       float *light_d, float *bvis_o, float *bvis_d) {
+    for (int32_t i = 0; i < n; i++) {
+        uint32_t fl = flags[i];
+        uint32_t len = (fl >> PF_LEN_SHIFT) & 0xffu, sidx = fl >> PF_SIDX_SHIFT;
+        rng_t r = {rng_key(cfg->seed, (uint32_t)i, sidx), len};
+        path_t p;
+        memset(&p, 0, sizeof(p));
+        p.ray.o = V(ray_o[3 * i], ray_o[3 * i + 1], ray_o[3 * i + 2]);
+        p.ray.d = V(ray_d[3 * i], ray_d[3 * i + 1], ray_d[3 * i + 2]);
+        p.isect = make_isect(sc, &p.ray, hit_tri[i], K_HUGE);
+        pick_light(sc, cfg->fixed, &r, &p);                    /* wf_logic :207-213 */
+        brdf_sample_t bs;
+        mat_mix_core(sc, cfg->fixed, &r, &p, &bs);
+        if (bs.has) apply_brdf_sample(&p, &bs);                /* the terms as if visible */
+        mis_t m = mis_terms(&p, bs.has);
+        uint32_t nf = (m.fzero ? PF_FZERO : 0u) | (m.condL ? PF_CONDL : 0u) | (bs.has && m.condB ? PF_CONDB : 0u) |
+                      (bs.has ? PF_HASVIS : 0u);
+        flags[i] = nf | ((len + 1) << PF_LEN_SHIFT) | (sidx << PF_SIDX_SHIFT);
+        v3 cB = bs.has ? m.cB : V(0.f, 0.f, 0.f);
+        beta[4 * i + 3] = m.ratio.x;
+        nee0[4 * i] = m.cL.x; nee0[4 * i + 1] = m.cL.y; nee0[4 * i + 2] = m.cL.z; nee0[4 * i + 3] = m.ratio.y;
+        nee1[4 * i] = cB.x; nee1[4 * i + 1] = cB.y; nee1[4 * i + 2] = cB.z; nee1[4 * i + 3] = m.ratio.z;
+        ray_o[3 * i] = p.ray.o.x; ray_o[3 * i + 1] = p.ray.o.y; ray_o[3 * i + 2] = p.ray.o.z;
+        ray_d[3 * i] = p.ray.d.x; ray_d[3 * i + 1] = p.ray.d.y; ray_d[3 * i + 2] = p.ray.d.z;
+        light_o[3 * i] = p.ray_light.o.x; light_o[3 * i + 1] = p.ray_light.o.y; light_o[3 * i + 2] = p.ray_light.o.z;
+        light_d[3 * i] = p.ray_light.d.x; light_d[3 * i + 1] = p.ray_light.d.y; light_d[3 * i + 2] = p.ray_light.d.z;
+        float qn = qnan();
+        v3 vo = bs.has ? bs.vis.o : V(qn, qn, qn), vd = bs.has ? bs.vis.d : V(qn, qn, qn);
+        bvis_o[3 * i] = vo.x; bvis_o[3 * i + 1] = vo.y; bvis_o[3 * i + 2] = vo.z;
+        bvis_d[3 * i] = vd.x; bvis_d[3 * i + 1] = vd.y; bvis_d[3 * i + 2] = vd.z;
+    }
 }
 
 /* wavefront_pathtrace (wavefront_kernels.cu:377-442) iterated until the tile

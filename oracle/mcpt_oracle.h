@@ -69,7 +69,8 @@ typedef struct or_config {
     int32_t rr_depth;     /* 'path_length > 3' (wavefront_kernels.cu:189)      */
     int32_t tile_w, tile_h;
     int32_t nthreads;
-    int32_t traversal;    /* 0 = reference stack traversal, 1 = brute force   */
+    int32_t traversal;    /* 0 = reference stack traversal, 1 = brute force, 2 = stack traversal with
+                             the literal reference leaf rule (no own-box check, first visited wins) */
     int32_t row_begin, row_end;  /* restrict to rows [begin,end); 0,0 = all */
     int32_t fixed;        /* 1 = quality mode (product MCPT_FLAG_FIXED) */
     int32_t tile_mod, tile_rank;  /* tile_mod > 0: only tiles with (tx+ty) % tile_mod == tile_rank
@@ -110,6 +111,24 @@ void or_env_dir(const or_scene *sc, float ex, float ey, float *wi);
 void or_brdf_eval(const float *params, const float *n, const float *wi, const float *wo, float *out);
 float or_power_heuristic(float f, float g);
 int32_t or_upper_bound(const float *list, int32_t size, float val);
+/* Per-stage restatements at the product's shading-stage boundary (include/mcpt.h mcpt_path_view;
+ * SURVEY.md section 4 item 2): the same logic_core / mis_terms / pick_light / mat_mix_core the
+ * full render runs.  Arrays are host SoA over n paths, path i = pixel i.
+ * or_stage_logic: wf_logic + wf_generate (wavefront_kernels.cu:90-251) of a W x H film (n = W*H),
+ *   one path per pixel.  In: flags, samples, hit_tri, ray_d (3n), beta/nee0/nee1 (4n), vis (2n),
+ *   Ld (3n).  Out (may alias the inputs): flags, samples, Ld, ray_o/ray_d of generated paths,
+ *   beta (xyz updated for continuing paths), queued (bit 1: continues into the material stage).
+ * or_stage_material: the light choice (:207-213) + wf_mat_mix (:295-375) of continuing paths.
+ *   In: flags (len, sample index), hit_tri, ray_o/ray_d, beta.  Out: flags, ray_o/ray_d (next
+ *   extension ray), beta (xyz, ratio.x), nee0/nee1 (4n), light_o/light_d and bvis_o/bvis_d
+ *   (3n; NaN for a delta light's absent visibility ray). */
+void or_stage_logic(const or_scene *sc, const or_camera *cam, const or_config *cfg, int32_t W, int32_t H,
+                    uint32_t *flags, uint32_t *samples, const int32_t *hit_tri, float *ray_o, float *ray_d,
+                    float *beta, const float *nee0, const float *nee1, const uint8_t *vis, float *Ld,
+                    uint8_t *queued);
+void or_stage_material(const or_scene *sc, const or_config *cfg, int32_t n, uint32_t *flags, const int32_t *hit_tri,
+                       float *ray_o, float *ray_d, float *beta, float *nee0, float *nee1, float *light_o,
+                       float *light_d, float *bvis_o, float *bvis_d);
 void or_gen_ray(const or_camera *cam, int32_t W, int32_t H, int32_t x, int32_t y,
                 uint64_t seed, uint32_t pixel, uint32_t sample, float *o, float *d);
 const char *or_version(void);

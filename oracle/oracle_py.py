@@ -68,6 +68,11 @@ def lib():
             "or_upper_bound": (C.c_int32, [_f, C.c_int32, C.c_float]),
             "or_gen_ray": (None, [C.POINTER(OrCamera), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_uint64,
                                   C.c_uint32, C.c_uint32, _f, _f]),
+            "or_stage_logic": (None, [C.POINTER(OrScene), C.POINTER(OrCamera), C.POINTER(OrConfig), C.c_int32,
+                                      C.c_int32, _u, _u, _i, _f, _f, _f, _f, _f, C.POINTER(C.c_uint8), _f,
+                                      C.POINTER(C.c_uint8)]),
+            "or_stage_material": (None, [C.POINTER(OrScene), C.POINTER(OrConfig), C.c_int32, _u, _i, _f, _f, _f,
+                                         _f, _f, _f, _f, _f, _f]),
             "or_version": (C.c_char_p, []),
         }
         for n, (r, a) in sig.items():
@@ -189,3 +194,47 @@ def env_build(tex: np.ndarray):
     den = np.zeros(1, np.float32)
     lib().or_env_build(W, H, fptr(tex), fptr(my), fptr(mp), fptr(cy), fptr(pdf), fptr(den))
     return {"marginal_y": my, "marginal_p": mp, "conds_y": cy, "pdf": pdf, "denom": float(den[0])}
+
+
+def _stage_cfg(spp, max_depth, rr_depth, seed, fixed):
+    return OrConfig(seed, spp, max_depth, rr_depth, 256, 256, 1, 0, 0, 0, int(fixed), 0, 0)
+
+
+def _a(state, k, dt, shape):
+    return np.ascontiguousarray(state[k], dt).reshape(shape).copy()
+
+
+def stage_logic(arrays, cam, W, H, state, spp, max_depth=5, rr_depth=3, seed=0x5EED2026, fixed=False):
+    """or_stage_logic: wf_logic + wf_generate over product-form path state (mcpt_path_view fields)."""
+    n = W * H
+    s = scene_struct(arrays)
+    c = camera_struct(cam)
+    cfg = _stage_cfg(spp, max_depth, rr_depth, seed, fixed)
+    fl, sm = _a(state, "flags", np.uint32, n), _a(state, "samples", np.uint32, n)
+    ht = _a(state, "hit_tri", np.int32, n)
+    ro = _a(state, "ray_o", np.float32, (n, 3)) if "ray_o" in state else np.zeros((n, 3), np.float32)
+    rd, be = _a(state, "ray_d", np.float32, (n, 3)), _a(state, "beta", np.float32, (n, 4))
+    n0, n1 = _a(state, "nee0", np.float32, (n, 4)), _a(state, "nee1", np.float32, (n, 4))
+    vis, Ld = _a(state, "vis", np.uint8, (n, 2)), _a(state, "Ld", np.float32, (n, 3))
+    q = np.zeros(n, np.uint8)
+    u8 = C.POINTER(C.c_uint8)
+    lib().or_stage_logic(C.byref(s), C.byref(c), C.byref(cfg), W, H, fl.ctypes.data_as(_u), sm.ctypes.data_as(_u),
+                         ht.ctypes.data_as(_i), fptr(ro), fptr(rd), fptr(be), fptr(n0), fptr(n1), vis.ctypes.data_as(u8),
+                         fptr(Ld), q.ctypes.data_as(u8))
+    return {"flags": fl, "samples": sm, "ray_o": ro, "ray_d": rd, "beta": be, "Ld": Ld, "queued": q}
+
+
+def stage_material(arrays, state, max_depth=5, rr_depth=3, seed=0x5EED2026, fixed=False):
+    """or_stage_material: light choice + wf_mat_mix over product-form continuing paths."""
+    n = len(state["flags"])
+    s = scene_struct(arrays)
+    cfg = _stage_cfg(0, max_depth, rr_depth, seed, fixed)
+    fl, ht = _a(state, "flags", np.uint32, n), _a(state, "hit_tri", np.int32, n)
+    ro, rd = _a(state, "ray_o", np.float32, (n, 3)), _a(state, "ray_d", np.float32, (n, 3))
+    be = _a(state, "beta", np.float32, (n, 4))
+    n0, n1 = np.zeros((n, 4), np.float32), np.zeros((n, 4), np.float32)
+    lo, ld, bo, bd = (np.zeros((n, 3), np.float32) for _ in range(4))
+    lib().or_stage_material(C.byref(s), C.byref(cfg), n, fl.ctypes.data_as(_u), ht.ctypes.data_as(_i), fptr(ro),
+                            fptr(rd), fptr(be), fptr(n0), fptr(n1), fptr(lo), fptr(ld), fptr(bo), fptr(bd))
+    return {"flags": fl, "ray_o": ro, "ray_d": rd, "beta": be, "nee0": n0, "nee1": n1, "light_o": lo, "light_d": ld,
+            "bvis_o": bo, "bvis_d": bd}

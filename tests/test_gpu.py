@@ -877,3 +877,66 @@ def test_env_device_tables_same_film(mcpt_mod, scene_c2):
         pt.close()
     (L0, s0), (L1, s1) = films
     assert np.array_equal(s0, s1) and np.array_equal(L0.view(np.uint32), L1.view(np.uint32))
+
+
+def _same(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    if a.dtype.kind == "f":
+        return bool(np.array_equal(a.view(np.uint32), b.view(np.uint32)) or
+                    np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(a[~np.isnan(a)], b[~np.isnan(b)]))
+    return bool(np.array_equal(a, b))
+
+
+@pytest.mark.parametrize("stage", ["logic", "generate", "material"])
+def test_stage_golden_vectors(mcpt_mod, oracle, stage):
+    """Per-stage golden vectors: mcpt_stage_run runs the product's
+    k_shade (LOGIC / GENERATE: wf_logic + wf_generate, wavefront_kernels.cu:90-251) or k_material
+    (MATERIAL: light choice + wf_mat_mix, :207-213, 295-375) on the fixture's path state; every
+    output field equals the oracle's stage restatement (tools/make_golden.py) bit for bit.  Rays
+    the kernels resolve in place because they cannot hit the scene are checked against the
+    oracle's traversal instead of a queue entry."""
+    import stage_fixtures as sf
+
+    g = np.load(os.path.join(GOLDEN, f"stage_{stage}_c1dir.npz"))
+    inp = {k[3:]: g[k] for k in g.files if k.startswith("in_")}
+    ref = {k[4:]: g[k] for k in g.files if k.startswith("out_")}
+    s = sf.stage_scene(mcpt_mod)
+    a = s.arrays()
+    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=sf.SPP, max_depth=sf.DEPTH, rr_depth=sf.RR))
+    pt.upload_scene(s)
+    pt.set_camera(sf.stage_camera(mcpt_mod))
+    got = pt.stage(stage, inp, film=sf.FILM if stage != "material" else None)
+    pt.close()
+    if stage in ("logic", "generate"):
+        for k in ("flags", "samples", "Ld"):
+            assert _same(got[k], ref[k]), k
+        cont = (ref["queued"] & 2) > 0
+        assert np.array_equal((got["queued"] & 2) > 0, cont)
+        assert _same(got["beta"][cont, :3], ref["beta"][cont, :3])
+        gen = (ref["queued"] & 1) > 0
+        assert gen.sum() > 50 and (stage == "generate" or cont.sum() > 50)
+        assert _same(got["ray_o"][gen], ref["ray_o"][gen]) and _same(got["ray_d"][gen], ref["ray_d"][gen])
+        queued = (got["queued"] & 1) > 0
+        assert not queued[~gen].any()
+        resolved = gen & ~queued  # camera rays missing the scene: resolved in place, never queued
+        assert np.all(got["hit_tri"][resolved] == -1)
+        if resolved.any():
+            assert np.all(oracle.trace_closest(a, ref["ray_o"][resolved], ref["ray_d"][resolved])[2] == -1)
+    else:
+        for k in ("flags", "ray_o", "ray_d", "beta", "nee0", "nee1"):
+            assert _same(got[k], ref[k]), k
+        q = got["queued"]
+        ext_resolved = (q & 1) == 0
+        if ext_resolved.any():
+            assert np.all(got["hit_tri"][ext_resolved] == -1)
+            assert np.all(oracle.trace_closest(a, ref["ray_o"][ext_resolved], ref["ray_d"][ext_resolved])[2] == -1)
+        for bit, vk, o_k, d_k in ((4, 0, "light_o", "light_d"), (8, 1, "bvis_o", "bvis_d")):
+            drawn = ~np.isnan(ref[o_k][:, 0])
+            qd = (q & bit) > 0
+            assert not qd[~drawn].any()
+            assert _same(got[o_k][qd], ref[o_k][qd]) and _same(got[d_k][qd], ref[d_k][qd])
+            res = drawn & ~qd  # resolved in place: visible
+            assert np.all(got["vis"][res, vk] == 1)
+            if res.any():
+                assert np.all(oracle.trace_any(a, ref[o_k][res], ref[d_k][res]) == 1)
+        assert (q & 4).sum() > 50 and (q & 8).sum() > 20 and np.isnan(ref["bvis_o"][:, 0]).sum() > 50

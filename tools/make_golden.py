@@ -12,9 +12,10 @@ import sys
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(REPO, "mc-path-tracer_amd"), os.path.join(REPO, "oracle")]
+sys.path[:0] = [os.path.join(REPO, "mc-path-tracer_amd"), os.path.join(REPO, "oracle"), os.path.join(REPO, "tests")]
 import mcpt  # noqa: E402
 import oracle_py as op  # noqa: E402
+import stage_fixtures as sf  # noqa: E402
 
 OUT = os.environ.get("GOLDEN_OUT", os.path.join(REPO, "tests", "golden"))
 
@@ -58,7 +59,27 @@ def main():
         pt, nm, tri = op.trace_closest(arr, ro, rd)  # tri: triangle ids (scene order, any BVH)
         vis = op.trace_any(arr, ro, rd)
         np.savez_compressed(os.path.join(OUT, f"trace_{name}_256.npz"), ro=ro, rd=rd, pos_t=pt, nrm_mat=nm, tri=tri, vis=vis)
+    stage_vectors()
     print("golden fixtures written to", OUT)
+
+
+def stage_vectors():
+    """Per-stage golden vectors: inputs from tests/stage_fixtures.py,
+    outputs from the oracle's stage restatements, diffed field by field against mcpt_stage_run
+    by tests/test_gpu.py::test_stage_golden_vectors."""
+    s = sf.stage_scene(mcpt)
+    a = s.arrays()
+    cam = sf.stage_camera(mcpt)
+    W, H = sf.FILM
+    kw = dict(max_depth=sf.DEPTH, rr_depth=sf.RR)
+    for name, st in (("logic", sf.logic_state(len(a["mat"]))), ("generate", sf.logic_state(len(a["mat"]), True))):
+        out = op.stage_logic(a, cam, W, H, st, sf.SPP, **kw)
+        np.savez_compressed(os.path.join(OUT, f"stage_{name}_c1dir.npz"), **{"in_" + k: v for k, v in st.items()},
+                            **{"out_" + k: v for k, v in out.items()})
+    st = sf.material_state(a, op.trace_closest)
+    out = op.stage_material(a, st, **kw)
+    np.savez_compressed(os.path.join(OUT, "stage_material_c1dir.npz"), **{"in_" + k: v for k, v in st.items()},
+                        **{"out_" + k: v for k, v in out.items()})
 
 
 if __name__ == "__main__":
