@@ -248,23 +248,24 @@ struct MatOut {
     uint32_t trivial_any;
 };
 
-// Light choice + wf_mat_mix for the continuing path pid (vertex len, sample
-// `samples`, throughput `beta_store` after the logic update).
+// Light choice + wf_mat_mix for the continuing path pid (vertex len, sample index
+// `sidx`, throughput `beta_store` after the logic update).
 //
 // FIXED (quality mode, mcpt_config.flags & MCPT_FLAG_FIXED) changes, each
 // a reference quirk of Appendix A: light-selection pdf 1/N folded into both light pdfs
 // (A.6), delta lights get MIS weight 1 (pdf_brdf.y = 0 instead of 1, A.7), textbook
 // Gram-Schmidt (A.9), env sampling/pdf on matched, clamped cells (A.11).
 template <bool FIXED>
-__device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t samples, uint32_t len, V3 beta_store,
+__device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sidx, uint32_t len, V3 beta_store,
                                  int32_t htri, float4* stage) {
     const DevScene& sc = a.scene;
     MatOut mo{false, false, false, false, false, 0u};
     SPROF_T0();
-    // path slot -> (pixel, sample index): slot k of a pixel runs samples k, k + S, k + 2S, ...
+    // path slot -> pixel; the sample index comes with the record (k_shade: slot k of a pixel
+    // runs samples k, k + S, k + 2S, ...)
     const uint32_t npix = (uint32_t)a.W * (uint32_t)a.H;
     const uint32_t slot = a.slots > 1 ? pid / npix : 0u;
-    const Rng r{rng_key(a.seed, pid - slot * npix, slot + (uint32_t)a.slots * samples), len};
+    const Rng r{rng_key(a.seed, pid - slot * npix, sidx), len};
     const V3 ro = xyz(a.p.ray_o[pid]), rdir = xyz(a.p.ray_d[pid]);
     V3 pos, n;
     int mat;
@@ -372,7 +373,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sam
         }
     }
     a.p.nee1[pid] = f4(cB, rr.z);
-    a.p.flags[pid] = nf | ((len + 1) << F_LEN_SHIFT);  // extend increments len (:270)
+    a.p.flags[pid] = nf | ((len + 1) << F_LEN_SHIFT) | (sidx << F_SIDX_SHIFT);  // extend increments len (:270)
     SPROF(6);
     SPROF(7);
     return mo;
