@@ -204,10 +204,8 @@ __global__ void k_permute(int n, const uint32_t* __restrict__ idx, const float4*
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t p = idx[i];
-    for (int k = 0; k < 3; k++) {
-        tri_out[kTriF4 * i + k] = tri_in[kTriF4 * p + k];
-        sh_out[3 * i + k] = sh_in[3 * p + k];
-    }
+    for (int k = 0; k < kTriF4; k++) tri_out[kTriF4 * i + k] = tri_in[kTriF4 * p + k];
+    for (int k = 0; k < 3; k++) sh_out[3 * i + k] = sh_in[3 * p + k];
 }
 
 // ---------------------------------------------------------------------------

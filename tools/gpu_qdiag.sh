@@ -1,0 +1,10 @@
+#!/bin/bash
+# quantised-node sanity per config (bounded): base vs libmcpt_q.so
+mkdir -p gpurun_out
+L=$PWD/mc-path-tracer_amd
+for c in 2 4 3 5; do
+  for lib in libmcpt.so libmcpt_q.so; do
+    echo "== $lib"
+    MCPT_LIB=$L/$lib timeout -k 5 60 python -u tools/q_diag.py $c || { echo "FAILED rc=$? ($lib config $c)"; exit 1; }
+  done
+done
