@@ -7,7 +7,7 @@ cleared (g_clear_dfilm, wavefront_kernels.cu:55-76) and every pixel the rank own
 256 spp by repeated wavefront iterations (wavefront_pathtrace, wavefront_kernels.cu:377-442:
 logic+generate+material -> extend -> shadow), startup and tail iterations included.  value =
 (extension + shadow + BRDF visibility rays of all ranks) / (max over ranks of the timed wall time).
-Three paths are in flight per pixel (mcpt_set_path_slots; BENCH_SLOTS per config); films equal
+BENCH_SLOTS[config] paths are in flight per pixel (mcpt_set_path_slots; 24 on config 2); films equal
 the one-path-per-pixel oracle's within the north star's 1e-4 (tests/test_bench_layout.py runs
 this exact layout).  `--steady` reports the steady-state iteration rate beside it.
 
@@ -45,9 +45,11 @@ B_TRI = 36            # per ray/triangle test
 B_HIT = 40            # per closest hit: 3 normals + material id
 B_SHADE = 195 + 172   # logic + material per path-bounce
 B_GEN = 49            # generate per new sample
-# Path slots (paths in flight per pixel) per BASELINE config: the measured best of
-# tools/configs.py; the parity tests run the same layout.
-BENCH_SLOTS = {1: 16, 2: 3, 3: 3, 4: 4, 5: 4}
+# Path slots (paths in flight per pixel) per BASELINE config: the measured best of the
+# whole-frame sweep (tools/gpu_kstats.sh, DESIGN.md section 2: config 2 at 3/8/16/24/32 slots
+# 7287/7856/8064/8095/8081 Mray/s, config 3 at 3/16/32 4924/6624/6822, config 5 (64 spp) at
+# 4/8/16 5257/5458/5486); the parity tests and smoke() run the same layout.
+BENCH_SLOTS = {1: 16, 2: 24, 3: 32, 4: 16, 5: 16}
 STEP = "frame"  # what one step is; stamped into the PMC summaries (tools/pmc.py)
 
 

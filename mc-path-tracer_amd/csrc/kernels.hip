@@ -401,6 +401,15 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     const int bs = (int)blockIdx.x - slot * per_slot;
     const int tile = bs / bpt;
     const int li = (bs - tile * bpt) * kBlock + threadIdx.x;
+    // A block whose paths have all finished their last sample stays so until the film is
+    // cleared: its logic would load their state and change nothing, so it returns here.
+    uint32_t done_idx = 0;
+    if (a.blk_done) {
+        const int2 t = a.tiles[tile];
+        const uint32_t ntx = (uint32_t)((a.W + a.tile_w - 1) / a.tile_w), nty = (uint32_t)((a.H + a.tile_h - 1) / a.tile_h);
+        done_idx = (((uint32_t)slot * nty + (uint32_t)t.y) * ntx + (uint32_t)t.x) * (uint32_t)bpt + (uint32_t)(bs - tile * bpt);
+        if (a.blk_done[done_idx]) return;
+    }
     const int lane = threadIdx.x & 63;
 #ifdef MCPT_SHADE_PROF
     const int wave = threadIdx.x >> 6;
@@ -431,6 +440,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     // this iteration, so the order of the two film updates does not change a bit.
     bool bg = false;
     V3 bg_film = v3(0.f, 0.f, 0.f), bg_dir = bg_film;
+    bool finished = true;  // dead with its last sample done (or no pixel): see blk_done
     if (valid) {
         // Every load the logic may need is issued up front, in one round: the
         // per-path state unconditionally, the len-dependent streams (ray_d for a
@@ -537,6 +547,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             }
         }
         if (!cont && nflags != fl) a.p.flags[pid] = nflags;  // continuing paths: written by material()
+        finished = dead && !(sidx < spp);
     }
     SPROF(1);
     // ---- pushes: generated extension rays and continuing paths (material queue); one
@@ -567,6 +578,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             __float_as_uint(film.z) != __float_as_uint(bg_film.z))
             a.p.Ld[pid] = f4(film, 0.f);
     }
+    if (a.blk_done && __syncthreads_and(finished ? 1 : 0) && threadIdx.x == 0) a.blk_done[done_idx] = 1;
 #ifdef MCPT_SHADE_PROF
     {
         unsigned long long _n = __builtin_readcyclecounter();

@@ -128,6 +128,10 @@ struct ShadeArgs {
     float4* mat_beta;
     uint32_t ext_cap, any_cap;  // per-shard queue capacity
     CounterBlock* cnt;
+    // k_shade block done flags, per (slot, film tile, block of the tile): set once every path of
+    // the block is dead with its last sample finished, so later launches skip the block's loads
+    // (cleared with the film; nullptr: off)
+    uint8_t* blk_done;
 };
 
 // One ray set of a trace launch: rays ro/rd[rid] for queue entries

@@ -57,6 +57,9 @@ struct mcpt_ctx {
     float4* film_Ld = nullptr;     // slots > 1: resolved film (sum of the slot accumulators)
     uint32_t* film_samples = nullptr;
     std::vector<void*> film_bufs;
+    uint8_t* blk_done = nullptr;  // k_shade block done flags (ShadeArgs::blk_done), in film_bufs
+    size_t blk_done_n = 0;
+    bool blk_done_off = getenv("MCPT_NO_BLOCK_DONE") != nullptr;  // A/B switch: every block runs
     DevPaths p{};
     uint32_t *ext_q = nullptr, *any_q = nullptr, *mat_q = nullptr;
     float4* any_ray = nullptr;          // any-hit rays at their queue positions: o [2 queue_alloc], then d
@@ -699,6 +702,7 @@ int mcpt_film_clear(mcpt_ctx* c) {
     ClearArgs a{c->p.flags, c->p.samples, c->p.Ld, (uint32_t)(c->P * c->slots)};
     launch_clear(a, c->stream);
     HIPCHK(c, hipGetLastError());
+    if (c->blk_done) HIPCHK(c, hipMemsetAsync(c->blk_done, 0, c->blk_done_n, c->stream));
     c->film_stale = false;
     HIPCHK(c, hipMemsetAsync(c->cnt, 0, sizeof(CounterBlock), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -715,6 +719,8 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
     HIPCHK(c, hipStreamSynchronize(c->stream));
     free_list(c->film_bufs);
     c->P = 0;
+    c->blk_done = nullptr;
+    c->blk_done_n = 0;
     c->W = w; c->H = h; c->tile_w = tw; c->tile_h = th;
     const size_t npix = (size_t)w * h, P = npix * c->slots;  // P: paths
     if (P >= (1ull << 31)) return set_err(c, MCPT_E_INVALID, "film too large for the path slots");
@@ -729,6 +735,11 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
         return rc;
     c->film_Ld = nullptr;
     c->film_samples = nullptr;
+    {  // k_shade block done flags: slots x film tiles x blocks per tile
+        const size_t ntiles = (size_t)((w + tw - 1) / tw) * ((h + th - 1) / th);
+        c->blk_done_n = c->slots * ntiles * (size_t)shade_blocks_per_tile((int)(tw * th), 1);
+        if ((rc = dalloc(c, c->film_bufs, &c->blk_done, c->blk_done_n))) return rc;
+    }
     if (c->slots > 1 && ((rc = dalloc(c, c->film_bufs, &c->film_Ld, npix)) ||
                          (rc = dalloc(c, c->film_bufs, &c->film_samples, npix))))
         return rc;
@@ -804,6 +815,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     sa.ext_cap = c->ext_cap;
     sa.any_cap = c->any_cap;
     sa.cnt = c->cnt;
+    sa.blk_done = c->blk_done_off ? nullptr : c->blk_done;
     const int bpt = shade_blocks_per_tile((int)(c->tile_w * c->tile_h), (int)c->slots);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 0), c->stream));
     if (sa.ntiles > 0)

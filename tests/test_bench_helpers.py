@@ -90,7 +90,8 @@ def test_frame_and_slots_layout():
     rc2, rc4 = mcpt.CONFIGS[2], mcpt.CONFIGS[4]
     assert bench.frame_size(rc2, 1, "weak") == (1920, 1080) and bench.frame_size(rc2, 8, "weak") == (1920, 8640)
     assert bench.frame_size(rc4, 8, "strong") == (3840, 2160)
-    assert bench.BENCH_SLOTS[2] == 3 and set(bench.BENCH_SLOTS) == set(mcpt.CONFIGS)
+    assert bench.BENCH_SLOTS[2] == 24 and set(bench.BENCH_SLOTS) == set(mcpt.CONFIGS)
+    assert all(1 <= s <= 64 for s in bench.BENCH_SLOTS.values())  # mcpt_set_path_slots' range
     a = bench.parse(["--gpus", "4", "--config", "4", "--scaling", "strong"])
     assert (a.gpus, a.config, a.scaling, a.slots, a.steps) == (4, 4, "strong", None, 5)
 

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round-3 session c: path-slot sweep of the whole-frame bench on configs 2 and 3
+# Round-3 session c: path-slot sweep of the whole-frame bench on configs 2, 3 and 5
 set -o pipefail
 mkdir -p gpurun_out
-bash tools/gpu_kstats.sh "MCPT_BENCH_SLOTS=5" "MCPT_BENCH_SLOTS=8" "MCPT_BENCH_SLOTS=12" "MCPT_BENCH_SLOTS=16" "MCPT_BENCH_SLOTS=8" 2>&1 | grep -E "==|value|k_trace|k_material|k_shade"
-KS_ARGS="--config 3" bash tools/gpu_kstats.sh "MCPT_BENCH_SLOTS=3" "MCPT_BENCH_SLOTS=8" "MCPT_BENCH_SLOTS=12" 2>&1 | grep -E "==|value|k_trace|k_material|k_shade"
+KS_STEPS=1 bash tools/gpu_kstats.sh "MCPT_BENCH_SLOTS=16" "MCPT_BENCH_SLOTS=24" "MCPT_BENCH_SLOTS=32" 2>&1 | grep -E "==|value|k_trace"
+KS_STEPS=1 KS_ARGS="--config 3" bash tools/gpu_kstats.sh "MCPT_BENCH_SLOTS=16" "MCPT_BENCH_SLOTS=24" "MCPT_BENCH_SLOTS=32" 2>&1 | grep -E "==|value|k_trace"
+KS_STEPS=1 KS_ARGS="--config 5 --spp 64" bash tools/gpu_kstats.sh "MCPT_BENCH_SLOTS=4" "MCPT_BENCH_SLOTS=8" "MCPT_BENCH_SLOTS=16" 2>&1 | grep -E "==|value|k_trace"
