@@ -277,6 +277,47 @@ def test_path_slots_ragged_and_resize(mcpt_mod, oracle, scene_c2):
         p.close()
 
 
+def test_finished_blocks_skip_and_reset(mcpt_mod, scene_c2):
+    """k_shade's block done flags (ShadeArgs::blk_done): once a film is complete, further
+    iterations trace nothing and leave it bit for bit; a film clear resets the flags, so the
+    re-render equals the first one; turning a camera change into a stale film does too.  A
+    render with the flags off (MCPT_NO_BLOCK_DONE, new context) gives the same film."""
+    import os
+
+    rc = mcpt_mod.CONFIGS[2]
+    W, H, T = 200, 120, 64
+    cam = mcpt_mod.config_camera(rc, W, H)
+    pt = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 3, 5, tile=T)
+    pt.set_path_slots(2)
+    pt.render()
+    L0, s0 = pt.film()
+    st = pt.iterate(5)
+    assert st.rays == 0
+    L1, s1 = pt.film()
+    assert np.array_equal(L0.view(np.uint32), L1.view(np.uint32)) and np.array_equal(s0, s1)
+    pt.clear()
+    pt.render()
+    L2, s2 = pt.film()
+    assert np.array_equal(L0.view(np.uint32), L2.view(np.uint32)) and np.array_equal(s0, s2)
+    pt.set_camera(mcpt_mod.make_camera((0.3, 0.1, 3.0), aspect=W / H))  # stale film: cleared by the next call
+    pt.render()
+    pt.set_camera(cam)
+    pt.render()
+    L3, s3 = pt.film()
+    assert np.array_equal(L0.view(np.uint32), L3.view(np.uint32)) and np.array_equal(s0, s3)
+    pt.close()
+    os.environ["MCPT_NO_BLOCK_DONE"] = "1"
+    try:
+        off = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 3, 5, tile=T)
+    finally:
+        del os.environ["MCPT_NO_BLOCK_DONE"]
+    off.set_path_slots(2)
+    off.render()
+    L4, s4 = off.film()
+    off.close()
+    assert np.array_equal(L0.view(np.uint32), L4.view(np.uint32)) and np.array_equal(s0, s4)
+
+
 def test_path_slots_partition_invariance(mcpt_mod, scene_c2):
     """With 2 path slots, tile subsets rendered separately (as ranks would) and the reference's
     one-tile-per-call orchestration give the batch film bit for bit (same slot order per pixel)."""
