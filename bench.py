@@ -103,11 +103,13 @@ def source_hash():
 
 
 def pmc_summary(config, slots, kind="pmc"):
-    """The newest committed rocprofv3 summary profiles/<kind>_*.json (kind "pmc": FETCH/WRITE
-    traffic, "pmcdetail": SQ/TCC counters) and whether it was measured on this code (source hash)
-    and this workload (config, path slots, step)."""
-    files = sorted(f for f in glob.glob(os.path.join(REPO, "profiles", f"{kind}_*.json"))
-                   if os.path.basename(f)[len(kind) + 1:][:1] == "r")
+    """The newest committed rocprofv3 summary of this config (kind "pmc": FETCH/WRITE traffic,
+    "pmcdetail": SQ/TCC counters; profiles/<kind>_rNN.json for config 2, <kind>_c<config>_rNN.json
+    for the others) and whether it was measured on this code (source hash) and this workload
+    (config, path slots, step)."""
+    pre = f"{kind}_r" if config == 2 else f"{kind}_c{config}_r"
+    files = sorted(f for f in glob.glob(os.path.join(REPO, "profiles", f"{pre}*.json"))
+                   if os.path.basename(f)[len(pre):][:1].isdigit())
     if not files:
         return None, f"no {kind} summary in profiles/"
     try:

@@ -44,6 +44,12 @@ def test_pmc_summary_stale_detection(tmp_path, monkeypatch):
         "void mcpt_dev::k_trace<2, 8>(mcpt_dev::TraceArgs)": {"ratios": {"valu_busy": 0.7}}}}))
     d, why = bench.pmc_summary(2, 3, "pmcdetail")
     assert why is None and bench.pmc_detail(d, ("mcpt_dev::k_trace<",)) == {"valu_busy": 0.7}
+    # other configs read their own summaries (pmc_c<config>_rNN.json), never config 2's
+    assert bench.pmc_summary(3, 32) == (None, "no pmc summary in profiles/")
+    (prof / "pmc_c3_r12.json").write_text(json.dumps({"stamp": _stamp(h="def", config=3, slots=32), "kernels": kern}))
+    d, why = bench.pmc_summary(3, 32)
+    assert why is None and d["stamp"]["config"] == 3
+    assert bench.pmc_summary(5, 16)[0] is None
 
 
 class _St:
