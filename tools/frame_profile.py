@@ -27,10 +27,12 @@ rays = sum(r[0] for r in rows)
 ms = sum(r[4] + r[5] for r in rows)
 print(f"iterations {len(rows)}  rays {rays / 1e9:.3f} G  device ms {ms:.1f}  rate {rays / ms / 1e3:.0f} Mray/s")
 n = len(rows)
-for lo, hi in ((0, 10), (10, n // 4), (n // 4, n // 2), (n // 2, 3 * n // 4), (3 * n // 4, n - 40), (n - 40, n)):
-    seg = rows[max(lo, 0):max(hi, lo)]
-    if not seg:
+edges = sorted(set([0, min(n, 4)] + [round(n * k / 8) for k in range(1, 9)]))
+for lo, hi in zip(edges[:-1], edges[1:]):
+    if hi <= lo:
         continue
+    seg = rows[lo:hi]
     r = sum(x[0] for x in seg)
-    t = sum(x[4] + x[5] for x in seg)
-    print(f"  iters {lo:4d}-{hi:4d}: rays/iter {r / len(seg) / 1e6:6.2f} M  ms/iter {t / len(seg):.3f}  rate {r / max(t, 1e-9) / 1e3:6.0f} Mray/s  share of time {t / ms:.3f}")
+    m = sum(x[4] + x[5] for x in seg)
+    print(f"  iters {lo:4d}-{hi:4d}: rays/iter {r / len(seg) / 1e6:6.2f} M  ms/iter {m / len(seg):.3f}  "
+          f"rate {r / max(m, 1e-9) / 1e3:6.0f} Mray/s  share of time {m / ms:.3f}")
