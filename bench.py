@@ -430,6 +430,8 @@ def main():
             "step": "one whole frame: film cleared, every pixel the rank owns rendered to spp "
                     "(all wavefront iterations: shade + extend + shadow)",
             "rays_per_step": int(rays_all / K),
+            "rays_per_step_rank0": {"extension": int(st.extend_rays / K), "shadow": int(st.shadow_rays / K),
+                                    "visibility": int(st.vis_rays / K)},
             "iterations_per_step_rank0": round(st.iterations / K, 1),
             "parallelism": f"tiles{world}",
             "path_slots": slots,
