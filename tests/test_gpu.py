@@ -951,6 +951,11 @@ def test_stage_golden_vectors(mcpt_mod, oracle, stage):
     pt.set_camera(sf.stage_camera(mcpt_mod))
     got = pt.stage(stage, inp, film=sf.FILM if stage != "material" else None)
     pt.close()
+    _check_stage(stage, got, ref, a, oracle)
+
+
+def _check_stage(stage, got, ref, a, oracle):
+    """mcpt_stage_run outputs against the oracle's stage restatement, field by field, bit for bit."""
     if stage in ("logic", "generate"):
         for k in ("flags", "samples", "Ld"):
             assert _same(got[k], ref[k]), k
@@ -984,3 +989,29 @@ def test_stage_golden_vectors(mcpt_mod, oracle, stage):
             if res.any():
                 assert np.all(oracle.trace_any(a, ref[o_k][res], ref[d_k][res]) == 1)
         assert (q & 4).sum() > 50 and (q & 8).sum() > 20 and np.isnan(ref["bvis_o"][:, 0]).sum() > 50
+
+
+@pytest.mark.parametrize("stage", ["logic", "generate", "material"])
+def test_stage_fixed_mode_vs_oracle(mcpt_mod, oracle, stage):
+    """The quality-mode integrator (MCPT_FLAG_FIXED, Appendix A) stage by stage: the same fixture
+    states through mcpt_stage_run on a FIXED context, against the oracle's stage restatement in
+    fixed mode computed here (no committed vector: the mode is an alternative, not reference
+    parity).  RR survivors reweighted, 1/N light pick, delta-light MIS weight 1, clamped env cells."""
+    import stage_fixtures as sf
+
+    s = sf.stage_scene(mcpt_mod)
+    a = s.arrays()
+    cam = sf.stage_camera(mcpt_mod)
+    kw = dict(max_depth=sf.DEPTH, rr_depth=sf.RR, fixed=True)
+    if stage == "material":
+        inp = sf.material_state(a, oracle.trace_closest)
+        ref = oracle.stage_material(a, inp, **kw)
+    else:
+        inp = sf.logic_state(len(a["mat"]), stage == "generate")
+        ref = oracle.stage_logic(a, cam, sf.FILM[0], sf.FILM[1], inp, sf.SPP, **kw)
+    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=sf.SPP, max_depth=sf.DEPTH, rr_depth=sf.RR, fixed=True))
+    pt.upload_scene(s)
+    pt.set_camera(cam)
+    got = pt.stage(stage, inp, film=sf.FILM if stage != "material" else None)
+    pt.close()
+    _check_stage(stage, got, ref, a, oracle)
