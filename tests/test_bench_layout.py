@@ -3,8 +3,8 @@
 bench.py renders each config's full frame with BENCH_SLOTS path slots per pixel (several paths
 in flight per pixel, each slot accumulating its own samples).  Here the GPU renders exactly that
 layout -- full resolution, the bench's slot count, the config's depth -- to high sample counts
-(256 spp for configs 2 and 3, as benched; 16 spp for configs 4 and 5, whose full 1024 / 4096 spp
-would take minutes), and a band of rows re-executed by the oracle (one path per pixel, the
+(config 1 whole, 16 spp at its 16 slots; 256 spp for configs 2 and 3, as benched; 16 spp for
+configs 4 and 5, whose full 1024 / 4096 spp would take minutes), and a band of rows re-executed by the oracle (one path per pixel, the
 reference's layout: wavefront_kernels.cu:90-375) must agree: sample counts exactly, radiance within
 the north star's 1e-4 relative (the slots only change the film's summation order).  High sample
 indices, Russian roulette at depth and the slots' interleaved sample chains are all exercised.
@@ -31,12 +31,13 @@ def film_close(g, c):
     return bool(ok.all()), int((~ok).sum())
 
 
-@pytest.mark.parametrize("cid,spp,rows", [(2, 256, (536, 540)), (3, 256, (600, 604)), (4, 16, (1078, 1082)),
-                                          (5, 16, (2046, 2049))], ids=["config2", "config3", "config4", "config5"])
+@pytest.mark.parametrize("cid,spp,rows", [(1, 16, (0, 255)), (2, 256, (536, 540)), (3, 256, (600, 604)),
+                                          (4, 16, (1078, 1082)), (5, 16, (2046, 2049))],
+                         ids=["config1", "config2", "config3", "config4", "config5"])
 def test_bench_layout_band_parity(request, mcpt_mod, oracle, cid, spp, rows):
     rc = mcpt_mod.CONFIGS[cid]
     slots = bench.BENCH_SLOTS[cid]
-    if cid in (2, 3):
+    if cid in (1, 2, 3):
         scene, arrays = request.getfixturevalue(f"scene_c{cid}")
     else:
         scene = mcpt_mod.build_config_scene(cid)
