@@ -68,3 +68,25 @@ def test_bench_layout_band_parity(request, mcpt_mod, oracle, cid, spp, rows):
     assert cnt["extend_rays"] > (r1 - r0) * (rc.width - 1) * spp
     print(f"config {cid}: {rc.width}x{rc.height} {spp} spp {slots} slots: GPU frame {t_gpu:.2f} s "
           f"({st.rays / t_gpu / 1e6:.0f} Mray/s), oracle rows {r0}-{r1} {t_cpu:.1f} s")
+
+
+def test_bench_layout_config2_scattered_rows(mcpt_mod, oracle, scene_c2):
+    """The benched frame itself (config 2, 1080p, 256 spp, the bench's slots) against the oracle
+    on eight single rows spread from the top edge to the last rendered row: sky-only rows, the
+    box walls, the spheres and the floor, each with its own path-length mix."""
+    rc = mcpt_mod.CONFIGS[2]
+    scene, arrays = scene_c2
+    cam = mcpt_mod.config_camera(rc)
+    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=rc.spp, max_depth=rc.max_depth))
+    pt.upload_scene(scene)
+    pt.set_camera(cam)
+    pt.set_path_slots(bench.BENCH_SLOTS[2])
+    pt.resize(rc.width, rc.height)
+    pt.render()
+    Ld, smp = pt.film()
+    pt.close()
+    for r in (0, 135, 270, 405, 675, 810, 945, rc.height - 2):
+        rL, rs, _ = oracle.render(arrays, cam, rc.width, rc.height, rc.spp, rc.max_depth, rows=(r, r + 1))
+        assert np.array_equal(smp[r], rs[r]), r
+        ok, nbad = film_close(Ld[r:r + 1], rL[r:r + 1])
+        assert ok, f"row {r}: {nbad} radiance values differ"
