@@ -1,5 +1,6 @@
 #!/bin/bash
 # HBM-byte attribution of the shading kernels over diagnostic builds (one frame each)
+# variant library: needs tools/build_variant.sh diag_<X> -DMCPT_DIAG_<X> builds from the diagnostic switches described in DESIGN.md section 4 (not kept in the sources)
 set -o pipefail
 export TMPDIR=/tmp
 L=$PWD/mc-path-tracer_amd

@@ -1,3 +1,4 @@
+# variant library: libmcpt_head.so: a build of an earlier commit (tools/build_rev_variant.sh)
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Config-2 steady-state sweep of the traversal launch knobs (env) and a variant library.
+# variant library: libmcpt_mat5.so: tools/build_variant.sh mat5 -DMCPT_MAT_WPE=5
 set -o pipefail
 mkdir -p gpurun_out
 run() {  # label, env assignments...

@@ -1,5 +1,6 @@
 #!/bin/bash
 # quantised-node sanity per config (bounded): base vs libmcpt_q.so
+# variant library: libmcpt_q.so: git apply tools/experiments/quantized_nodes.patch, then tools/build_variant.sh q -DMCPT_QNODES=1
 mkdir -p gpurun_out
 L=$PWD/mc-path-tracer_amd
 for c in 2 4 3 5; do

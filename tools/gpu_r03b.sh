@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round-3 session b: GPU tests, the slot sweep of the whole-frame bench, the multi-rank rehearsal
+# variant library: libmcpt_head.so: a build of an earlier commit (tools/build_rev_variant.sh)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_b.log 2>&1 || { tail -40 gpurun_out/pytest_b.log; exit 1; }

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round-3 session d: quantised nodes (libmcpt_q.so) parity and A/B
+# variant library: libmcpt_q.so: git apply tools/experiments/quantized_nodes.patch, then tools/build_variant.sh q -DMCPT_QNODES=1
 set -o pipefail
 mkdir -p gpurun_out
 L=$PWD/mc-path-tracer_amd
