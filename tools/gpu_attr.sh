@@ -1,6 +1,6 @@
 #!/bin/bash
 # HBM-byte attribution of the shading kernels over diagnostic builds (one frame each)
-# variant library: needs tools/build_variant.sh diag_<X> -DMCPT_DIAG_<X> builds from the diagnostic switches described in DESIGN.md section 4 (not kept in the sources)
+# variant library: git apply tools/experiments/diag_env_attribution.patch, then tools/build_variant.sh diag_<X> -DMCPT_DIAG_<X>
 set -o pipefail
 export TMPDIR=/tmp
 L=$PWD/mc-path-tracer_amd

@@ -1,6 +1,6 @@
 #!/bin/bash
 # time of the shading kernels without the env lookups (diagnostic builds; upper bounds of a deferral)
-# variant library: needs the diag_NO_ENVB / diag_NO_ENVL variant builds (see tools/gpu_attr.sh)
+# variant library: the diag_NO_ENVB / diag_NO_ENVL builds of tools/experiments/diag_env_attribution.patch (see tools/gpu_attr.sh)
 set -o pipefail
 L=$PWD/mc-path-tracer_amd
 KS_STEPS=2 bash tools/gpu_kstats.sh "MCPT_X=0" "MCPT_LIB=$L/libmcpt_diag_NO_ENVB.so" "MCPT_LIB=$L/libmcpt_diag_NO_ENVL.so" "MCPT_X=0" 2>&1 | grep -E "==|value|k_trace|k_material|k_shade"
