@@ -200,6 +200,7 @@ class Acc:
     def __init__(self):
         for k in self.KEYS:
             setattr(self, k, 0)
+        self.occ = 0  # any-hit rays the occluder cache resolved in k_material (not traced by k_trace)
 
     def add(self, st):
         for k in self.KEYS:
@@ -224,7 +225,9 @@ def roofline(st, ms_trace, ms_shade, config, slots):
     n = max(1, st.iterations)
     avg_s = ms_trace / n * 1e-3
     ext_q = st.extend_rays
-    any_q = st.shadow_rays + st.vis_rays
+    any_all = st.shadow_rays + st.vis_rays
+    occ = getattr(st, "occ", 0)
+    any_q = any_all - occ  # any-hit rays k_trace traced (the occluder cache resolved the rest)
     state = (B_EXT_STATE * ext_q + B_ANY_STATE * any_q) / n
     bvh = (2 * B_NODE * (st.ext_nodes + st.any_nodes) + B_TRI * (st.ext_tests + st.any_tests) + B_HIT * st.ext_hits) / n
     achieved = state / avg_s
@@ -246,7 +249,8 @@ def roofline(st, ms_trace, ms_shade, config, slots):
             "per_ray": {"ext_pair_nodes": round(st.ext_nodes / max(1, ext_q), 2),
                         "ext_tri_tests": round(st.ext_tests / max(1, ext_q), 2),
                         "any_pair_nodes": round(st.any_nodes / max(1, any_q), 2),
-                        "any_tri_tests": round(st.any_tests / max(1, any_q), 2)}}
+                        "any_tri_tests": round(st.any_tests / max(1, any_q), 2),
+                        "any_resolved_by_occluder_cache": round(occ / max(1, any_all), 4)}}
     util = {"l2": roof["cache_served"]["l2_frac"]}
     if traffic is not None:
         roof["traffic_GBps"] = round(traffic / avg_s / 1e9, 1)
@@ -340,6 +344,7 @@ def main():
     st = Acc()
     for _ in range(args.steps):
         st.add(frame())
+        st.occ += pt.occ_stats()[0]  # host copy of the frame's counters (no device call)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

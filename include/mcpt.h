@@ -254,6 +254,10 @@ int mcpt_debug_env_tables(mcpt_ctx *ctx, float *marginal_y, float *conds_y, floa
  * 2 breadth-first (default 2 for trees of <= 2 MiB of nodes, else 0; MCPT_SIBLING_LAYOUT=0/1/2
  * at upload forces one; inputs that are not a tree -- a shared child -- always get 0). */
 int mcpt_debug_node_layout(const mcpt_ctx *ctx);
+/* any-hit occluder cache: any-hit rays resolved by it since the film was
+ * last cleared (counted in shadow_rays / vis_rays as traced rays; they skip the traversal), and
+ * whether the uploaded scene has the cache (MCPT_OCC_G=0 at upload turns it off). */
+int mcpt_debug_occ_stats(const mcpt_ctx *ctx, uint64_t *resolved, int32_t *enabled);
 /* k_trace loop profile (diagnostics builds with -DMCPT_TRACE_PROF; returns 0 and zeros otherwise):
  * out12 = {loop trips, refills, node lane-steps, triangle phases, triangle lane-steps, trips with a finish,
  * idle lane-trips, trips with a pop, popping lanes, trips with a non-finite-direction slab, finishing lanes, -}

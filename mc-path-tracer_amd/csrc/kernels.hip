@@ -211,6 +211,71 @@ __device__ inline void hit_record(const DevScene& sc, V3 o, V3 d, int tri, V3& p
 }
 
 // ---------------------------------------------------------------------------
+// Any-hit occluder cache.  An any-hit ray's outcome is one bit (wf_shadow,
+// wavefront_kernels.cu:274-293): occluded iff some triangle passes the traversal's
+// acceptance -- its leaf box and every ancestor box pass the slab test and the cull,
+// and Moller-Trumbore accepts it with 0 <= t < K_HUGE (Triangle.cu:157-205).  Which
+// occluder is found does not matter.  k_trace records the occluder of each occluded
+// ray in a small table keyed by (origin cell, direction bin), and k_material tests a new
+// any-hit ray against its cell's entry first, under that triangle's own leaf box with
+// the traversal's arithmetic (pair_slab's products, keep_box with the any-hit cut).
+// Every ancestor box contains the leaf box and the rounded slab interval is monotone in
+// the box, so an ancestor passes whenever the leaf does: a cache hit is a triangle the
+// traversal accepts as well, and the ray is resolved as occluded exactly as the
+// traversal would resolve it.  A miss costs the test and the ray is traced as before.
+// The table's contents (racy plain stores) only decide how much work is skipped, never
+// a result.  Rays with an infinite inverse component (slab(), NaN slabs) are not tested.
+// ---------------------------------------------------------------------------
+__device__ inline uint32_t occ_index(const DevScene& sc, V3 o, V3 d) {
+    const float gm = (float)(sc.occ_g - 1), bm = (float)(sc.occ_b - 1), hb = 0.5f * (float)sc.occ_b;
+    // fmaxf(NaN, 0) = 0: a NaN coordinate falls in cell / bin 0
+    const uint32_t cx = (uint32_t)__builtin_fminf(__builtin_fmaxf((o.x - sc.root_mn[0]) * sc.occ_inv[0], 0.f), gm);
+    const uint32_t cy = (uint32_t)__builtin_fminf(__builtin_fmaxf((o.y - sc.root_mn[1]) * sc.occ_inv[1], 0.f), gm);
+    const uint32_t cz = (uint32_t)__builtin_fminf(__builtin_fmaxf((o.z - sc.root_mn[2]) * sc.occ_inv[2], 0.f), gm);
+    const float ax = __builtin_fabsf(d.x), ay = __builtin_fabsf(d.y), az = __builtin_fabsf(d.z);
+    uint32_t face;
+    float u, v, m;
+    if (ax >= ay && ax >= az) {
+        face = d.x < 0.f ? 1u : 0u; u = d.y; v = d.z; m = ax;
+    } else if (ay >= az) {
+        face = d.y < 0.f ? 3u : 2u; u = d.x; v = d.z; m = ay;
+    } else {
+        face = d.z < 0.f ? 5u : 4u; u = d.x; v = d.y; m = az;
+    }
+    const float r = hb * __builtin_amdgcn_rcpf(m);  // cube-map coordinates in [-1, 1] -> [0, B)
+    const uint32_t ub = (uint32_t)__builtin_fminf(__builtin_fmaxf(u * r + hb, 0.f), bm);
+    const uint32_t vb = (uint32_t)__builtin_fminf(__builtin_fmaxf(v * r + hb, 0.f), bm);
+    const uint32_t G = (uint32_t)sc.occ_g, B = (uint32_t)sc.occ_b;
+    return ((((cz * G + cy) * G + cx) * 6u + face) * B + ub) * B + vb;
+}
+
+// true: (o, d) is occluded by its cell's cached triangle (see above)
+__device__ inline bool occ_hit(const DevScene& sc, V3 o, V3 d) {
+    const uint32_t t = sc.occ[occ_index(sc, o, d)];
+    if (t >= sc.ntri) return false;  // empty (or a stale entry of an earlier scene: never read)
+    const float4 bmn = sc.leaf_box[2 * t], bmx = sc.leaf_box[2 * t + 1];
+    const float4* tp = sc.tri + kTriF4 * t;
+    const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
+    const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);  // k_trace's reciprocal
+    if (!(__builtin_fabsf(inv.x) < K_INF_F && __builtin_fabsf(inv.y) < K_INF_F && __builtin_fabsf(inv.z) < K_INF_F))
+        return false;
+    // pair_slab's arithmetic for one box (its first lane)
+    const float ax = (bmn.x - o.x) * inv.x, bx = (bmx.x - o.x) * inv.x;
+    const float ay = (bmn.y - o.y) * inv.y, by = (bmx.y - o.y) * inv.y;
+    const float az = (bmn.z - o.z) * inv.z, bz = (bmx.z - o.z) * inv.z;
+    const float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax, bx), __builtin_fminf(ay, by)),
+                                     __builtin_fminf(az, bz));
+    const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by)),
+                                     __builtin_fmaxf(az, bz));
+    const float best = K_HUGE;
+    const float cut = best + best * kCullRel;  // an any-hit ray's cut in k_trace
+    if (!(t0 <= t1) || !keep_box(t0, t1, cut)) return false;
+    float th;
+    return tri_test_t(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), th) && !(th < 0.f) &&
+           th < K_HUGE;
+}
+
+// ---------------------------------------------------------------------------
 // k_shade: the first half of one wavefront iteration's shading, for one block of
 // 256 pixels of a path slot.
 //   phase 1, one thread per pixel: wf_logic (MIS combine, throughput update,
@@ -613,7 +678,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
     __syncthreads();
     unsigned long long _t_mat = __builtin_readcyclecounter();
 #endif
-    uint32_t n_ext = 0, n_any = 0, n_vis = 0;
+    uint32_t n_ext = 0, n_any = 0, n_vis = 0, n_occ = 0;
     // Any-hit rays are staged here (light ray o/d, BRDF visibility ray o/d) and stored after
     // the block push at their queue positions: the block's rays of one kind land contiguously,
     // so k_trace reads them densely and without the queue-entry hop (the pid-indexed layout
@@ -623,11 +688,28 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
         const uint32_t i = base + threadIdx.x;
         MatOut mo{false, false, false, false, false, 0u};
         uint32_t mpid = 0;
+        bool occ_l = false, occ_b = false;  // resolved by the occluder cache
         if (i < n) {
             const uint4 q = a.mat_rec[shard * a.ext_cap + i];  // {pid, len, sample index, hit_tri}
             const float4 b4 = a.mat_beta[shard * a.ext_cap + i];
             mpid = q.x;
             mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w, &s_any[0][0]);
+            // the occluder cache (see occ_hit), after the path's shading state is dead: a ray it
+            // resolves gets its wf_shadow result here and is not queued
+            if (a.scene.occ) {
+                if (mo.want_l && occ_hit(a.scene, xyz(s_any[0][threadIdx.x]), xyz(s_any[1][threadIdx.x]))) {
+                    a.p.vis[2 * mpid] = 0;
+                    mo.want_l = false;
+                    mo.trivial_any++;
+                    occ_l = true;
+                }
+                if (mo.want_b && occ_hit(a.scene, xyz(s_any[2][threadIdx.x]), xyz(s_any[3][threadIdx.x]))) {
+                    a.p.vis[2 * mpid + 1] = 0;
+                    mo.want_b = false;
+                    mo.trivial_any++;
+                    occ_b = true;
+                }
+            }
         }
         bool want[3] = {mo.want_ext, mo.want_l, mo.want_b};
         uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
@@ -646,6 +728,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
             a.p.sray_o[k] = s_any[2][threadIdx.x];
             a.p.sray_d[k] = s_any[3][threadIdx.x];
         }
+        n_occ += (uint32_t)(__popcll(__ballot(occ_l)) + __popcll(__ballot(occ_b)));  // wave-uniform
         n_ext += (mo.want_ext || mo.trivial_ext) ? 1u : 0u;  // queued + resolved-in-place rays
         n_any += (mo.want_l ? 1u : 0u) + (mo.want_b ? 1u : 0u) + mo.trivial_any;
         n_vis += mo.vis_ray ? 1u : 0u;
@@ -659,6 +742,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
         if (n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
         if (n_any) atomicAdd(sc_ctr + C_ANY_RAYS, n_any);
         if (n_vis) atomicAdd(sc_ctr + C_VIS, n_vis);
+        if (n_occ) atomicAdd(sc_ctr + C_OCC, n_occ);
     }
 #ifdef MCPT_SHADE_PROF
     {
@@ -929,8 +1013,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         uint32_t* rs = kind ? a.set[1].ray_steps : a.set[0].ray_steps;
         if (rs) rs[qi] = rn + rt;
 #endif
-        if (kind) a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
-        else a.hit_tri[rid] = tri;                  // hit record rebuilt by the consumer (hit_record())
+        if (kind) {
+            a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
+            if (tri >= 0 && sc.occ) sc.occ[occ_index(sc, o, d)] = (uint32_t)tri;  // the cell's occluder (occ_hit)
+        } else {
+            a.hit_tri[rid] = tri;  // hit record rebuilt by the consumer (hit_record())
+        }
         act = false;
     };
     for (;;) {
@@ -1366,17 +1454,20 @@ __global__ void k_accumulate(CounterBlock* c, uint32_t nparts) {  // fold per-it
         for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
     if (__ballot(short_part) != 0 && t == 0) c->trace_short += 1;
     if (t < kMaxParts) c->grab[t][0] = 0;  // k_trace chunk hand-out counters
-    uint32_t er = c->shard[t][C_EXT_RAYS], ar = c->shard[t][C_ANY_RAYS];
+    uint32_t er = c->shard[t][C_EXT_RAYS], ar = c->shard[t][C_ANY_RAYS], oc = c->shard[t][C_OCC];
     c->shard[t][C_EXT_RAYS] = 0;
     c->shard[t][C_ANY_RAYS] = 0;
     c->shard[t][C_MAT] = 0;
+    c->shard[t][C_OCC] = 0;
     for (int off = 32; off > 0; off >>= 1) {
         er += __shfl_xor(er, off);
         ar += __shfl_xor(ar, off);
+        oc += __shfl_xor(oc, off);
     }
     if (t == 0) {
         c->tot_ext += er;
         c->tot_any += ar;
+        c->tot_occ += oc;
         c->tot_vis += v[C_VIS];
         c->last_ext = v[C_EXT];
         c->last_live = er;
@@ -1578,6 +1669,35 @@ int trace_profile(unsigned long long* out, int reset) {  // diagnostics build on
     (void)reset;
     return 0;
 #endif
+}
+__global__ void k_leaf_boxes(DevScene sc, uint32_t nnodes, float4* out) {  // see launch_leaf_boxes
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    auto put = [&](int ref, float mnx, float mny, float mnz, float mxx, float mxy, float mxz) {
+        if (ref >= 0 || ref == kEnd) return;
+        const uint32_t off = (uint32_t)ref & 0xffffffu, cnt = (((uint32_t)ref >> 24) & 7u) + 1u;
+        for (uint32_t k = off; k < off + cnt && k < sc.ntri; k++) {
+            out[2 * k] = make_float4(mnx, mny, mnz, 0.f);
+            out[2 * k + 1] = make_float4(mxx, mxy, mxz, 0.f);
+        }
+    };
+    if (i == 0 && sc.root_ref < 0)  // the whole tree is one leaf: its box is the root box
+        put(sc.root_ref, sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1], sc.root_mx[2]);
+    if (i >= nnodes) return;
+    if (sc.width == 4) {  // mn.x[4], mx.x[4], mn.y[4], mx.y[4], mn.z[4], mx.z[4], refs[4]
+        const float4* nd = sc.nodes + 8 * (size_t)i;
+        const float4 mnx = nd[0], mxx = nd[1], mny = nd[2], mxy = nd[3], mnz = nd[4], mxz = nd[5], rf = nd[6];
+        const float* a0 = &mnx.x; const float* a1 = &mxx.x; const float* b0 = &mny.x;
+        const float* b1 = &mxy.x; const float* c0 = &mnz.x; const float* c1 = &mxz.x; const float* r = &rf.x;
+        for (int k = 0; k < 4; k++) put(__float_as_int(r[k]), a0[k], b0[k], c0[k], a1[k], b1[k], c1[k]);
+    } else {  // per axis (mn0, mn1, mx0, mx1), then (ref0, ref1, -, -)
+        const float4* nd = sc.nodes + 4 * (size_t)i;
+        const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        put(__float_as_int(q3.x), q0.x, q1.x, q2.x, q0.z, q1.z, q2.z);
+        put(__float_as_int(q3.y), q0.y, q1.y, q2.y, q0.w, q1.w, q2.w);
+    }
+}
+void launch_leaf_boxes(const DevScene& sc, uint32_t nnodes, float4* leaf_box, hipStream_t s) {
+    hipLaunchKernelGGL(k_leaf_boxes, dim3(nnodes / 256 + 1), dim3(256), 0, s, sc, nnodes, leaf_box);
 }
 void launch_clear(const ClearArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_clear, dim3((a.n + 255) / 256), dim3(256), 0, s, a);

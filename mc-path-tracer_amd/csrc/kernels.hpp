@@ -82,7 +82,20 @@ struct DevScene {
     const float* mats;      // 8 floats per material
     const float* dirs;      // 7 floats per directional light
     mcpt::EnvView env;
+    // Any-hit occluder cache: occ[i] is the triangle record that last
+    // occluded an any-hit ray of cell i (origin cell of the root box x direction bin), or
+    // kOccEmpty; leaf_box[2t] / [2t + 1] are mn / mx of the BVH leaf box that holds record t.
+    // k_material tests an any-hit ray against its cell's triangle under that leaf box first:
+    // a hit there is one the traversal would find too, so the ray is resolved as occluded.
+    // occ == nullptr: off.
+    uint32_t* occ;
+    const float4* leaf_box;
+    uint32_t ntri;
+    int occ_g, occ_b;       // origin cells per axis, direction bins per face coordinate
+    float occ_inv[3];       // occ_g / root box extent, per axis
 };
+constexpr uint32_t kOccEmpty = 0xffffffffu;
+__host__ __device__ constexpr size_t occ_entries(int g, int b) { return (size_t)g * g * g * 6 * b * b; }
 
 struct DevPaths {
     float4 *ray_o, *ray_d, *sray_o, *sray_d, *beta, *nee0, *nee1, *Ld;
@@ -97,7 +110,8 @@ struct DevPaths {
 // statistics adds per iteration would otherwise cost.
 constexpr int kShards = 64;
 constexpr int kMaxParts = kShards;  // k_trace work partitions (at most one per queue shard)
-enum : int { C_EXT = 0, C_ANY = 1, C_VIS = 2, C_STATS = 3, C_EXT_RAYS = 9, C_ANY_RAYS = 10, C_MAT = 11, C_WORDS = 32 };  // C_STATS..+5
+enum : int { C_EXT = 0, C_ANY = 1, C_VIS = 2, C_STATS = 3, C_EXT_RAYS = 9, C_ANY_RAYS = 10, C_MAT = 11, C_OCC = 12,
+              C_WORDS = 32 };  // C_STATS..+5; C_OCC: any-hit rays resolved by the occluder cache
 struct CounterBlock {
     uint32_t shard[kShards][C_WORDS];  // [0] ext pushes [1] any-hit pushes [2] vis rays [3..8] traversal stats [9,10] rays [11] material pushes
     uint32_t last_ext, last_live;
@@ -107,7 +121,7 @@ struct CounterBlock {
     uint32_t pad[28];
     uint32_t last_ext_shard[kShards];  // per-shard extension pushes of the last iteration
     uint32_t grab[kMaxParts][C_WORDS];  // k_trace ray hand-out, one counter line per partition
-    unsigned long long tot_ext, tot_any, tot_vis, pad2;
+    unsigned long long tot_ext, tot_any, tot_vis, tot_occ;
     unsigned long long tot_stats[6];
 };
 
@@ -185,6 +199,9 @@ void launch_shade_stage(bool material_stage, const ShadeArgs& a, int nblocks, co
                         hipStream_t s);
 void launch_trace(const TraceArgs& a, const LaunchGeom& g, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
+// leaf_box[2t], [2t + 1] = the box of the leaf that holds triangle record t (nodes: nnodes nodes
+// of the given width; a root that is itself a leaf gets the root box)
+void launch_leaf_boxes(const DevScene& sc, uint32_t nnodes, float4* leaf_box, hipStream_t s);
 void launch_env_table(const mcpt::EnvView& e, bool fixed_mode, float4* out, float2* row, float2* col, hipStream_t s);
 // HRDI tables on the device (env_build.hip), bit-identical to the host build: scratch holds
 // env_build_scratch_floats(W, H) floats; W * H < 2^31.

@@ -474,6 +474,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     // 1.148 ms with quads; config 4 (252K, 16 MB) 7.69 -> 7.79 ms and config 2 (4.8K) 0.783 ->
     // 0.848 ms, so those keep pairs.  MCPT_BVH_WIDTH=2/4 forces a width.
     const size_t tree_pairs = gpu_bvh ? (size_t)lb.nnodes : pn.size() / 4;
+    uint32_t nnodes = (uint32_t)tree_pairs;  // nodes of the uploaded width (the leaf-box pass)
     int width = tree_pairs * 64 > ((size_t)32 << 20) ? 4 : 2;
     if (const char* we = getenv("MCPT_BVH_WIDTH"))
         if ((we[0] == '2' || we[0] == '4') && we[1] == 0) width = we[0] - '0';
@@ -499,6 +500,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             float4* dq;
             if ((rc = dupload(c, c->scene_bufs, &dq, quads.data(), quads.size()))) return rc;
             s.nodes = dq;
+            nnodes = (uint32_t)(quads.size() / 8);
         }
     }
     s.nlights = 1 + d->ndir;
@@ -607,6 +609,38 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     }
     s.depth = width == 4 ? quad_push : c->pair_depth;
     s.width = width;
+    // Any-hit occluder cache (kernels.hip occ_hit): every triangle record's leaf box and the
+    // (origin cell x direction bin) table, empty at upload.  MCPT_OCC_G=0 turns it off;
+    // MCPT_OCC_G / MCPT_OCC_B set the cells per axis / bins per face coordinate.
+    s.ntri = (uint32_t)d->ntri;
+    s.occ = nullptr;
+    s.leaf_box = nullptr;
+    {
+        int G = 8, B = 8;
+        if (const char* e = getenv("MCPT_OCC_G")) G = atoi(e);
+        if (const char* e = getenv("MCPT_OCC_B")) B = atoi(e);
+        if (G > 0 && G <= 64 && B > 0 && B <= 64 && d->ntri > 0) {
+            float4* lbx;
+            uint32_t* occ;
+            const size_t ne = occ_entries(G, B);
+            if ((rc = dalloc(c, c->scene_bufs, &lbx, 2 * (size_t)d->ntri)) || (rc = dalloc(c, c->scene_bufs, &occ, ne)))
+                return rc;
+            // NaN boxes (all-ones bytes) for a record no leaf holds: occ_hit's slab then fails
+            HIPCHK(c, hipMemsetAsync(lbx, 0xff, 2 * (size_t)d->ntri * sizeof(float4), c->stream));
+            HIPCHK(c, hipMemsetAsync(occ, 0xff, ne * sizeof(uint32_t), c->stream));
+            launch_leaf_boxes(s, nnodes, lbx, c->stream);
+            HIPCHK(c, hipGetLastError());
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            s.leaf_box = lbx;
+            s.occ = occ;
+            s.occ_g = G;
+            s.occ_b = B;
+            for (int k = 0; k < 3; k++) {
+                const float ext = s.root_mx[k] - s.root_mn[k];
+                s.occ_inv[k] = ext > 0.f && ext < 3.4e38f ? (float)G / ext : 0.f;
+            }
+        }
+    }
     c->scene = s;
     c->ntri = d->ntri;
     if (c->has_scene_before) c->film_stale = true;  // a re-upload notifies the film
@@ -639,6 +673,12 @@ int mcpt_debug_env_tables(mcpt_ctx* c, float* marginal_y, float* conds_y, float*
     return MCPT_OK;
 }
 int mcpt_debug_node_layout(const mcpt_ctx* c) { return c ? c->node_layout : MCPT_E_INVALID; }
+int mcpt_debug_occ_stats(const mcpt_ctx* c, uint64_t* resolved, int32_t* enabled) {
+    if (!c) return MCPT_E_INVALID;
+    if (resolved) *resolved = c->totals_ok ? c->totals.tot_occ : 0;
+    if (enabled) *enabled = c->scene.occ != nullptr;
+    return MCPT_OK;
+}
 
 int mcpt_camera_set(mcpt_ctx* c, const mcpt_camera* cam) {
     if (!c || !cam) return set_err(c, MCPT_E_INVALID, "null argument");
@@ -1077,6 +1117,7 @@ static int stage_run_paths(mcpt_ctx* c, int stage, const mcpt_path_view* in, mcp
     if (e != hipSuccess) return set_err(c, MCPT_E_HIP, std::string("stage upload: ") + hipGetErrorString(e));
     ShadeArgs sa{};
     sa.scene = c->scene;
+    sa.scene.occ = nullptr;  // stage runs: outputs of the stage alone (no occluder cache)
     sa.cam = c->cam;
     sa.p = p;
     sa.tiles = tl;
@@ -1203,6 +1244,7 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
         return rc;
     TraceArgs ta{};
     ta.scene = c->scene;
+    ta.scene.occ = nullptr;  // stage runs: outputs of the stage alone (no occluder cache)
     ta.nshards = 1;
     TraceSet& ts = ta.set[stage == MCPT_STAGE_SHADOW ? 1 : 0];
     ts.ro = dro;

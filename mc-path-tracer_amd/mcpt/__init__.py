@@ -138,6 +138,7 @@ ABI = {
     "mcpt_debug_last_env_build_ms": (C.c_float, [C.c_void_p]),
     "mcpt_debug_env_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _i]),
     "mcpt_debug_node_layout": (C.c_int, [C.c_void_p]),
+    "mcpt_debug_occ_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]),
     "mcpt_scene_upload_gpu_bvh": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mcpt_set_gpu_bvh_builder": (C.c_int, [C.c_void_p, C.c_int32]),
     "mcpt_film_size": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
@@ -408,6 +409,12 @@ class PathTracer:
             self._ck(lib().mcpt_scene_upload_gpu_bvh(self.h, C.byref(d)))
         else:
             self._ck(lib().mcpt_scene_upload(self.h, C.byref(d)))
+
+    def occ_stats(self):
+        """(any-hit rays the occluder cache resolved since the last film clear, cache enabled)."""
+        r, e = C.c_uint64(0), C.c_int32(0)
+        self._ck(lib().mcpt_debug_occ_stats(self.h, C.byref(r), C.byref(e)))
+        return int(r.value), bool(e.value)
 
     @property
     def last_build_ms(self) -> float:

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round-3 session: any-hit occluder cache.  GPU parity suite, then interleaved whole-frame A/B
+# (cache off / default 8 cells x 4 bins / variants) on config 2 and config 3.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_occ.log 2>&1 || { grep -E "FAILED|Error|assert" gpurun_out/pytest_occ.log | head -20; tail -5 gpurun_out/pytest_occ.log; exit 1; }
+grep -E "passed|failed" gpurun_out/pytest_occ.log | tail -1
+KS_STEPS=2 bash tools/gpu_kstats.sh "MCPT_OCC_G=0" "MCPT_X=0" "MCPT_OCC_G=16" "MCPT_OCC_B=8" "MCPT_OCC_G=0" "MCPT_X=0" 2>&1 | grep -E "==|value|k_trace|k_material|k_shade"
+KS_STEPS=1 KS_ARGS="--config 3" bash tools/gpu_kstats.sh "MCPT_OCC_G=0" "MCPT_X=0" 2>&1 | grep -E "==|value|k_trace|k_material|k_shade"
