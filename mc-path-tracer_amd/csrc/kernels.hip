@@ -249,16 +249,8 @@ __device__ inline uint32_t occ_index(const DevScene& sc, V3 o, V3 d) {
     return ((((cz * G + cy) * G + cx) * 6u + face) * B + ub) * B + vb;
 }
 
-// true: (o, d) is occluded by its cell's cached triangle (see above)
-__device__ inline bool occ_hit(const DevScene& sc, V3 o, V3 d) {
-    const uint32_t t = sc.occ[occ_index(sc, o, d)];
-    if (t >= sc.ntri) return false;  // empty (or a stale entry of an earlier scene: never read)
-    const float4 bmn = sc.leaf_box[2 * t], bmx = sc.leaf_box[2 * t + 1];
-    const float4* tp = sc.tri + kTriF4 * t;
-    const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-    const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);  // k_trace's reciprocal
-    if (!(__builtin_fabsf(inv.x) < K_INF_F && __builtin_fabsf(inv.y) < K_INF_F && __builtin_fabsf(inv.z) < K_INF_F))
-        return false;
+// true: (o, d) (reciprocal inv, all finite) is occluded by triangle record w0..w2 under its leaf box
+__device__ inline bool occ_test(V3 o, V3 d, V3 inv, float4 bmn, float4 bmx, float4 w0, float4 w1, float4 w2) {
     // pair_slab's arithmetic for one box (its first lane)
     const float ax = (bmn.x - o.x) * inv.x, bx = (bmx.x - o.x) * inv.x;
     const float ay = (bmn.y - o.y) * inv.y, by = (bmx.y - o.y) * inv.y;
@@ -273,6 +265,26 @@ __device__ inline bool occ_hit(const DevScene& sc, V3 o, V3 d) {
     float th;
     return tri_test_t(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), th) && !(th < 0.f) &&
            th < K_HUGE;
+}
+// The cell's entries of (o, d): kOccWays triangle records (k_trace writes way tri mod kOccWays)
+__device__ inline uint2 occ_entry(const DevScene& sc, V3 o, V3 d) {
+    return reinterpret_cast<const uint2*>(sc.occ)[occ_index(sc, o, d)];
+}
+// true: (o, d) is occluded by one of its cell's cached triangles e.  Both candidates' leaf boxes
+// and records are fetched in one round trip (an empty way reads record 0 and is not tested).
+__device__ inline bool occ_hit(const DevScene& sc, V3 o, V3 d, uint2 e) {
+    const bool v0 = e.x < sc.ntri, v1 = e.y < sc.ntri;
+    if (!v0 && !v1) return false;
+    const uint32_t t0 = v0 ? e.x : 0u, t1 = v1 ? e.y : 0u;
+    const float4 b0n = sc.leaf_box[2 * t0], b0x = sc.leaf_box[2 * t0 + 1];
+    const float4 b1n = sc.leaf_box[2 * t1], b1x = sc.leaf_box[2 * t1 + 1];
+    const float4* p0 = sc.tri + kTriF4 * t0;
+    const float4* p1 = sc.tri + kTriF4 * t1;
+    const float4 r00 = p0[0], r01 = p0[1], r02 = p0[2], r10 = p1[0], r11 = p1[1], r12 = p1[2];
+    const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);  // k_trace's reciprocal
+    if (!(__builtin_fabsf(inv.x) < K_INF_F && __builtin_fabsf(inv.y) < K_INF_F && __builtin_fabsf(inv.z) < K_INF_F))
+        return false;
+    return (v0 && occ_test(o, d, inv, b0n, b0x, r00, r01, r02)) || (v1 && occ_test(o, d, inv, b1n, b1x, r10, r11, r12));
 }
 
 // ---------------------------------------------------------------------------
@@ -678,7 +690,8 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
     __syncthreads();
     unsigned long long _t_mat = __builtin_readcyclecounter();
 #endif
-    uint32_t n_ext = 0, n_any = 0, n_vis = 0, n_occ = 0;
+    uint32_t n_ext = 0, n_any = 0, n_vis = 0, n_occ = 0, occ_try = 0;
+    const bool occ_on = a.scene.occ && a.scene.occ_gate[0] == 0;  // see DevScene::occ_gate
     // Any-hit rays are staged here (light ray o/d, BRDF visibility ray o/d) and stored after
     // the block push at their queue positions: the block's rays of one kind land contiguously,
     // so k_trace reads them densely and without the queue-entry hop (the pid-indexed layout
@@ -688,7 +701,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
         const uint32_t i = base + threadIdx.x;
         MatOut mo{false, false, false, false, false, 0u};
         uint32_t mpid = 0;
-        bool occ_l = false, occ_b = false;  // resolved by the occluder cache
+        bool occ_l = false, occ_b = false, try_l = false, try_b = false;  // resolved by / tested against the occluder cache
         if (i < n) {
             const uint4 q = a.mat_rec[shard * a.ext_cap + i];  // {pid, len, sample index, hit_tri}
             const float4 b4 = a.mat_beta[shard * a.ext_cap + i];
@@ -696,14 +709,22 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
             mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w, &s_any[0][0]);
             // the occluder cache (see occ_hit), after the path's shading state is dead: a ray it
             // resolves gets its wf_shadow result here and is not queued
-            if (a.scene.occ) {
-                if (mo.want_l && occ_hit(a.scene, xyz(s_any[0][threadIdx.x]), xyz(s_any[1][threadIdx.x]))) {
+            if (occ_on) {
+                try_l = mo.want_l;
+                try_b = mo.want_b;
+                // both rays' cell entries in one round trip, then each ray's candidates
+                const V3 ol = xyz(s_any[0][threadIdx.x]), dl = xyz(s_any[1][threadIdx.x]);
+                const V3 ob = xyz(s_any[2][threadIdx.x]), db = xyz(s_any[3][threadIdx.x]);
+                const uint2 none = make_uint2(kOccEmpty, kOccEmpty);
+                const uint2 el = mo.want_l ? occ_entry(a.scene, ol, dl) : none;
+                const uint2 eb = mo.want_b ? occ_entry(a.scene, ob, db) : none;
+                if (mo.want_l && occ_hit(a.scene, ol, dl, el)) {
                     a.p.vis[2 * mpid] = 0;
                     mo.want_l = false;
                     mo.trivial_any++;
                     occ_l = true;
                 }
-                if (mo.want_b && occ_hit(a.scene, xyz(s_any[2][threadIdx.x]), xyz(s_any[3][threadIdx.x]))) {
+                if (mo.want_b && occ_hit(a.scene, ob, db, eb)) {
                     a.p.vis[2 * mpid + 1] = 0;
                     mo.want_b = false;
                     mo.trivial_any++;
@@ -728,21 +749,21 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
             a.p.sray_o[k] = s_any[2][threadIdx.x];
             a.p.sray_d[k] = s_any[3][threadIdx.x];
         }
-        n_occ += (uint32_t)(__popcll(__ballot(occ_l)) + __popcll(__ballot(occ_b)));  // wave-uniform
-        n_ext += (mo.want_ext || mo.trivial_ext) ? 1u : 0u;  // queued + resolved-in-place rays
-        n_any += (mo.want_l ? 1u : 0u) + (mo.want_b ? 1u : 0u) + mo.trivial_any;
-        n_vis += mo.vis_ray ? 1u : 0u;
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        n_ext += __shfl_xor(n_ext, off);
-        n_any += __shfl_xor(n_any, off);
-        n_vis += __shfl_xor(n_vis, off);
+        // per-wave ray counts from lane masks (wave-uniform scalars: no registers held across the
+        // next trip's material())
+        n_occ += (uint32_t)(__popcll(__ballot(occ_l)) + __popcll(__ballot(occ_b)));
+        occ_try += (uint32_t)(__popcll(__ballot(try_l)) + __popcll(__ballot(try_b)));
+        n_ext += (uint32_t)__popcll(__ballot(mo.want_ext || mo.trivial_ext));  // queued + resolved-in-place rays
+        n_any += (uint32_t)(__popcll(__ballot(mo.want_l)) + __popcll(__ballot(mo.want_b)) +
+                            __popcll(__ballot(mo.trivial_any >= 1u)) + __popcll(__ballot(mo.trivial_any >= 2u)));
+        n_vis += (uint32_t)__popcll(__ballot(mo.vis_ray));
     }
     if (lane == 0) {
         if (n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
         if (n_any) atomicAdd(sc_ctr + C_ANY_RAYS, n_any);
         if (n_vis) atomicAdd(sc_ctr + C_VIS, n_vis);
         if (n_occ) atomicAdd(sc_ctr + C_OCC, n_occ);
+        if (occ_try) atomicAdd(sc_ctr + C_OCC_TRY, occ_try);
     }
 #ifdef MCPT_SHADE_PROF
     {
@@ -951,6 +972,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     };
     enter(home);
     const DevScene& sc = a.scene;
+    // occluder-cache records (see occ_hit): off while k_material's lookups are gated off, except in
+    // the iteration before the next lookups (DevScene::occ_gate)
+    const bool occ_rec = sc.occ && sc.occ_gate[0] <= 1u;
 
     // per-lane work counters (wave-reduced at exit): tot_* count every node step, triangle
     // test and hit; the any-hit set's share is attributed per ray (tot_n1 -= tot_n when an
@@ -1015,7 +1039,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #endif
         if (kind) {
             a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
-            if (tri >= 0 && sc.occ) sc.occ[occ_index(sc, o, d)] = (uint32_t)tri;  // the cell's occluder (occ_hit)
+            if (tri >= 0 && occ_rec)  // the cell's occluder (occ_hit)
+                sc.occ[(size_t)occ_index(sc, o, d) * kOccWays + (uint32_t)tri % kOccWays] = (uint32_t)tri;
         } else {
             a.hit_tri[rid] = tri;  // hit record rebuilt by the consumer (hit_record())
         }
@@ -1429,7 +1454,7 @@ __global__ void k_tonemap(TonemapArgs a) {  // draw_to_surface (wavefront_kernel
     a.out[i] = o;
 }
 
-__global__ void k_accumulate(CounterBlock* c, uint32_t nparts) {  // fold per-iteration shard counts into 64-bit totals
+__global__ void k_accumulate(CounterBlock* c, uint32_t nparts, uint32_t* occ_gate) {  // fold per-iteration shard counts into 64-bit totals
     if (c->idle) return;  // nothing ran since the iteration that set it; every counter is zero
     const int t = threadIdx.x;  // one lane per shard
     uint32_t v[C_STATS + 6];
@@ -1454,20 +1479,36 @@ __global__ void k_accumulate(CounterBlock* c, uint32_t nparts) {  // fold per-it
         for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
     if (__ballot(short_part) != 0 && t == 0) c->trace_short += 1;
     if (t < kMaxParts) c->grab[t][0] = 0;  // k_trace chunk hand-out counters
-    uint32_t er = c->shard[t][C_EXT_RAYS], ar = c->shard[t][C_ANY_RAYS], oc = c->shard[t][C_OCC];
+    uint32_t er = c->shard[t][C_EXT_RAYS], ar = c->shard[t][C_ANY_RAYS], oc = c->shard[t][C_OCC],
+             ot = c->shard[t][C_OCC_TRY];
     c->shard[t][C_EXT_RAYS] = 0;
     c->shard[t][C_ANY_RAYS] = 0;
     c->shard[t][C_MAT] = 0;
     c->shard[t][C_OCC] = 0;
+    c->shard[t][C_OCC_TRY] = 0;
     for (int off = 32; off > 0; off >>= 1) {
         er += __shfl_xor(er, off);
         ar += __shfl_xor(ar, off);
         oc += __shfl_xor(oc, off);
+        ot += __shfl_xor(ot, off);
     }
     if (t == 0) {
         c->tot_ext += er;
         c->tot_any += ar;
         c->tot_occ += oc;
+        // occluder-cache gate for the next iterations' k_material (a speed choice only)
+        if (occ_gate) {
+            if (occ_gate[0]) {
+                occ_gate[0]--;
+            } else if (ot >= 4096u) {
+                if ((unsigned long long)oc * kOccMinRate < ot) {
+                    occ_gate[1] = occ_gate[1] ? min(2u * occ_gate[1] + 1u, 255u) : 3u;
+                    occ_gate[0] = occ_gate[1];
+                } else {
+                    occ_gate[1] = 0;
+                }
+            }
+        }
         c->tot_vis += v[C_VIS];
         c->last_ext = v[C_EXT];
         c->last_live = er;
@@ -1711,8 +1752,9 @@ void launch_resolve(const ResolveArgs& a, hipStream_t s) {
 void launch_tonemap(const TonemapArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_tonemap, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
-void launch_accumulate(CounterBlock* c, uint32_t nparts, hipStream_t s) {
-    hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(kShards), 0, s, c, std::min<uint32_t>(kMaxParts, std::max<uint32_t>(1, nparts)));
+void launch_accumulate(CounterBlock* c, uint32_t nparts, uint32_t* occ_gate, hipStream_t s) {
+    hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(kShards), 0, s, c, std::min<uint32_t>(kMaxParts, std::max<uint32_t>(1, nparts)),
+                       occ_gate);
 }
 void launch_unpack(const UnpackArgs& a, hipStream_t s) {
     const uint32_t n = (uint32_t)(a.ntiles * a.tile_w * a.tile_h);

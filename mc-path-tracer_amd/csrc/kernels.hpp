@@ -82,20 +82,30 @@ struct DevScene {
     const float* mats;      // 8 floats per material
     const float* dirs;      // 7 floats per directional light
     mcpt::EnvView env;
-    // Any-hit occluder cache: occ[i] is the triangle record that last
-    // occluded an any-hit ray of cell i (origin cell of the root box x direction bin), or
+    // Any-hit occluder cache: occ[kOccWays i + w] is a triangle record
+    // that occluded an any-hit ray of cell i (origin cell of the root box x direction bin), or
     // kOccEmpty; leaf_box[2t] / [2t + 1] are mn / mx of the BVH leaf box that holds record t.
     // k_material tests an any-hit ray against its cell's triangle under that leaf box first:
     // a hit there is one the traversal would find too, so the ray is resolved as occluded.
     // occ == nullptr: off.
     uint32_t* occ;
+    // The lookup gate, two words kept with the table (not cleared with the film, so it learns across
+    // frames; reset at upload): [0] skip: k_material skips the lookups while nonzero; k_accumulate
+    // sets it to [1] after an iteration whose lookups resolved under 1 in kOccMinRate of the rays
+    // tested and counts it down one per iteration; k_trace records occluders only while it is <= 1,
+    // so the next lookups meet a fresh table.  [1] backoff: 3, 7, 15, ... 255 after consecutive
+    // failed lookup iterations, 0 while they pay.
+    uint32_t* occ_gate;
     const float4* leaf_box;
     uint32_t ntri;
     int occ_g, occ_b;       // origin cells per axis, direction bins per face coordinate
     float occ_inv[3];       // occ_g / root box extent, per axis
 };
 constexpr uint32_t kOccEmpty = 0xffffffffu;
-__host__ __device__ constexpr size_t occ_entries(int g, int b) { return (size_t)g * g * g * 6 * b * b; }
+constexpr uint32_t kOccWays = 2;      // entries per cell: k_trace writes way tri mod 2, k_material tests both
+                                      // (1 way resolved 52 % of config 2's any-hit rays, 2 ways 64 %)
+constexpr uint32_t kOccMinRate = 10;  // lookups pay when >= 1 in kOccMinRate resolves a ray (see occ_skip)
+__host__ __device__ constexpr size_t occ_entries(int g, int b) { return (size_t)g * g * g * 6 * b * b * kOccWays; }
 
 struct DevPaths {
     float4 *ray_o, *ray_d, *sray_o, *sray_d, *beta, *nee0, *nee1, *Ld;
@@ -111,7 +121,8 @@ struct DevPaths {
 constexpr int kShards = 64;
 constexpr int kMaxParts = kShards;  // k_trace work partitions (at most one per queue shard)
 enum : int { C_EXT = 0, C_ANY = 1, C_VIS = 2, C_STATS = 3, C_EXT_RAYS = 9, C_ANY_RAYS = 10, C_MAT = 11, C_OCC = 12,
-              C_WORDS = 32 };  // C_STATS..+5; C_OCC: any-hit rays resolved by the occluder cache
+              C_OCC_TRY = 13, C_WORDS = 32 };  // C_STATS..+5; C_OCC / C_OCC_TRY: any-hit rays resolved by /
+                                               // tested against the occluder cache
 struct CounterBlock {
     uint32_t shard[kShards][C_WORDS];  // [0] ext pushes [1] any-hit pushes [2] vis rays [3..8] traversal stats [9,10] rays [11] material pushes
     uint32_t last_ext, last_live;
@@ -242,7 +253,7 @@ void launch_copy(const float4* src, float4* dst, size_t n, hipStream_t s);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);
 void launch_tonemap(const TonemapArgs& a, hipStream_t s);
 void launch_resolve(const ResolveArgs& a, hipStream_t s);
-void launch_accumulate(CounterBlock* c, uint32_t nparts, hipStream_t s);
+void launch_accumulate(CounterBlock* c, uint32_t nparts, uint32_t* occ_gate, hipStream_t s);
 void launch_pack(const PackArgs& a, hipStream_t s);
 void launch_unpack(const UnpackArgs& a, hipStream_t s);
 

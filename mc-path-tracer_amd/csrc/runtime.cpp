@@ -616,23 +616,25 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     s.occ = nullptr;
     s.leaf_box = nullptr;
     {
-        int G = 8, B = 8;
+        int G = 16, B = 8;
         if (const char* e = getenv("MCPT_OCC_G")) G = atoi(e);
         if (const char* e = getenv("MCPT_OCC_B")) B = atoi(e);
         if (G > 0 && G <= 64 && B > 0 && B <= 64 && d->ntri > 0) {
             float4* lbx;
             uint32_t* occ;
             const size_t ne = occ_entries(G, B);
-            if ((rc = dalloc(c, c->scene_bufs, &lbx, 2 * (size_t)d->ntri)) || (rc = dalloc(c, c->scene_bufs, &occ, ne)))
+            if ((rc = dalloc(c, c->scene_bufs, &lbx, 2 * (size_t)d->ntri)) || (rc = dalloc(c, c->scene_bufs, &occ, ne + 2)))
                 return rc;
             // NaN boxes (all-ones bytes) for a record no leaf holds: occ_hit's slab then fails
             HIPCHK(c, hipMemsetAsync(lbx, 0xff, 2 * (size_t)d->ntri * sizeof(float4), c->stream));
             HIPCHK(c, hipMemsetAsync(occ, 0xff, ne * sizeof(uint32_t), c->stream));
+            HIPCHK(c, hipMemsetAsync(occ + ne, 0, 2 * sizeof(uint32_t), c->stream));  // the lookup gate: on
             launch_leaf_boxes(s, nnodes, lbx, c->stream);
             HIPCHK(c, hipGetLastError());
             HIPCHK(c, hipStreamSynchronize(c->stream));
             s.leaf_box = lbx;
             s.occ = occ;
+            s.occ_gate = occ + ne;
             s.occ_g = G;
             s.occ_b = B;
             for (int k = 0; k < 3; k++) {
@@ -888,7 +890,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     ta.idle = &c->cnt->idle;
     launch_trace(ta, c->geom, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
-    launch_accumulate(c->cnt, c->geom.trace_parts, c->stream);
+    launch_accumulate(c->cnt, c->geom.trace_parts, c->scene.occ ? c->scene.occ_gate : nullptr, c->stream);
     HIPCHK(c, hipGetLastError());
     return MCPT_OK;
 }

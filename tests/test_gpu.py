@@ -280,6 +280,55 @@ def test_path_slots_ragged_and_resize(mcpt_mod, oracle, scene_c2):
         p.close()
 
 
+@pytest.mark.parametrize("which", ["scene_c2", "scene_cube", "scene_c1", "scene_c3"])
+def test_occluder_cache_same_film(request, mcpt_mod, which):
+    """The any-hit occluder cache (kernels.hip occ_hit) decides only which any-hit rays skip the
+    traversal: a cached triangle counts only under its own leaf box with the traversal's slab
+    arithmetic and cull, so every ray it resolves is one the traversal finds occluded too.  Films
+    and ray counts with the cache (default; a cold table, then a warm one on the re-render) and
+    without it (MCPT_OCC_G=0 at upload) are bit-identical; on the closed config-2 box and the cube
+    (flat, axis-aligned leaf boxes) it resolves rays."""
+    scene = request.getfixturevalue(which)[0]
+    W, H = 160, 90
+    if which == "scene_cube":
+        cam = mcpt_mod.make_camera((0.3, 0.1, 3.0), aspect=W / H)
+    else:
+        cam = mcpt_mod.config_camera(mcpt_mod.CONFIGS[int(which[-1])], W, H)
+
+    def run(env):
+        old = os.environ.get("MCPT_OCC_G")
+        if env is None:
+            os.environ.pop("MCPT_OCC_G", None)
+        else:
+            os.environ["MCPT_OCC_G"] = env
+        try:
+            pt = make_pt(mcpt_mod, scene, cam, W, H, 24, 5, tile=64)
+        finally:
+            if old is None:
+                os.environ.pop("MCPT_OCC_G", None)
+            else:
+                os.environ["MCPT_OCC_G"] = old
+        pt.set_path_slots(2)
+        out = []
+        for _ in range(2):
+            pt.clear()
+            st = pt.render()
+            L, smp = pt.film()
+            out.append((L.copy(), smp.copy(), (st.extend_rays, st.shadow_rays, st.vis_rays), pt.occ_stats()))
+        pt.close()
+        return out
+
+    off, on = run("0"), run(None)
+    assert off[0][3] == (0, False) and on[0][3][1]
+    for a in on + off[1:]:
+        assert np.array_equal(a[0].view(np.uint32), off[0][0].view(np.uint32))
+        assert np.array_equal(a[1], off[0][1]) and a[2] == off[0][2]
+    resolved = on[1][3][0]
+    print(f"{which}: any-hit rays {sum(off[0][2][1:])}, resolved by the warm cache {resolved}")
+    if which in ("scene_c2", "scene_cube"):
+        assert resolved > 0
+
+
 def test_finished_blocks_skip_and_reset(mcpt_mod, scene_c2):
     """k_shade's block done flags (ShadeArgs::blk_done): once a film is complete, further
     iterations trace nothing and leave it bit for bit; a film clear resets the flags, so the
