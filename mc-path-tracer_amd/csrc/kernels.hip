@@ -270,7 +270,33 @@ __device__ inline bool occ_test(V3 o, V3 d, V3 inv, float4 bmn, float4 bmx, floa
 __device__ inline uint2 occ_entry(const DevScene& sc, V3 o, V3 d) {
     return reinterpret_cast<const uint2*>(sc.occ)[occ_index(sc, o, d)];
 }
-// true: (o, d) is occluded by one of its cell's cached triangles e.  Both candidates' leaf boxes
+// Both any-hit rays of a path against their cells' entries: all four candidates' leaf boxes and
+// records are fetched in one round trip (an empty way reads record 0 and is not tested).
+__device__ inline void occ_hit2(const DevScene& sc, V3 ol, V3 dl, uint2 el, V3 ob, V3 db, uint2 eb, bool& hl,
+                                bool& hb) {
+    hl = hb = false;
+    const bool v0 = el.x < sc.ntri, v1 = el.y < sc.ntri, v2 = eb.x < sc.ntri, v3_ = eb.y < sc.ntri;
+    if (!(v0 || v1 || v2 || v3_)) return;
+    const uint32_t t[4] = {v0 ? el.x : 0u, v1 ? el.y : 0u, v2 ? eb.x : 0u, v3_ ? eb.y : 0u};
+    float4 bn[4], bx[4], r0[4], r1[4], r2[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        bn[k] = sc.leaf_box[2 * t[k]];
+        bx[k] = sc.leaf_box[2 * t[k] + 1];
+        const float4* p = sc.tri + kTriF4 * t[k];
+        r0[k] = p[0];
+        r1[k] = p[1];
+        r2[k] = p[2];
+    }
+    const V3 il = v3(1.f / dl.x, 1.f / dl.y, 1.f / dl.z), ib = v3(1.f / db.x, 1.f / db.y, 1.f / db.z);  // k_trace's
+    const bool fl = __builtin_fabsf(il.x) < K_INF_F && __builtin_fabsf(il.y) < K_INF_F && __builtin_fabsf(il.z) < K_INF_F;
+    const bool fb = __builtin_fabsf(ib.x) < K_INF_F && __builtin_fabsf(ib.y) < K_INF_F && __builtin_fabsf(ib.z) < K_INF_F;
+    hl = fl && ((v0 && occ_test(ol, dl, il, bn[0], bx[0], r0[0], r1[0], r2[0])) ||
+                (v1 && occ_test(ol, dl, il, bn[1], bx[1], r0[1], r1[1], r2[1])));
+    hb = fb && ((v2 && occ_test(ob, db, ib, bn[2], bx[2], r0[2], r1[2], r2[2])) ||
+                (v3_ && occ_test(ob, db, ib, bn[3], bx[3], r0[3], r1[3], r2[3])));
+}
+// true: (o, d) is occluded by one of its cell's cached triangles e.// true: (o, d) is occluded by one of its cell's cached triangles e.  Both candidates' leaf boxes
 // and records are fetched in one round trip (an empty way reads record 0 and is not tested).
 __device__ inline bool occ_hit(const DevScene& sc, V3 o, V3 d, uint2 e) {
     const bool v0 = e.x < sc.ntri, v1 = e.y < sc.ntri;
@@ -323,6 +349,7 @@ __shared__ unsigned long long s_sprof[kBlock / 64][12];
 struct MatOut {
     bool want_ext, want_l, want_b, trivial_ext, vis_ray;
     uint32_t trivial_any;
+    uint2 el, eb;  // occluder-cache entries of the light / BRDF rays (loads issued inside material())
 };
 
 // Light choice + wf_mat_mix for the continuing path pid (vertex len, sample index
@@ -334,9 +361,10 @@ struct MatOut {
 // Gram-Schmidt (A.9), env sampling/pdf on matched, clamped cells (A.11).
 template <bool FIXED>
 __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sidx, uint32_t len, V3 beta_store,
-                                 int32_t htri, float4* stage) {
+                                 int32_t htri, float4* stage, bool occ_on) {
     const DevScene& sc = a.scene;
-    MatOut mo{false, false, false, false, false, 0u};
+    const uint2 none = make_uint2(kOccEmpty, kOccEmpty);
+    MatOut mo{false, false, false, false, false, 0u, none, none};
     SPROF_T0();
     // path slot -> pixel; the sample index comes with the record (k_shade: slot k of a pixel
     // runs samples k, k + S, k + 2S, ...)
@@ -421,6 +449,9 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
             stage[0 * kBlock + threadIdx.x] = f4(so_l, 0.f);
             stage[1 * kBlock + threadIdx.x] = f4(ldir, 0.f);
             mo.want_l = true;
+            // the occluder-cache entry, loaded now and used after material(): its latency
+            // hides behind the BRDF sample below
+            if (occ_on) mo.el = occ_entry(sc, so_l, ldir);
         }
     }
     SPROF(5);
@@ -428,6 +459,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
     if (!delta) {
         V3 wi_b = brdf_sample_wi<FIXED>(m, n, wo, r, SL_MAT_E0, r(SL_MAT_LOBE) < 0.5f);  // spec : diff
         const V3 so_b = pos + wi_b * 0.001f;
+        if (occ_on) mo.eb = occ_entry(sc, so_b, wi_b);  // (used only if the ray is queued)
         V3 f_b;
         float pdfb_x;
         brdf_f_pdf(m, n, wi_b, wo, f_b, pdfb_x);
@@ -452,7 +484,6 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
     a.p.nee1[pid] = f4(cB, rr.z);
     a.p.flags[pid] = nf | ((len + 1) << F_LEN_SHIFT) | (sidx << F_SIDX_SHIFT);  // extend increments len (:270)
     SPROF(6);
-    SPROF(7);
     return mo;
 }
 
@@ -460,6 +491,9 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
 #define MCPT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_SHADE_WPE, MCPT_SHADE_WPE)))
 #else
 #define MCPT_SHADE_ATTR
+#endif
+#ifndef MCPT_MAT_WPE
+#define MCPT_MAT_WPE 4  // 4 waves per SIMD (<= 128 VGPRs): without it the occluder-cache prefetch tips it to 130
 #endif
 #ifdef MCPT_MAT_WPE
 #define MCPT_MAT_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_MAT_WPE, MCPT_MAT_WPE)))
@@ -706,32 +740,35 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
             const uint4 q = a.mat_rec[shard * a.ext_cap + i];  // {pid, len, sample index, hit_tri}
             const float4 b4 = a.mat_beta[shard * a.ext_cap + i];
             mpid = q.x;
-            mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w, &s_any[0][0]);
+            mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w, &s_any[0][0], occ_on);
+#ifdef MCPT_SHADE_PROF
+            unsigned long long _sp_t = __builtin_readcyclecounter();
+#endif
             // the occluder cache (see occ_hit), after the path's shading state is dead: a ray it
             // resolves gets its wf_shadow result here and is not queued
             if (occ_on) {
                 try_l = mo.want_l;
                 try_b = mo.want_b;
-                // both rays' cell entries in one round trip, then each ray's candidates
                 const V3 ol = xyz(s_any[0][threadIdx.x]), dl = xyz(s_any[1][threadIdx.x]);
                 const V3 ob = xyz(s_any[2][threadIdx.x]), db = xyz(s_any[3][threadIdx.x]);
-                const uint2 none = make_uint2(kOccEmpty, kOccEmpty);
-                const uint2 el = mo.want_l ? occ_entry(a.scene, ol, dl) : none;
-                const uint2 eb = mo.want_b ? occ_entry(a.scene, ob, db) : none;
-                if (mo.want_l && occ_hit(a.scene, ol, dl, el)) {
+                occ_hit2(a.scene, ol, dl, mo.want_l ? mo.el : make_uint2(kOccEmpty, kOccEmpty), ob, db,
+                         mo.want_b ? mo.eb : make_uint2(kOccEmpty, kOccEmpty), occ_l, occ_b);
+                if (occ_l) {
                     a.p.vis[2 * mpid] = 0;
                     mo.want_l = false;
                     mo.trivial_any++;
-                    occ_l = true;
                 }
-                if (mo.want_b && occ_hit(a.scene, ob, db, eb)) {
+                if (occ_b) {
                     a.p.vis[2 * mpid + 1] = 0;
                     mo.want_b = false;
                     mo.trivial_any++;
-                    occ_b = true;
                 }
             }
+            SPROF(7);  // occluder-cache lookups
         }
+#ifdef MCPT_SHADE_PROF
+        unsigned long long _t_push = __builtin_readcyclecounter();
+#endif
         bool want[3] = {mo.want_ext, mo.want_l, mo.want_b};
         uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
         uint32_t slot[3], total[3];
@@ -757,6 +794,9 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
         n_any += (uint32_t)(__popcll(__ballot(mo.want_l)) + __popcll(__ballot(mo.want_b)) +
                             __popcll(__ballot(mo.trivial_any >= 1u)) + __popcll(__ballot(mo.trivial_any >= 2u)));
         n_vis += (uint32_t)__popcll(__ballot(mo.vis_ray));
+#ifdef MCPT_SHADE_PROF
+        if (lane == 0) s_sprof[threadIdx.x >> 6][9] += __builtin_readcyclecounter() - _t_push;  // pushes + stores
+#endif
     }
     if (lane == 0) {
         if (n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);

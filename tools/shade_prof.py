@@ -13,7 +13,7 @@ N = 10
 st = pt.iterate(N)
 p = list(pt.trace_profile().values())
 names = ["shade:logic", "shade:gen", "shade:push", "mat:hit_record", "mat:continuation", "mat:light_sample",
-         "mat:brdf_sample", "-", "mat:whole kernel"]
+         "mat:brdf_sample", "mat:occ_lookup", "mat:whole kernel", "mat:push+stores"]
 sw, mw = p[11], p[10]
 print(f"k_shade waves/launch {sw / N:.0f}  k_material waves/launch {mw / N:.0f}  ms/iter (both) {st.ms_shade / N:.4f}")
 for i, n in enumerate(names):
