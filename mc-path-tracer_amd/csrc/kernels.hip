@@ -246,6 +246,8 @@ __device__ inline uint32_t occ_index(const DevScene& sc, V3 o, V3 d) {
     const uint32_t ub = (uint32_t)__builtin_fminf(__builtin_fmaxf(u * r + hb, 0.f), bm);
     const uint32_t vb = (uint32_t)__builtin_fminf(__builtin_fmaxf(v * r + hb, 0.f), bm);
     const uint32_t G = (uint32_t)sc.occ_g, B = (uint32_t)sc.occ_b;
+    // one table cell per key (hashing the keys into a 2^21- or 2^23-cell table measured 43 % / 60 %
+    // of config 2's any-hit rays resolved against 72 % direct: the keys that occur collide heavily)
     return ((((cz * G + cy) * G + cx) * 6u + face) * B + ub) * B + vb;
 }
 

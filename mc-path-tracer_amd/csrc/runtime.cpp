@@ -616,10 +616,13 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     s.occ = nullptr;
     s.leaf_box = nullptr;
     {
-        int G = 16, B = 8;
+        // 32^3 cells x 6 x 16^2 bins x 2 ways = 403 MB (config 2: 72 % of the any-hit rays resolved,
+        // against 68 % with 16^3 x 8^2 at 12.6 MB; +1 % frame rate)
+        int G = 32, B = 16;
         if (const char* e = getenv("MCPT_OCC_G")) G = atoi(e);
         if (const char* e = getenv("MCPT_OCC_B")) B = atoi(e);
-        if (G > 0 && G <= 64 && B > 0 && B <= 64 && d->ntri > 0) {
+        // the index G^3 * 6 * B^2 must fit 32 bits
+        if (G > 0 && G <= 64 && B > 0 && B <= 64 && (uint64_t)G * G * G * 6 * B * B <= 0xffffffffull && d->ntri > 0) {
             float4* lbx;
             uint32_t* occ;
             const size_t ne = occ_entries(G, B);
