@@ -440,6 +440,7 @@ def main():
             "iterations_per_step_rank0": round(st.iterations / K, 1),
             "parallelism": f"tiles{world}",
             "path_slots": slots,
+            "occluder_cache": pt.occ_stats()[1],  # any-hit occluder cache: same results
             "device": pt.device_name,
         },
         "stage_ms_per_step": {"k_trace": round(st.ms_extend / K, 3), "k_shade+k_material": round(st.ms_shade / K, 3)},

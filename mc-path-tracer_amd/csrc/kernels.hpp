@@ -89,8 +89,7 @@ struct DevScene {
     // a hit there is one the traversal would find too, so the ray is resolved as occluded.
     // occ == nullptr: off.
     uint32_t* occ;
-    // The lookup gate, two words kept with the table (not cleared with the film, so it learns across
-    // frames; reset at upload): [0] skip: k_material skips the lookups while nonzero; k_accumulate
+    // The lookup gate, two words kept with the table (both reset at upload and with the film): [0] skip: k_material skips the lookups while nonzero; k_accumulate
     // sets it to [1] after an iteration whose lookups resolved under 1 in kOccMinRate of the rays
     // tested and counts it down one per iteration; k_trace records occluders only while it is <= 1,
     // so the next lookups meet a fresh table.  [1] backoff: 3, 7, 15, ... 255 after consecutive

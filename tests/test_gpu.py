@@ -285,9 +285,9 @@ def test_occluder_cache_same_film(request, mcpt_mod, which):
     """The any-hit occluder cache (kernels.hip occ_hit) decides only which any-hit rays skip the
     traversal: a cached triangle counts only under its own leaf box with the traversal's slab
     arithmetic and cull, so every ray it resolves is one the traversal finds occluded too.  Films
-    and ray counts with the cache (default; a cold table, then a warm one on the re-render) and
-    without it (MCPT_OCC_G=0 at upload) are bit-identical; on the closed config-2 box and the cube
-    (flat, axis-aligned leaf boxes) it resolves rays."""
+    and ray counts with the cache (default; it starts empty with every film clear and fills during
+    the frame) and without it (MCPT_OCC_G=0 at upload) are bit-identical, frame after frame; on the
+    closed config-2 box and the cube (flat, axis-aligned leaf boxes) it resolves rays."""
     scene = request.getfixturevalue(which)[0]
     W, H = 160, 90
     if which == "scene_cube":
@@ -324,7 +324,10 @@ def test_occluder_cache_same_film(request, mcpt_mod, which):
         assert np.array_equal(a[0].view(np.uint32), off[0][0].view(np.uint32))
         assert np.array_equal(a[1], off[0][1]) and a[2] == off[0][2]
     resolved = on[1][3][0]
-    print(f"{which}: any-hit rays {sum(off[0][2][1:])}, resolved by the warm cache {resolved}")
+    # the table is emptied with each film clear, so both frames start cold; which rays it resolves
+    # depends on the order the traversal's records land in (racy stores), never the films
+    assert abs(on[0][3][0] - resolved) <= 0.05 * max(resolved, 20)
+    print(f"{which}: any-hit rays {sum(off[0][2][1:])}, resolved by the cache {resolved}")
     if which in ("scene_c2", "scene_cube"):
         assert resolved > 0
 
