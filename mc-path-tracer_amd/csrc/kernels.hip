@@ -298,22 +298,6 @@ __device__ inline void occ_hit2(const DevScene& sc, V3 ol, V3 dl, uint2 el, V3 o
     hb = fb && ((v2 && occ_test(ob, db, ib, bn[2], bx[2], r0[2], r1[2], r2[2])) ||
                 (v3_ && occ_test(ob, db, ib, bn[3], bx[3], r0[3], r1[3], r2[3])));
 }
-// true: (o, d) is occluded by one of its cell's cached triangles e.// true: (o, d) is occluded by one of its cell's cached triangles e.  Both candidates' leaf boxes
-// and records are fetched in one round trip (an empty way reads record 0 and is not tested).
-__device__ inline bool occ_hit(const DevScene& sc, V3 o, V3 d, uint2 e) {
-    const bool v0 = e.x < sc.ntri, v1 = e.y < sc.ntri;
-    if (!v0 && !v1) return false;
-    const uint32_t t0 = v0 ? e.x : 0u, t1 = v1 ? e.y : 0u;
-    const float4 b0n = sc.leaf_box[2 * t0], b0x = sc.leaf_box[2 * t0 + 1];
-    const float4 b1n = sc.leaf_box[2 * t1], b1x = sc.leaf_box[2 * t1 + 1];
-    const float4* p0 = sc.tri + kTriF4 * t0;
-    const float4* p1 = sc.tri + kTriF4 * t1;
-    const float4 r00 = p0[0], r01 = p0[1], r02 = p0[2], r10 = p1[0], r11 = p1[1], r12 = p1[2];
-    const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);  // k_trace's reciprocal
-    if (!(__builtin_fabsf(inv.x) < K_INF_F && __builtin_fabsf(inv.y) < K_INF_F && __builtin_fabsf(inv.z) < K_INF_F))
-        return false;
-    return (v0 && occ_test(o, d, inv, b0n, b0x, r00, r01, r02)) || (v1 && occ_test(o, d, inv, b1n, b1x, r10, r11, r12));
-}
 
 // ---------------------------------------------------------------------------
 // k_shade: the first half of one wavefront iteration's shading, for one block of
@@ -746,7 +730,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
 #ifdef MCPT_SHADE_PROF
             unsigned long long _sp_t = __builtin_readcyclecounter();
 #endif
-            // the occluder cache (see occ_hit), after the path's shading state is dead: a ray it
+            // the occluder cache (see occ_hit2), after the path's shading state is dead: a ray it
             // resolves gets its wf_shadow result here and is not queued
             if (occ_on) {
                 try_l = mo.want_l;
@@ -1014,7 +998,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     };
     enter(home);
     const DevScene& sc = a.scene;
-    // occluder-cache records (see occ_hit): off while k_material's lookups are gated off, except in
+    // occluder-cache records (see occ_hit2): off while k_material's lookups are gated off, except in
     // the iteration before the next lookups (DevScene::occ_gate)
     const bool occ_rec = sc.occ && sc.occ_gate[0] <= 1u;
 
@@ -1081,7 +1065,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
 #endif
         if (kind) {
             a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
-            if (tri >= 0 && occ_rec)  // the cell's occluder (occ_hit)
+            if (tri >= 0 && occ_rec)  // the cell's occluder (occ_hit2)
                 sc.occ[(size_t)occ_index(sc, o, d) * kOccWays + (uint32_t)tri % kOccWays] = (uint32_t)tri;
         } else {
             a.hit_tri[rid] = tri;  // hit record rebuilt by the consumer (hit_record())

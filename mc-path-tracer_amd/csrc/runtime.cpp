@@ -610,7 +610,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     }
     s.depth = width == 4 ? quad_push : c->pair_depth;
     s.width = width;
-    // Any-hit occluder cache (kernels.hip occ_hit): every triangle record's leaf box and the
+    // Any-hit occluder cache (kernels.hip occ_hit2): every triangle record's leaf box and the
     // (origin cell x direction bin) table, empty at upload.  MCPT_OCC_G=0 turns it off;
     // MCPT_OCC_G / MCPT_OCC_B set the cells per axis / bins per face coordinate.
     s.ntri = (uint32_t)d->ntri;
@@ -630,7 +630,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             const size_t ne = occ_entries(G, B);
             if ((rc = dalloc(c, c->scene_bufs, &lbx, 2 * (size_t)d->ntri)) || (rc = dalloc(c, c->scene_bufs, &occ, ne + 2)))
                 return rc;
-            // NaN boxes (all-ones bytes) for a record no leaf holds: occ_hit's slab then fails
+            // NaN boxes (all-ones bytes) for a record no leaf holds: occ_test's slab then fails
             HIPCHK(c, hipMemsetAsync(lbx, 0xff, 2 * (size_t)d->ntri * sizeof(float4), c->stream));
             HIPCHK(c, hipMemsetAsync(occ, 0xff, ne * sizeof(uint32_t), c->stream));
             HIPCHK(c, hipMemsetAsync(occ + ne, 0, 2 * sizeof(uint32_t), c->stream));  // the lookup gate: on

@@ -282,7 +282,7 @@ def test_path_slots_ragged_and_resize(mcpt_mod, oracle, scene_c2):
 
 @pytest.mark.parametrize("which", ["scene_c2", "scene_cube", "scene_c1", "scene_c3"])
 def test_occluder_cache_same_film(request, mcpt_mod, which):
-    """The any-hit occluder cache (kernels.hip occ_hit) decides only which any-hit rays skip the
+    """The any-hit occluder cache (kernels.hip occ_hit2) decides only which any-hit rays skip the
     traversal: a cached triangle counts only under its own leaf box with the traversal's slab
     arithmetic and cull, so every ray it resolves is one the traversal finds occluded too.  Films
     and ray counts with the cache (default; it starts empty with every film clear and fills during
