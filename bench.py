@@ -13,13 +13,18 @@ this exact layout).  `--steady` reports the steady-state iteration rate beside i
 
 Multi-GPU: one process per GPU.  `--gpus N` without an external launcher starts
 the N ranks itself (torch.distributed.run, before anything touches the GPU); under a launcher
-WORLD_SIZE must equal N.  256x256 tiles are dealt to ranks by (tx + ty) mod N.
+WORLD_SIZE must equal N.  Film tiles are dealt to ranks by (tx + ty) mod N (64 x 64 tiles for
+N > 1: MULTI_TILE).
   --scaling weak (default): the frame is 1920 x 1080*N pixels of the same view (N-fold vertical
       supersampling), so every rank owns ~one 1080p frame of pixels with the same sky / geometry
       mix as the 1-GPU run;
   --scaling strong: the config's own frame (e.g. --config 4: 3840x2160) split over the ranks.
-No collective runs inside the timed region (tiles are independent); `--gather` sends every
-rank's tile pixels to rank 0's device film after timing (mcpt/parallel.py, RCCL send/recv).
+Under weak scaling an N>1 run then also times the strong split of the config's own frame
+("strong" in the JSON: per-rank times, path slots scaled by each rank's pixel share) and, after
+timing, gathers that frame into rank 0's device film (mcpt/parallel.py: point-to-point RCCL
+sends over xGMI) and checks it against rank 0 rendering the frame alone, bit for bit
+(--no-strong / --no-gather / --no-verify-gather skip these).  No collective runs inside a
+timed region: tiles are independent.
 """
 from __future__ import annotations
 
@@ -46,7 +51,7 @@ B_HIT = 40            # per closest hit: 3 normals + material id
 B_SHADE = 195 + 172   # logic + material per path-bounce
 B_GEN = 49            # generate per new sample
 # Path slots (paths in flight per pixel) per BASELINE config: the measured best of the
-# whole-frame sweep (tools/gpu_kstats.sh, DESIGN.md section 2: config 2 at 3/8/16/24/32 slots
+# whole-frame sweep (tools/gpu/run.sh kstats, DESIGN.md section 2: config 2 at 3/8/16/24/32 slots
 # 7287/7856/8064/8095/8081 Mray/s, config 3 at 3/16/32 4924/6624/6822, config 5 (64 spp) at
 # 4/8/16 5257/5458/5486); the parity tests and smoke() run the same layout.
 BENCH_SLOTS = {1: 16, 2: 24, 3: 32, 4: 16, 5: 16}
@@ -63,16 +68,30 @@ def parse(argv=None):
     ap.add_argument("--spp", type=int, default=None, help="override the config's spp (not the BASELINE workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=12, help="spp of the full-frame CPU-oracle sample")
-    ap.add_argument("--gather", action="store_true", help="gather the film on rank 0 after timing (N>1)")
-    ap.add_argument("--verify-gather", action="store_true",
-                    help="with --gather: rank 0 then renders the whole frame alone and checks the gathered film "
-                         "equals it bit for bit")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="N>1: skip the strong-scaling split of the config's own frame (run after the weak frames)")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: skip the frame-end gather of the strong frame into rank 0's device film (RCCL)")
+    ap.add_argument("--no-verify-gather", action="store_true",
+                    help="N>1: skip checking the gathered frame against rank 0 rendering it alone (bit for bit)")
     ap.add_argument("--steady", action="store_true",
                     help="also time 60 steady-state iterations (outside value; off by default so that every "
                          "k_trace launch of the process belongs to a timed or warmup frame, as rocprofv3 sees it)")
     ap.add_argument("--slots", type=int, default=int(os.environ["MCPT_BENCH_SLOTS"]) if "MCPT_BENCH_SLOTS" in os.environ else None,
                     help="paths in flight per pixel (mcpt_set_path_slots); default BENCH_SLOTS[config]")
     return ap.parse_args(argv)
+
+
+# Film tile of the multi-GPU partition.  The rank of tile (tx, ty) is (tx + ty) mod N; with the
+# reference's 256 x 256 tiles (Film.cu:17) a 1080p frame is 8 x 5 tiles, and at N = 8 each rank's
+# five tiles form one diagonal: the slowest partition took 1.74x the mean (one GPU timing each
+# partition alone, profiles/partition_r04.json).  64 x 64 tiles (510 of them) give 1.03 at N = 8,
+# 1.006 at N = 4.  Results do not depend on the tiling (keyed RNG); one rank keeps 256.
+MULTI_TILE = 64
+
+
+def part_tile(world):
+    return 256 if world == 1 else MULTI_TILE
 
 
 def tiles_for(rank, world, W, H, tile):
@@ -197,10 +216,13 @@ class Acc:
     KEYS = ("extend_rays", "shadow_rays", "vis_rays", "iterations", "ms_shade", "ms_extend",
             "ext_nodes", "ext_tests", "ext_hits", "any_nodes", "any_tests", "any_hits")
 
+    RAYS = ("extension", "extension_traversed", "any_hit", "any_hit_traversed", "any_hit_occluder_cache")
+
     def __init__(self):
         for k in self.KEYS:
             setattr(self, k, 0)
         self.occ = 0  # any-hit rays the occluder cache resolved in k_material (not traced by k_trace)
+        self.counts = dict.fromkeys(self.RAYS, 0)  # mcpt_debug_ray_counts, summed over frames
 
     def add(self, st):
         for k in self.KEYS:
@@ -211,7 +233,7 @@ class Acc:
         return int(self.extend_rays + self.shadow_rays + self.vis_rays)
 
 
-def roofline(st, ms_trace, ms_shade, config, slots):
+def roofline(st, ms_trace, ms_shade, config, slots, work=None):
     """roofline object of the dominant kernel (k_trace) and of the shading stages.
 
     achieved = SURVEY.md 8(d)'s algorithmic bytes that live in HBM: the per-ray state (65 B per
@@ -221,15 +243,21 @@ def roofline(st, ms_trace, ms_shade, config, slots):
     roof is the L2's).  traffic = measured HBM bytes per launch from the committed rocprofv3 PMC
     summary (profiles/pmc_r*.json) when it was taken on this code and workload.  bound = the
     resource with the highest measured utilisation (HBM traffic, L2 bytes, VALU issue), or
-    "latency" when none reaches 0.5."""
+    "latency" when none reaches 0.5.  work: the traversal work counters (node steps, triangle
+    tests, hits) of one extra, untimed frame rendered with mcpt_set_work_counters on (the counting
+    k_trace build is slower, so the timed frames run without it); st's own counters otherwise."""
     n = max(1, st.iterations)
+    w = work if work is not None else st
+    wn = max(1, w.iterations)
+    w_occ = getattr(w, "occ", 0)
+    w_ext, w_any = w.extend_rays, w.shadow_rays + w.vis_rays - w_occ
     avg_s = ms_trace / n * 1e-3
     ext_q = st.extend_rays
     any_all = st.shadow_rays + st.vis_rays
     occ = getattr(st, "occ", 0)
     any_q = any_all - occ  # any-hit rays k_trace traced (the occluder cache resolved the rest)
     state = (B_EXT_STATE * ext_q + B_ANY_STATE * any_q) / n
-    bvh = (2 * B_NODE * (st.ext_nodes + st.any_nodes) + B_TRI * (st.ext_tests + st.any_tests) + B_HIT * st.ext_hits) / n
+    bvh = (2 * B_NODE * (w.ext_nodes + w.any_nodes) + B_TRI * (w.ext_tests + w.any_tests) + B_HIT * w.ext_hits) / wn
     achieved = state / avg_s
     names = {"k_trace": ("mcpt_dev::k_trace<",), "shade": ("mcpt_dev::k_shade<", "mcpt_dev::k_material<")}
     summary, stale = pmc_summary(config, slots)
@@ -246,11 +274,13 @@ def roofline(st, ms_trace, ms_shade, config, slots):
                              "l2_peak_GBps": L2_PEAK / 1e9, "l2_frac": round(bvh / avg_s / L2_PEAK, 4),
                              "what": "SURVEY 8(d) B_bvh: 64 B per child-pair node step, 36 B per triangle "
                                      "test, 40 B per closest hit (logical; served by L1/L2/MALL)"},
-            "per_ray": {"ext_pair_nodes": round(st.ext_nodes / max(1, ext_q), 2),
-                        "ext_tri_tests": round(st.ext_tests / max(1, ext_q), 2),
-                        "any_pair_nodes": round(st.any_nodes / max(1, any_q), 2),
-                        "any_tri_tests": round(st.any_tests / max(1, any_q), 2),
-                        "any_resolved_by_occluder_cache": round(occ / max(1, any_all), 4)}}
+            "per_ray": {"ext_pair_nodes": round(w.ext_nodes / max(1, w_ext), 2),
+                        "ext_tri_tests": round(w.ext_tests / max(1, w_ext), 2),
+                        "any_pair_nodes": round(w.any_nodes / max(1, w_any), 2),
+                        "any_tri_tests": round(w.any_tests / max(1, w_any), 2),
+                        "any_resolved_by_occluder_cache": round(occ / max(1, any_all), 4),
+                        "counted_on": "one extra untimed frame, counting k_trace build" if work is not None
+                                      else "the timed frames"}}
     util = {"l2": roof["cache_served"]["l2_frac"]}
     if traffic is not None:
         roof["traffic_GBps"] = round(traffic / avg_s / 1e9, 1)
@@ -286,6 +316,118 @@ def roofline(st, ms_trace, ms_shade, config, slots):
     return roof
 
 
+def extend_shade(st, frame_s, steps, config, slots):
+    """The metric's own roofline fraction: the whole wavefront step (extend + shade: k_shade,
+    k_material, k_trace) against 8 TB/s, per frame.  state: SURVEY.md 8(d)'s algorithmic bytes
+    (465 B per path-bounce split as logic+material 367 per continuing path-bounce, extend 65 per
+    extension ray, shadow 33 per any-hit ray, generate 49 per new sample); traffic: the committed
+    PMC summary's HBM bytes per launch of each kernel x launches per frame (when its stamp matches
+    this code and workload)."""
+    K = max(1, steps)
+    it = st.iterations / K
+    gen = max(0, st.extend_rays - st.shadow_rays)
+    state = (B_SHADE * st.shadow_rays + B_GEN * gen + B_EXT_STATE * st.extend_rays +
+             B_ANY_STATE * (st.shadow_rays + st.vis_rays)) / K
+    out = {"frame_s": round(frame_s, 5), "iterations_per_frame": round(it, 1),
+           "state_bytes_per_frame": int(state), "state_GBps": round(state / frame_s / 1e9, 1),
+           "state_frac": round(state / frame_s / HBM_PEAK, 4)}
+    summary, stale = pmc_summary(config, slots)
+    if stale is None:
+        per = [pmc_traffic(summary, (p,)) for p in ("mcpt_dev::k_trace<", "mcpt_dev::k_shade<", "mcpt_dev::k_material<")]
+        if None not in per:
+            traffic = sum(per) * it
+            out.update({"traffic_bytes_per_frame": int(traffic), "traffic_GBps": round(traffic / frame_s / 1e9, 1),
+                        "traffic_frac": round(traffic / frame_s / HBM_PEAK, 4),
+                        "traffic_per_kernel_per_launch": dict(zip(("k_trace", "k_shade", "k_material"), per))})
+    else:
+        out["pmc_stale"] = stale
+    return out
+
+
+def dev_of(backend):
+    return "cuda" if backend == "nccl" else "cpu"
+
+
+def timed_frames(pt, steps, warmup, dist, torch):
+    """warmup untimed frames, then `steps` frames timed between barrier + synchronize on both
+    sides.  A frame: the film cleared and every pixel of the rank's tile set rendered to spp."""
+    for _ in range(warmup):
+        pt.clear()
+        pt.render()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = Acc()
+    for _ in range(steps):
+        pt.clear()
+        st.add(pt.render())  # returns after its stream has drained
+        st.occ += pt.occ_stats()[0]  # host copies of the frame's counters (no device call)
+        for k, v in pt.ray_counts().items():
+            st.counts[k] += v
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    return time.perf_counter() - t0, st
+
+
+def rank_times(dist, dev, dt, rays, world, torch):
+    """Every rank's (seconds, rays) of its timed frames, on every rank (all_gather)."""
+    mine = torch.tensor([dt, float(rays)], dtype=torch.float64, device=dev)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    t = [float(a[0]) for a in allr]
+    r = [float(a[1]) for a in allr]
+    mean = sum(t) / len(t)
+    return {"seconds": [round(x, 4) for x in t], "mray_s": [round(b / a / 1e6, 1) for a, b in zip(t, r)],
+            "max_over_mean": round(max(t) / mean, 4) if mean > 0 else None}
+
+
+def run_strong(pt, rc, rank, world, dist, backend, spp, args, torch):
+    """Strong scaling: the config's own frame split over the ranks by the tile
+    partition, path slots scaled so every rank keeps the one-GPU run's paths in flight
+    (parallel.strong_slots).  Then, outside the timed region, the frame-end gather of the film into
+    rank 0's device film (point-to-point sends over RCCL / xGMI) and its check against rank 0
+    rendering the whole frame alone with the same slots (bit for bit)."""
+    from mcpt import parallel
+
+    W, H = rc.width, rc.height
+    slots = parallel.strong_slots(args.slots or BENCH_SLOTS[args.config], world, W, H, spp)
+    tile = part_tile(world)
+    pt.set_path_slots(slots)
+    pt.resize(W, H, tile, tile)
+    pt.set_tiles(tiles_for(rank, world, W, H, tile))
+    dt, st = timed_frames(pt, args.steps, args.warmup, dist, torch)
+    per = rank_times(dist, dev_of(backend), dt, st.rays, world, torch)
+    tmax = max(per["seconds"])
+    rays = sum(b * a * 1e6 for a, b in zip(per["seconds"], per["mray_s"]))
+    out = {"frame": [W, H], "slots": slots, "spp": spp, "steps": args.steps,
+           "ms_per_frame": round(tmax * 1e3 / args.steps, 3), "mray_s": round(rays / tmax / 1e6, 2),
+           "per_rank": per, "tile": tile, "tiles_per_rank": [len(tiles_for(r, world, W, H, tile)) for r in range(world)]}
+    if not args.no_gather:
+        pt.clear()
+        pt.render()  # the film the gather moves: one whole strong frame
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg = time.perf_counter()
+        parallel.gather_film_to_root(pt, rank, world, tile)
+        torch.cuda.synchronize()
+        out["gather_s"] = round(time.perf_counter() - tg, 4)
+        out["gather_backend"] = dist.get_backend()
+        if not args.no_verify_gather and rank == 0:
+            import numpy as np
+
+            Lg, sg = pt.film()  # the gathered frame
+            pt.set_tiles(None)  # every tile on rank 0 alone: the reference film
+            pt.clear()
+            pt.render()
+            Lr, sr = pt.film()
+            out["gather_equals_one_rank_frame"] = bool(np.array_equal(Lg.view(np.uint32), Lr.view(np.uint32)) and
+                                                       np.array_equal(sg, sr))
+        dist.barrier()
+    return out
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -317,9 +459,13 @@ def main():
 
     import mcpt
 
+    from mcpt import parallel
+
     rc = mcpt.CONFIGS[args.config]
-    slots = args.slots or BENCH_SLOTS[args.config]
     spp = args.spp or rc.spp
+    slots = args.slots or BENCH_SLOTS[args.config]
+    if args.scaling == "strong" and world > 1:  # each rank owns 1/N of the pixels: keep its paths in flight
+        slots = parallel.strong_slots(slots, world, rc.width, rc.height, spp)
     W, H = frame_size(rc, world, args.scaling)
     scene = mcpt.build_config_scene(args.config)
     cam = mcpt.config_camera(rc, rc.width, rc.height)  # the config's view at any N (see docstring)
@@ -327,28 +473,12 @@ def main():
     pt.upload_scene(scene)
     pt.set_camera(cam)
     pt.set_path_slots(slots)
-    pt.resize(W, H)
-    my_tiles = tiles_for(rank, world, W, H, 256)
+    tile = part_tile(world)
+    pt.resize(W, H, tile, tile)
+    my_tiles = tiles_for(rank, world, W, H, tile)
     pt.set_tiles(my_tiles)
 
-    def frame():
-        pt.clear()
-        return pt.render()  # returns after its stream has drained
-
-    for _ in range(args.warmup):
-        frame()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    st = Acc()
-    for _ in range(args.steps):
-        st.add(frame())
-        st.occ += pt.occ_stats()[0]  # host copy of the frame's counters (no device call)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    dt, st = timed_frames(pt, args.steps, args.warmup, dist, torch)
 
     # steady state (outside `value`): iterations with every pixel's paths in flight
     steady = None
@@ -374,25 +504,23 @@ def main():
     else:
         dt_all, rays_all = dt, float(st.rays)
 
-    gathered = verified = None
-    if args.gather and dist:
-        from mcpt import parallel
-
+    # traversal work counters (node steps, triangle tests, hits) from one more, untimed frame with
+    # the counting k_trace build (mcpt_set_work_counters): they feed the roofline's per-ray figures
+    work = None
+    if rank == 0:
+        pt.set_work_counters(True)
         pt.clear()
-        pt.render()  # the film the gather moves: one whole frame
-        dist.barrier()
-        tg = time.perf_counter()
-        parallel.gather_film_to_root(pt, rank, world)
-        gathered = round(time.perf_counter() - tg, 4)
-        if args.verify_gather and rank == 0:
-            import numpy as np
-
-            Lg, sg = pt.film()  # the gathered frame
-            pt.set_tiles(None)  # every tile, one rank: the reference film
-            pt.clear()
-            pt.render()
-            Lr, sr = pt.film()
-            verified = bool(np.array_equal(Lg.view(np.uint32), Lr.view(np.uint32)) and np.array_equal(sg, sr))
+        work = Acc()
+        work.add(pt.render())
+        work.occ = pt.occ_stats()[0]
+        pt.set_work_counters(False)
+    # N > 1: every rank's own time and rays of the timed frames (the value's max-over-ranks above)
+    per_rank = None
+    if dist:
+        per_rank = rank_times(dist, dev_of(backend), dt, st.rays, world, torch)
+    strong = None
+    if dist and not args.no_strong and args.scaling == "weak":
+        strong = run_strong(pt, rc, rank, world, dist, backend, spp, args, torch)
 
     if rank != 0:
         if dist:
@@ -401,7 +529,8 @@ def main():
         return
 
     K = args.steps
-    roof = roofline(st, st.ms_extend, st.ms_shade, args.config, slots)
+    roof = roofline(st, st.ms_extend, st.ms_shade, args.config, slots, work)
+    roof["extend_shade"] = extend_shade(st, dt_all / K, K, args.config, slots)
     roof["measured_copy_GBps"] = round(pt.hbm_copy_gbps(1 << 30, 20), 1)  # one-pass dwordx4 copy ceiling
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -431,10 +560,22 @@ def main():
                         + (" (spp overridden: not the BASELINE workload)" if args.spp else ""),
             "frame": [W, H],
             "spp": spp,
-            "tiles": "256x256, rank = (tx+ty) mod N",
+            "tiles": f"{tile}x{tile}, rank = (tx+ty) mod N",
             "step": "one whole frame: film cleared, every pixel the rank owns rendered to spp "
                     "(all wavefront iterations: shade + extend + shadow)",
             "rays_per_step": int(rays_all / K),
+            "rays_traversed_per_step_rank0": {
+                "extension": int(st.counts["extension_traversed"] / K),
+                "extension_resolved_in_place": int((st.counts["extension"] - st.counts["extension_traversed"]) / K),
+                "any_hit": int(st.counts["any_hit_traversed"] / K),
+                "any_hit_resolved_in_place": int((st.counts["any_hit"] - st.counts["any_hit_traversed"] -
+                                                  st.counts["any_hit_occluder_cache"]) / K),
+                "any_hit_occluder_cache": int(st.counts["any_hit_occluder_cache"] / K),
+                "what": "rays k_trace traversed; the rest of rays_per_step were resolved where they were made "
+                        "(NaN / zero direction or a root-box miss; an any-hit ray occluded by its cell's cached "
+                        "triangle): counted as rays, as the reference traces them",
+                "mray_s_traversed": round((st.counts["extension_traversed"] + st.counts["any_hit_traversed"]) /
+                                          dt / 1e6, 2)},
             "rays_per_step_rank0": {"extension": int(st.extend_rays / K), "shadow": int(st.shadow_rays / K),
                                     "visibility": int(st.vis_rays / K)},
             "iterations_per_step_rank0": round(st.iterations / K, 1),
@@ -453,10 +594,10 @@ def main():
                                "k_trace_ms": round(steady[2] / 60, 4), "shade_ms": round(steady[3] / 60, 4),
                                "what": "60 wavefront iterations after 30, every pixel's path slots in flight "
                                        "(rank 0's kernel times; rays and time over all ranks)"}
-    if gathered is not None:
-        out["gather_s"] = gathered
-    if verified is not None:
-        out["gather_equals_one_rank_frame"] = verified
+    if per_rank:
+        out["per_rank"] = per_rank
+    if strong:
+        out["strong"] = strong
     print(json.dumps(out), flush=True)
     pt.close()
     if dist:

@@ -113,7 +113,8 @@ typedef struct mcpt_stage_stats {
     float ms_shade;         /* k_shade: logic + generate + material (fused) */
     float ms_extend;        /* k_trace: extension AND any-hit rays (one fused persistent launch) */
     float ms_shadow;        /* 0: the any-hit rays are traced inside the k_trace launch */
-    uint64_t ext_nodes;     /* closest-hit: child-pair nodes fetched (2 boxes each) */
+    uint64_t ext_nodes;     /* closest-hit: child-pair nodes fetched (2 boxes each); this and the next five
+                               are counted only under mcpt_set_work_counters(ctx, 1) */
     uint64_t ext_tests;     /* closest-hit: ray/triangle tests */
     uint64_t ext_hits;      /* closest-hit: rays that found a surface */
     uint64_t any_nodes, any_tests, any_hits;   /* any-hit (shadow + visibility) */
@@ -171,7 +172,7 @@ typedef struct mcpt_soa_view {
     float *hit_nrm_mat;     /* EXTEND out: 4*n normal.xyz, (float)material (-1 miss) */
     int32_t *hit_tri;       /* EXTEND out: n triangle index or -1 */
     uint8_t *visible;       /* SHADOW out: n */
-    uint32_t *steps;        /* optional out: per-ray child-pair node fetches + triangle tests */
+    uint32_t *steps;        /* optional out, unused since round 4 (was: per-ray node fetches + tests in diagnostics builds; left zero) */
     mcpt_path_view *paths;  /* LOGIC / GENERATE / MATERIAL: in->paths inputs, out->paths outputs */
 } mcpt_soa_view;
 
@@ -210,6 +211,10 @@ int mcpt_set_path_slots(mcpt_ctx *ctx, uint32_t slots);
  * partition of their die and, once it is drained, join the others, so all settings trace every
  * ray and give identical results -- a tuning knob only (MCPT_TRACE_PARTS sets the default). */
 int mcpt_set_trace_partitions(mcpt_ctx *ctx, uint32_t nparts);
+/* Traversal work counters (mcpt_stage_stats ext_nodes / ext_tests / ext_hits / any_*): on = 1 runs
+ * k_trace's counting build, off (0, the default) leaves them 0.  The counting build holds six more
+ * per-lane registers, which the 64-VGPR 8-wave traversal cannot afford without spilling. */
+int mcpt_set_work_counters(mcpt_ctx *ctx, int32_t on);
 int mcpt_set_tiles(mcpt_ctx *ctx, const uint32_t *tile_xy, uint32_t ntiles); /* batch tile set; NULL = all */
 int mcpt_wavefront_step(mcpt_ctx *ctx, uint32_t tile_x, uint32_t tile_y, mcpt_stage_stats *st); /* one iteration, one tile */
 int mcpt_iterate(mcpt_ctx *ctx, uint32_t iterations, mcpt_stage_stats *st);  /* batch iterations over the tile set */
@@ -258,10 +263,12 @@ int mcpt_debug_node_layout(const mcpt_ctx *ctx);
  * last cleared (counted in shadow_rays / vis_rays as traced rays; they skip the traversal), and
  * whether the uploaded scene has the cache (MCPT_OCC_G=0 at upload turns it off). */
 int mcpt_debug_occ_stats(const mcpt_ctx *ctx, uint64_t *resolved, int32_t *enabled);
-/* k_trace loop profile (diagnostics builds with -DMCPT_TRACE_PROF; returns 0 and zeros otherwise):
- * out12 = {loop trips, refills, node lane-steps, triangle phases, triangle lane-steps, trips with a finish,
- * idle lane-trips, trips with a pop, popping lanes, trips with a non-finite-direction slab, finishing lanes, -}
- * summed over waves since the last reset. */
+/* Ray counts since the last film clear (5 values): extension rays, of them traversed by k_trace
+ * (the rest: NaN / zero directions and root-box misses resolved where the ray was made), any-hit
+ * (shadow + BRDF visibility) rays, of them traversed, and of them resolved by the occluder cache. */
+int mcpt_debug_ray_counts(const mcpt_ctx *ctx, uint64_t *out);
+/* k_trace loop profile of the round-2/3 diagnostics builds, which are gone since round 4 (rocprofv3
+ * counter passes replace them): returns 0, out12 untouched.  Kept so that existing callers link. */
 int mcpt_debug_trace_profile(mcpt_ctx *ctx, uint64_t *out12, int reset);
 /* diagnostics: the kernels' shared-denominator division (mcpt::quot3, mcpt_core.hpp) on the
  * device for n host pairs: out[i] = a[i] / b[i] as the kernels compute it (must equal IEEE fp32). */

@@ -797,4 +797,57 @@ MCPT_HD bool tri_test_t(V3 o, V3 d, V3 p0, V3 e1, V3 e2, float& t) {
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Conservative box culling ("the culling bound").  The reference visits
+// every box the infinite line crosses (Bounds3f.h:114-153) and keeps the smallest accepted t
+// (Triangle.cu:157-202); the traversal skips a box only when no triangle in it can be accepted
+// with t >= 0 (behind the origin) or with t <= t_best (beyond the best hit).  Moller-Trumbore's
+// fp32 expressions (tri_test) can put the accepted point o + t d away from the triangle when the
+// ray grazes it: with det >= 1e-6 as the only guard (Triangle.cu:17-21), the rounding error of
+// the four dot-of-cross products bounds the point's distance from the triangle, per axis, by
+//   w <= omega_T + beta_T |o - p0|,   beta_T = 28.3 u |e1| |e2| / 1e-6 (|d| <= 1 + 2^-10) + 1.01 u,
+//   omega_T = 2.1 u max(|e1|, |e2|)          (u = 2^-24; derivation in DESIGN.md section 5)
+// and |o - p0| <= t |d| + sqrt3 w + diam_T, so on the t range the cull decides about
+//   w <= W'_T + (beta_T / (1 - sqrt3 beta_T)) |d| t,   W'_T = (omega_T + beta_T diam_T) / (1 - sqrt3 beta_T).
+// A box's margin W is the largest W'_T of the triangles under it (+inf when one has sqrt3 beta_T
+// >= 1/2: a triangle so large against the det threshold that nothing near it is ever culled); P
+// is the scene's largest beta_T / (1 - sqrt3 beta_T).  With iota = max_a |1 / d_a| (1 + 2^-18), a
+// box is skipped when
+//   behind:  t1 (1 - 2^-18) + W iota < 0      (only if iota P <= 1: the exit axis is not grazing)
+//   beyond:  t0 - W iota > t_best (1 + 2^-18 + iota P)     (closest hit only)
+// The 2^-18 factors cover every fp32 rounding in the tests themselves (each <= 4u = 2^-22).
+constexpr float kCullSlackF = 1.0f + 1.0f / 262144.0f;  // 1 + 2^-18
+constexpr float kCullBehindF = 1.0f - 1.0f / 262144.0f;  // 1 - 2^-18
+constexpr float kCullNormMax = 1.0f + 1.0f / 512.0f;  // |d|^2 bound of a ray the culls apply to (|d| <= 1 + 2^-10)
+constexpr double kCullU = 5.9604644775390625e-08;      // 2^-24
+constexpr double kCullSlackD = 1.0 + 1.0 / 262144.0;
+// beta_T of a triangle record (e1, e2 as stored: the values tri_test uses)
+MCPT_HD double cull_beta(V3 e1, V3 e2) {
+    const double n1 = __builtin_sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+    const double n2 = __builtin_sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+    return 28.3 * kCullU * n1 * n2 / (double)K_EPSILON * (1.0 + 1.0 / 512.0) + 1.01 * kCullU;
+}
+// true when no box holding the triangle may be culled (sqrt3 beta_T >= 1/2)
+MCPT_HD bool cull_unbounded(double beta) { return !(1.7321 * beta * kCullSlackD < 0.5); }
+// W'_T of a triangle record (+inf when unbounded), in double; far: its contribution to P
+MCPT_HD double cull_tri_margin(V3 e1, V3 e2, double* far) {
+    const double beta = cull_beta(e1, e2);
+    *far = 0.0;
+    if (cull_unbounded(beta)) return __builtin_huge_val();
+    const V3 e3 = v3(e2.x - e1.x, e2.y - e1.y, e2.z - e1.z);
+    const double n1 = __builtin_sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+    const double n2 = __builtin_sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+    const double n3 = __builtin_sqrt((double)e3.x * e3.x + (double)e3.y * e3.y + (double)e3.z * e3.z) * (1.0 + 1e-7);
+    const double diam = n1 > n2 ? (n1 > n3 ? n1 : n3) : (n2 > n3 ? n2 : n3);
+    const double omega = 2.1 * kCullU * (n1 > n2 ? n1 : n2);
+    const double den = 1.0 - 1.7321 * beta * kCullSlackD;
+    *far = beta / den * kCullSlackD * (1.0 + 1.0 / 1048576.0);
+    return (omega + beta * diam * (1.0 + 1e-12)) * kCullSlackD / den;
+}
+// double -> float rounded up (twice 2^-20 covers the conversion's rounding)
+MCPT_HD float cull_to_float_up(double w) {
+    if (!(w < 3.0e38)) return __builtin_huge_valf();
+    return (float)(w * (1.0 + 1.0 / 1048576.0)) * (1.0f + 1.0f / 1048576.0f);
+}
+
 }  // namespace mcpt

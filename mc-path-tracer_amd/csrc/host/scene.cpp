@@ -751,10 +751,10 @@ struct Builder {
     // each a Builder of its own over its disjoint range of info (every decision depends on
     // the range alone, so the tree -- and the flattened arrays -- are identical).  Task
     // nodes are appended afterwards and the cut's child links re-pointed.
-    int build_parallel(int T, int nthreads) {
+    int build_parallel(int start0, int end0, int depth0, int nthreads) {
         struct Task { int start, end, depth, parent, slot; Builder* b; int root; };
         std::vector<Task> tasks;
-        const int grain = std::max(4096, T / (8 * nthreads));
+        const int grain = std::max(4096, (end0 - start0) / (8 * nthreads));
         std::function<int(int, int, int, int, int)> top = [&](int start, int end, int depth, int parent, int slot) -> int {
             max_depth = std::max(max_depth, depth);
             if (end - start <= grain) {
@@ -773,7 +773,7 @@ struct Builder {
             nodes[me].n = 0;
             return me;
         };
-        const int root = top(0, T, 0, -1, 0);
+        const int root = top(start0, end0, depth0, -1, 0);
         std::vector<std::unique_ptr<Builder>> owned;
         for (Task& t : tasks) {
             owned.emplace_back(new Builder(info, max_prims));
@@ -849,7 +849,42 @@ int Scene::build(const mcpt_bvh_params& prm, std::string& err) {
         // MCPT_BVH_THREADS: worker threads for the subtrees (default min(16, cores); 1 = sequential)
         int nth = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
         if (const char* e = std::getenv("MCPT_BVH_THREADS")) nth = std::max(1, std::atoi(e));
-        int root = (T >= 65536 && nth > 1) ? bld.build_parallel((int)T, nth) : bld.build(0, (int)T, 0);
+        // SAH3: triangles whose boxes the traversal may never cull (mcpt_core.hpp cull_unbounded:
+        // large against the det >= 1e-6 threshold, e.g. walls and ground quads) get a subtree of
+        // their own under the root.  Every ancestor of such a triangle is unbounded too, so mixed
+        // into the tree they would keep whole subtrees of small triangles from being culled
+        // (config 2's ten wall triangles sat under 7 interior nodes).  MCPT_BVH_ISOLATE=0: off.
+        int nbig = 0;
+        if (bld.mode == 1) {
+            const char* iso = std::getenv("MCPT_BVH_ISOLATE");
+            if (!(iso && iso[0] == '0' && iso[1] == 0)) {
+                auto unbounded = [&](const PrimInfo& p) {
+                    const V3* P = tris[(size_t)p.prim].p;
+                    const V3 e1 = P[1] - P[0], e2 = P[2] - P[0];  // as the triangle record stores them
+                    return mcpt::cull_unbounded(mcpt::cull_beta(e1, e2));
+                };
+                auto it = std::stable_partition(info.begin(), info.end(), unbounded);
+                nbig = (int)(it - info.begin());
+                if (nbig == (int)T) nbig = 0;  // every triangle unbounded: nothing to isolate
+            }
+        }
+        auto sub = [&](int start, int end, int depth) {
+            return (end - start >= 65536 && nth > 1) ? bld.build_parallel(start, end, depth, nth) : bld.build(start, end, depth);
+        };
+        int root;
+        if (nbig > 0) {
+            root = (int)bld.nodes.size();
+            bld.nodes.push_back(BuildNode());
+            const int c0 = sub(0, nbig, 1), c1 = sub(nbig, (int)T, 1);
+            bld.nodes[root].child[0] = c0;
+            bld.nodes[root].child[1] = c1;
+            bld.nodes[root].b = bld.nodes[c0].b;
+            bld.nodes[root].b.add(bld.nodes[c1].b);
+            bld.nodes[root].n = 0;
+            bld.max_depth = std::max(bld.max_depth, 1);
+        } else {
+            root = sub(0, (int)T, 0);
+        }
         bvh_depth = bld.max_depth;
         // flatten_tree (BVH.cu:312-333): depth-first, first child adjacent.
         std::function<int(int)> flatten = [&](int ni) -> int {

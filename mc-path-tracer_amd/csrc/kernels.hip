@@ -113,12 +113,33 @@ __device__ inline bool slab(float mnx, float mny, float mnz, float mxx, float mx
     t1 = (tzmax < b) ? tzmax : b;
     return !miss;
 }
-constexpr float kCullAbs = 1e-5f;
-constexpr float kCullRel = 1.0f / 256.0f;
 constexpr float K_INF_F = __builtin_huge_valf();
 constexpr int kEnd = -1;  // not a valid leaf: offset + count <= ntri < 2^24
 
-__device__ inline bool keep_box(float t0, float t1, float cut) { return !(t1 < -kCullAbs) && !(t0 > cut); }
+// Culling scale of a ray (mcpt_core.hpp "conservative box culling"): iota = max_a |1/d_a| (1 + 2^-18)
+// for the rays the bound covers -- finite inverse, |d| <= 1 + 2^-10, a scene whose boxes contain
+// their triangles.  The sign says whether the behind cut applies: +iota when iota P <= 1 (no
+// direction component below P |d|), -iota when not.  Rays the bound does not cover get -FLT_MAX:
+// W iota is then beyond every t for any box holding a triangle that can be accepted at all (det
+// >= 1e-6 needs |e1| |e2| |d| >= 1e-6, so such a box has W > 1e-9), i.e. nothing is culled.  A
+// ray with an infinite inverse component gets -inf (it takes slab(): |iota| = inf is the test).
+// One register per ray holds all of it.
+__device__ inline float cull_iota(const DevScene& sc, V3 d, V3 inv) {
+    const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
+    if (!(ax < K_INF_F && ay < K_INF_F && az < K_INF_F)) return -K_INF_F;
+    const float n2 = d.x * d.x + d.y * d.y + d.z * d.z;
+    if (!sc.cull_ok || !(n2 <= kCullNormMax)) return -3.4028235e38f;
+    const float io = __builtin_fmaxf(__builtin_fmaxf(ax, ay), az) * kCullSlackF;
+    return io * sc.cull_p <= 1.f ? io : -io;
+}
+// The cull of a box whose slab test passed, with m = W iota (W: the box's margin, iota signed as
+// cull_iota returns it).  key = t0 - |m|: no triangle in the box can be accepted with t below it,
+// so it orders the stack and is re-tested against the cut on pop.  The behind cut needs m >= 0 (a
+// NaN m, from W = 0 with iota = inf, culls nothing).  Any-hit rays pass cut = +inf.
+__device__ inline bool keep_box(float t0, float t1, float m, float cut, float& key) {
+    key = t0 - __builtin_fabsf(m);
+    return !(m >= 0.f && __builtin_fmaf(t1, kCullBehindF, m) < 0.f) && !(key > cut);
+}
 
 // Both child boxes of a pair node at once, for rays whose inverse direction is
 // finite in all three components (then no slab product can be NaN).  The six
@@ -179,10 +200,11 @@ __device__ inline bool ray_misses_scene(const DevScene& sc, V3 o, V3 d) {
         o.z >= sc.root_mn[2] && o.z <= sc.root_mx[2])
         return false;
     const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-    float t0, t1;
-    const float cut = K_HUGE + K_HUGE * kCullRel;
+    const float m = sc.root_w * cull_iota(sc, d, inv);
+    float t0, t1, key;
     return !(slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1], sc.root_mx[2], o, inv,
-                  inv.x < 0.f, inv.y < 0.f, inv.z < 0.f, t0, t1) && keep_box(t0, t1, cut));
+                  inv.x < 0.f, inv.y < 0.f, inv.z < 0.f, t0, t1) &&
+             keep_box(t0, t1, m, K_INF_F, key));
 }
 
 // Hit record of ray (o, d) on triangle tri, as dTriangle::hit builds it
@@ -251,8 +273,10 @@ __device__ inline uint32_t occ_index(const DevScene& sc, V3 o, V3 d) {
     return ((((cz * G + cy) * G + cx) * 6u + face) * B + ub) * B + vb;
 }
 
-// true: (o, d) (reciprocal inv, all finite) is occluded by triangle record w0..w2 under its leaf box
-__device__ inline bool occ_test(V3 o, V3 d, V3 inv, float4 bmn, float4 bmx, float4 w0, float4 w1, float4 w2) {
+// true: (o, d) (reciprocal inv, all finite; signed culling scale io) is occluded by triangle record
+// w0..w2 under its leaf box (bmn.w: the leaf's margin)
+__device__ inline bool occ_test(V3 o, V3 d, V3 inv, float io, float4 bmn, float4 bmx, float4 w0, float4 w1,
+                                float4 w2) {
     // pair_slab's arithmetic for one box (its first lane)
     const float ax = (bmn.x - o.x) * inv.x, bx = (bmx.x - o.x) * inv.x;
     const float ay = (bmn.y - o.y) * inv.y, by = (bmx.y - o.y) * inv.y;
@@ -261,9 +285,8 @@ __device__ inline bool occ_test(V3 o, V3 d, V3 inv, float4 bmn, float4 bmx, floa
                                      __builtin_fminf(az, bz));
     const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by)),
                                      __builtin_fmaxf(az, bz));
-    const float best = K_HUGE;
-    const float cut = best + best * kCullRel;  // an any-hit ray's cut in k_trace
-    if (!(t0 <= t1) || !keep_box(t0, t1, cut)) return false;
+    float key;
+    if (!(t0 <= t1) || !keep_box(t0, t1, bmn.w * io, K_INF_F, key)) return false;  // k_trace's any-hit cull
     float th;
     return tri_test_t(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), th) && !(th < 0.f) &&
            th < K_HUGE;
@@ -293,10 +316,11 @@ __device__ inline void occ_hit2(const DevScene& sc, V3 ol, V3 dl, uint2 el, V3 o
     const V3 il = v3(1.f / dl.x, 1.f / dl.y, 1.f / dl.z), ib = v3(1.f / db.x, 1.f / db.y, 1.f / db.z);  // k_trace's
     const bool fl = __builtin_fabsf(il.x) < K_INF_F && __builtin_fabsf(il.y) < K_INF_F && __builtin_fabsf(il.z) < K_INF_F;
     const bool fb = __builtin_fabsf(ib.x) < K_INF_F && __builtin_fabsf(ib.y) < K_INF_F && __builtin_fabsf(ib.z) < K_INF_F;
-    hl = fl && ((v0 && occ_test(ol, dl, il, bn[0], bx[0], r0[0], r1[0], r2[0])) ||
-                (v1 && occ_test(ol, dl, il, bn[1], bx[1], r0[1], r1[1], r2[1])));
-    hb = fb && ((v2 && occ_test(ob, db, ib, bn[2], bx[2], r0[2], r1[2], r2[2])) ||
-                (v3_ && occ_test(ob, db, ib, bn[3], bx[3], r0[3], r1[3], r2[3])));
+    const float iol = cull_iota(sc, dl, il), iob = cull_iota(sc, db, ib);
+    hl = fl && ((v0 && occ_test(ol, dl, il, iol, bn[0], bx[0], r0[0], r1[0], r2[0])) ||
+                (v1 && occ_test(ol, dl, il, iol, bn[1], bx[1], r0[1], r1[1], r2[1])));
+    hb = fb && ((v2 && occ_test(ob, db, ib, iob, bn[2], bx[2], r0[2], r1[2], r2[2])) ||
+                (v3_ && occ_test(ob, db, ib, iob, bn[3], bx[3], r0[3], r1[3], r2[3])));
 }
 
 // ---------------------------------------------------------------------------
@@ -313,25 +337,6 @@ __device__ inline void occ_hit2(const DevScene& sc, V3 ol, V3 dl, uint2 el, V3 o
 // Per path the arithmetic is the reference's, so which thread evaluates a path
 // does not change any result.
 // ---------------------------------------------------------------------------
-// Optional section profile of k_shade (diagnostics build, -DMCPT_SHADE_PROF): per
-// wave, the s_memtime cycles between section marks, summed per block in LDS and
-// folded into 64 shards of g_trace_prof (read back with mcpt_debug_trace_profile).
-#ifdef MCPT_SHADE_PROF
-__device__ unsigned long long g_trace_prof[64 * 12];
-__shared__ unsigned long long s_sprof[kBlock / 64][12];
-#define SPROF_T0() unsigned long long _sp_t = __builtin_readcyclecounter()
-#define SPROF(i)                                                                             \
-    do {                                                                                     \
-        const unsigned long long _n = __builtin_readcyclecounter();                          \
-        if ((threadIdx.x & 63) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1))           \
-            s_sprof[threadIdx.x >> 6][i] += _n - _sp_t;                                      \
-        _sp_t = _n;                                                                          \
-    } while (0)
-#else
-#define SPROF_T0() ((void)0)
-#define SPROF(i) ((void)0)
-#endif
-
 struct MatOut {
     bool want_ext, want_l, want_b, trivial_ext, vis_ray;
     uint32_t trivial_any;
@@ -351,7 +356,6 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
     const DevScene& sc = a.scene;
     const uint2 none = make_uint2(kOccEmpty, kOccEmpty);
     MatOut mo{false, false, false, false, false, 0u, none, none};
-    SPROF_T0();
     // path slot -> pixel; the sample index comes with the record (k_shade: slot k of a pixel
     // runs samples k, k + S, k + 2S, ...)
     const uint32_t npix = (uint32_t)a.W * (uint32_t)a.H;
@@ -364,7 +368,6 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
     hit_record(sc, ro, rdir, htri, pos, n, mat, t_hit);
     const V3 wo = -rdir;
     const Mat m = load_mat(sc.mats + 8 * mat);
-    SPROF(3);
     // The three parts of wf_mat_mix draw from disjoint RNG slots and share only the hit
     // record, so they are evaluated in the order that lets each store its results at
     // once (short register live ranges): the continuation first (:353-358, its ratio
@@ -390,7 +393,6 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
             mo.trivial_ext = true;
         }
     }
-    SPROF(4);
     int l_id = (int)(r(SL_LIGHT) * (float)(sc.nlights - 0) + (float)0);
     const int light_id = (l_id == sc.nlights) ? 0 : l_id;
     const bool delta = light_id > 0;
@@ -440,7 +442,6 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
             if (occ_on) mo.el = occ_entry(sc, so_l, ldir);
         }
     }
-    SPROF(5);
     V3 cB = v3(0.f, 0.f, 0.f);
     if (!delta) {
         V3 wi_b = brdf_sample_wi<FIXED>(m, n, wo, r, SL_MAT_E0, r(SL_MAT_LOBE) < 0.5f);  // spec : diff
@@ -469,7 +470,6 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
     }
     a.p.nee1[pid] = f4(cB, rr.z);
     a.p.flags[pid] = nf | ((len + 1) << F_LEN_SHIFT) | (sidx << F_SIDX_SHIFT);  // extend increments len (:270)
-    SPROF(6);
     return mo;
 }
 
@@ -508,12 +508,6 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         if (a.blk_done[done_idx]) return;
     }
     const int lane = threadIdx.x & 63;
-#ifdef MCPT_SHADE_PROF
-    const int wave = threadIdx.x >> 6;
-    if (threadIdx.x < kBlock / 64 * 12) s_sprof[threadIdx.x / 12][threadIdx.x % 12] = 0;
-    __syncthreads();
-#endif
-    SPROF_T0();
     bool valid = tile < a.ntiles && li < tile_px;
     uint32_t pid = 0, pix = 0;  // path id (slot * pixels + pixel) and pixel id
     int x = 0, y = 0;
@@ -627,7 +621,6 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         }
         uint32_t nflags = fl;
         if (dead) nflags = F_DEAD;
-        SPROF(0);
         if (dead && sidx < spp) {  // :219-222 + wf_generate (:225-251)
             const Rng r0{rng_key(a.seed, pix, sidx), 0u};
             V3 new_o, new_d;
@@ -646,7 +639,6 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         if (!cont && nflags != fl) a.p.flags[pid] = nflags;  // continuing paths: written by material()
         finished = dead && !(sidx < spp);
     }
-    SPROF(1);
     // ---- pushes: generated extension rays and continuing paths (material queue); one
     // atomic per block and queue.  A continuing path's record and updated throughput go
     // to k_material densely (it writes p.beta with f_s/pdf_s in .w).
@@ -676,19 +668,6 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             a.p.Ld[pid] = f4(film, 0.f);
     }
     if (a.blk_done && __syncthreads_and(finished ? 1 : 0) && threadIdx.x == 0) a.blk_done[done_idx] = 1;
-#ifdef MCPT_SHADE_PROF
-    {
-        unsigned long long _n = __builtin_readcyclecounter();
-        _sp_t = _n - _sp_t;  // pushes + statistics
-        if (lane == 0) { s_sprof[wave][2] += _sp_t; s_sprof[wave][11] += 1; }
-        __syncthreads();
-        if (threadIdx.x < 12) {
-            unsigned long long v = 0;
-            for (int w = 0; w < kBlock / 64; w++) v += s_sprof[w][threadIdx.x];
-            atomicAdd(&g_trace_prof[(blockIdx.x % 64) * 12 + threadIdx.x], v);
-        }
-    }
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -705,11 +684,6 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
     uint32_t* sc_ctr = a.cnt->shard[shard];
     const uint32_t n = sc_ctr[C_MAT];
     const int lane = threadIdx.x & 63;
-#ifdef MCPT_SHADE_PROF
-    if (threadIdx.x < kBlock / 64 * 12) s_sprof[threadIdx.x / 12][threadIdx.x % 12] = 0;
-    __syncthreads();
-    unsigned long long _t_mat = __builtin_readcyclecounter();
-#endif
     uint32_t n_ext = 0, n_any = 0, n_vis = 0, n_occ = 0, occ_try = 0;
     const bool occ_on = a.scene.occ && a.scene.occ_gate[0] == 0;  // see DevScene::occ_gate
     // Any-hit rays are staged here (light ray o/d, BRDF visibility ray o/d) and stored after
@@ -727,9 +701,6 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
             const float4 b4 = a.mat_beta[shard * a.ext_cap + i];
             mpid = q.x;
             mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w, &s_any[0][0], occ_on);
-#ifdef MCPT_SHADE_PROF
-            unsigned long long _sp_t = __builtin_readcyclecounter();
-#endif
             // the occluder cache (see occ_hit2), after the path's shading state is dead: a ray it
             // resolves gets its wf_shadow result here and is not queued
             if (occ_on) {
@@ -750,11 +721,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
                     mo.trivial_any++;
                 }
             }
-            SPROF(7);  // occluder-cache lookups
         }
-#ifdef MCPT_SHADE_PROF
-        unsigned long long _t_push = __builtin_readcyclecounter();
-#endif
         bool want[3] = {mo.want_ext, mo.want_l, mo.want_b};
         uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
         uint32_t slot[3], total[3];
@@ -780,9 +747,6 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
         n_any += (uint32_t)(__popcll(__ballot(mo.want_l)) + __popcll(__ballot(mo.want_b)) +
                             __popcll(__ballot(mo.trivial_any >= 1u)) + __popcll(__ballot(mo.trivial_any >= 2u)));
         n_vis += (uint32_t)__popcll(__ballot(mo.vis_ray));
-#ifdef MCPT_SHADE_PROF
-        if (lane == 0) s_sprof[threadIdx.x >> 6][9] += __builtin_readcyclecounter() - _t_push;  // pushes + stores
-#endif
     }
     if (lane == 0) {
         if (n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
@@ -791,30 +755,18 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
         if (n_occ) atomicAdd(sc_ctr + C_OCC, n_occ);
         if (occ_try) atomicAdd(sc_ctr + C_OCC_TRY, occ_try);
     }
-#ifdef MCPT_SHADE_PROF
-    {
-        const int wave = threadIdx.x >> 6;
-        const unsigned long long _n = __builtin_readcyclecounter();
-        if (lane == 0) { s_sprof[wave][8] += _n - _t_mat; s_sprof[wave][10] += 1; }
-        __syncthreads();
-        if (threadIdx.x < 12) {
-            unsigned long long v = 0;
-            for (int w = 0; w < (int)(blockDim.x >> 6); w++) v += s_sprof[w][threadIdx.x];
-            atomicAdd(&g_trace_prof[(blockIdx.x % 64) * 12 + threadIdx.x], v);
-        }
-    }
-#endif
 }
 
 // ---------------------------------------------------------------------------
 // BVH traversal (BVH.cu:115-207 closest hit, Triangle.cu:157-205 any hit).
 // Child-pair nodes (both child boxes in the parent, 64 B) with the reference's
 // slab arithmetic per box (Bounds3f.h:121-153).  Culling beyond the reference
-// (which visits every box the infinite line crosses) is conservative: a box is
-// skipped only when it lies entirely behind the origin or starts more than
-// 2^-8 * t_best past the current best hit, so the result is unchanged unless a
-// triangle's Moller-Trumbore t error exceeded that margin.  Ties on t go to the
-// lower triangle index, so the visit order is free (near child first here).
+// (which visits every box the infinite line crosses) is provably conservative: a box
+// is skipped only when no triangle in it can be accepted with t >= 0 or below the
+// best t, for any angle between the ray and the triangle, by the Moller-Trumbore
+// error bound of mcpt_core.hpp ("conservative box culling": each child carries its
+// margin W, keep_box).  Ties on t go to the lower triangle index, so the visit order
+// is free (near child first here, by the cull key t0 - W iota).
 //
 // One persistent kernel traces both ray sets of an iteration: set 0 closest hit
 // (extension rays -> hit_tri), set 1 any hit (light and BRDF visibility rays ->
@@ -860,15 +812,6 @@ __device__ inline void wave_stats(uint32_t* stats, int lane, uint32_t nodes, uin
     }
 }
 
-// Optional loop profile of k_trace (diagnostics build, -DMCPT_TRACE_PROF): per
-// launch sums of wave-level events, read back with mcpt_debug_trace_profile().
-#ifdef MCPT_TRACE_PROF
-__device__ unsigned long long g_trace_prof[12];
-#define PROF_ADD(i, v) (prof[i] += (v))
-#else
-#define PROF_ADD(i, v) ((void)0)
-#endif
-
 #ifndef MCPT_NODE_STEPS
 #define MCPT_NODE_STEPS 4
 #endif
@@ -885,14 +828,15 @@ constexpr int kGrabMax = MCPT_GRAB_MAX;  // rays one hand-out atomic may reserve
 #endif
 constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
 
-// Waves per SIMD: 8 (<= 64 VGPRs) for child pairs with the 8-entry LDS stack, 7 (<= 72) with
-// the deep stack (the 8-wave build falls back to 6 there), 6 (80) for 4-wide nodes (8 float4
-// of node data per step).  The attribute lets the register allocator park the partition
-// scan's loop-invariant lane addresses (and a few scalars) in scratch -- reloaded only by
-// the scan -- instead of giving up a wave.  Config 2 k_trace 0.777 -> 0.758 ms at 8 waves
-// (32 per CU) against 7 (interleaved runs on one box).
+// Waves per SIMD: 7 (<= 72 VGPRs) for child pairs with either LDS stack, 6 (80) for 4-wide nodes
+// (8 float4 of node data per step).  The attribute lets the register allocator park the
+// partition scan's loop-invariant lane addresses (and a few scalars) in scratch -- reloaded only
+// by the scan -- instead of giving up a wave.  Round 2 ran the pair kernel at 8 waves (64 VGPRs:
+// config 2 0.758 ms against 0.777 at 7); the culling bound's per-ray scale (cull_iota, round 4)
+// is one register too many there: 8 spilled VGPRs in the loop, config 2 2.74 against 2.52 ms
+// per launch at 7 (interleaved, one box).
 #ifndef MCPT_TRACE_WPE
-#define MCPT_TRACE_WPE 8
+#define MCPT_TRACE_WPE 7
 #endif
 #ifndef MCPT_TRACE_WPE_DEEP
 #define MCPT_TRACE_WPE_DEEP 7
@@ -904,15 +848,9 @@ constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
     ((kW) == 4 ? MCPT_TRACE_WPE4 : ((kS) > ::mcpt_dev::kLdsStack ? MCPT_TRACE_WPE_DEEP : MCPT_TRACE_WPE))
 #define MCPT_TRACE_ATTR \
     __attribute__((amdgpu_waves_per_eu(MCPT_TRACE_WPE_OF(kW, kLdsStack), MCPT_TRACE_WPE_OF(kW, kLdsStack))))
-#ifdef MCPT_WAVE_TIMES
-__device__ unsigned long long g_wave_t[4 * 16384];  // per wave: s_memrealtime (100 MHz, chip-wide) at entry and
-                                                     // exit, partition, time its partition ran dry for it
-#endif
-template <int kW, int kLdsStack>  // node width (2: child pairs, 4: quads), LDS stack entries per lane
+// node width (2: child pairs, 4: quads), LDS stack entries per lane, work counters (TraceSet::stats)
+template <int kW, int kLdsStack, bool kCount>
 __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs a) {
-#ifdef MCPT_WAVE_TIMES
-    if (threadIdx.x == 0 && blockIdx.x < 16384) g_wave_t[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
     if (a.idle && *a.idle) return;  // the tile set is complete
     __shared__ int2 stk[kLdsStack][kTraceBlock];
     const int lane = threadIdx.x;
@@ -1002,41 +940,27 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     // the iteration before the next lookups (DevScene::occ_gate)
     const bool occ_rec = sc.occ && sc.occ_gate[0] <= 1u;
 
-    // per-lane work counters (wave-reduced at exit): tot_* count every node step, triangle
+    // Work counters (only the kCount instantiation: six long-lived per-lane registers cost the
+    // 64-VGPR, 8-wave kernel its spill-free hot loop).  tot_* count every node step, triangle
     // test and hit; the any-hit set's share is attributed per ray (tot_n1 -= tot_n when an
-    // any-hit ray starts, += when it finishes), so a step costs one add instead of a
-    // kind-selected add per set.  Per-ray step counts only in diagnostics builds
-    // (MCPT_RAY_STEPS).
+    // any-hit ray starts, += when it finishes), so a step costs one add.
     uint32_t tot_n = 0, tot_t = 0, tot_h = 0, tot_n1 = 0, tot_t1 = 0, tot_h1 = 0;
-#ifdef MCPT_RAY_STEPS
-    uint32_t rn = 0, rt = 0;
-#define RAY_STEP_NODE() (rn++)
-#define RAY_STEP_TRI() (rt++)
-#else
-#define RAY_STEP_NODE() ((void)0)
-#define RAY_STEP_TRI() ((void)0)
-#endif
-#ifdef MCPT_TRACE_PROF
-    uint64_t prof[12] = {};  // see mcpt_debug_trace_profile
-#endif
     uint64_t drained = 0;  // partitions this wave saw run dry (by an atomic: never stale)
     for (;;) {  // one trip per partition joined
     // Per-lane ray state is declared per partition trip: when the trip ends no lane holds a
     // ray, so none of it is live across the partition scan below (VGPR budget).
     uint32_t buf_lo = 0, buf_hi = 0, last_p = 0;  // wave-uniform reservation of the partition (refill)
     bool act = false;
-    int kind = 0;  // 0 closest, 1 any
     uint32_t rid = 0;
-#ifdef MCPT_RAY_STEPS
-    uint32_t qi = 0;
-#endif
     V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
     int ref = kEnd, leaf = kEnd, sp = 0, tri = -1;
-    bool fin = true;  // inverse direction finite: pair_slab() is exact
-    float best = K_HUGE, cut = K_HUGE;
+    // best: the closest hit's t, or -1 for an any-hit ray (its kind: best < 0; an accepted t is never
+    // below +-0); io: the ray's signed culling scale (cull_iota; |io| = inf: an infinite inverse
+    // component, the slab() path)
+    float best = K_HUGE, cut = K_HUGE, io = K_INF_F;
     int2 spill[kMaxStack - kLdsStack];
     // Pop the next entry still in front of the current cut (any-hit rays keep
-    // cut = K_HUGE * (1 + 2^-8), so for them every entry is taken).
+    // cut = +inf, so for them every entry is taken).
     auto pop = [&]() -> int {
         while (sp > 0) {
             sp--;
@@ -1053,16 +977,15 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         return kEnd;
     };
     auto finish = [&]() {
-        tot_h += tri >= 0 ? 1u : 0u;
-        if (kind) {
-            tot_n1 += tot_n;
-            tot_t1 += tot_t;
-            tot_h1 += tri >= 0 ? 1u : 0u;
+        const bool kind = best < 0.f;
+        if constexpr (kCount) {
+            tot_h += tri >= 0 ? 1u : 0u;
+            if (kind) {
+                tot_n1 += tot_n;
+                tot_t1 += tot_t;
+                tot_h1 += tri >= 0 ? 1u : 0u;
+            }
         }
-#ifdef MCPT_RAY_STEPS
-        uint32_t* rs = kind ? a.set[1].ray_steps : a.set[0].ray_steps;
-        if (rs) rs[qi] = rn + rt;
-#endif
         if (kind) {
             a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
             if (tri >= 0 && occ_rec)  // the cell's occluder (occ_hit2)
@@ -1073,14 +996,10 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         act = false;
     };
     for (;;) {
-        PROF_ADD(0, 1);
         // ---- refill idle lanes with the partition's next rays
         const uint64_t idle = __ballot(!act);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if ((more || buf_lo < buf_hi) && (nidle >= a.refill_min || nidle == 64u)) {
-#ifdef MCPT_TRACE_PROF
-            const uint64_t _rf_t0 = __builtin_readcyclecounter();
-#endif
             // Positions come from a per-wave reservation [buf_lo, buf_hi) of the partition,
             // refilled by one atomic when empty.  By default (kGrabMax 0) an atomic reserves
             // exactly the idle lanes' rays.  Reserving more (a share of what is left, up to
@@ -1121,7 +1040,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     uint32_t my_e = e0;
                     while (pos >= s_pre[my_e + 1]) my_e++;  // the grab spans entries (rarely a step)
                     const uint32_t my_pre = s_pre[my_e];
-                    kind = kAnyFirst ? my_e < spart : my_e >= spart;
+                    const bool kind = kAnyFirst ? my_e < spart : my_e >= spart;
                     const uint32_t sh = part + (my_e >= spart ? my_e - spart : my_e) * nparts;
                     const uint32_t qslot = sh * (kind ? a.set[1].shard_cap : a.set[0].shard_cap) + (pos - my_pre);
                     // select the set's fields with ternaries: indexing a.set[kind] with a
@@ -1129,9 +1048,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     const uint32_t* qp = kind ? a.set[1].queue : a.set[0].queue;
                     const float4* rop = kind ? a.set[1].ro : a.set[0].ro;
                     const float4* rdp = kind ? a.set[1].rd : a.set[0].rd;
-#ifdef MCPT_RAY_STEPS
-                    qi = qslot;
-#endif
                     // a dense set (ray_at_slot: the any-hit rays k_material stores at their queue
                     // positions) issues its ray loads with the queue-entry load, not after it
                     const bool at_slot = kind ? a.set[1].ray_at_slot : a.set[0].ray_at_slot;
@@ -1140,20 +1056,17 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     if (at_slot && qp) rid = qp[qslot];  // the result index, needed only when the ray finishes
                     o = xyz(o4);
                     d = xyz(d4);
-#ifdef MCPT_RAY_STEPS
-                    rn = 0;
-                    rt = 0;
-#endif
                     tri = -1;
-                    best = K_HUGE;
-                    cut = best + best * kCullRel;
+                    best = kind ? -1.f : K_HUGE;
+                    if constexpr (kCount) {
+                        if (kind) {  // the any-hit set's counts start here (see tot_n)
+                            tot_n1 -= tot_n;
+                            tot_t1 -= tot_t;
+                        }
+                    }
                     sp = 0;
                     leaf = kEnd;
                     act = true;
-                    if (kind) {  // the any-hit set's counts start here (see tot_n)
-                        tot_n1 -= tot_n;
-                        tot_t1 -= tot_t;
-                    }
                     const bool pre = kind ? a.set[1].prefiltered : a.set[0].prefiltered;
                     // NaN / zero direction: a miss / visible
                     if (!pre &&
@@ -1161,32 +1074,21 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                         finish();
                     } else {
                         inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-                        fin = __builtin_fabsf(inv.x) < K_INF_F && __builtin_fabsf(inv.y) < K_INF_F &&
-                              __builtin_fabsf(inv.z) < K_INF_F;
-                        float t0, t1;
+                        io = cull_iota(sc, d, inv);
+                        cut = kind ? K_INF_F : best * __builtin_fmaf(__builtin_fabsf(io), sc.cull_p, kCullSlackF);
+                        float t0, t1, key;
                         // (k_shade resolved the rays that miss the root box in place, so the
                         // queued sets skip this test: same outcome, ray_misses_scene())
                         if (!pre && (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0],
                                            sc.root_mx[1], sc.root_mx[2], o, inv, inv.x < 0.f, inv.y < 0.f, inv.z < 0.f,
                                            t0, t1) ||
-                                     !keep_box(t0, t1, cut)))
+                                     !keep_box(t0, t1, sc.root_w * io, cut, key)))
                             finish();
                         else
                             ref = sc.root_ref;
                     }
                 }
             }
-#ifdef MCPT_WAVE_TIMES
-            if (!more && lane == 0 && blockIdx.x < 16384) g_wave_t[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef MCPT_TRACE_PROF
-            {   // refill latency: atomic, queue entry and ray loads until the new lanes are set up
-                float _sink = inv.x + o.x;
-                __asm__ volatile("" :: "v"(_sink));
-                PROF_ADD(11, __builtin_readcyclecounter() - _rf_t0);
-            }
-#endif
-            PROF_ADD(1, 1);
         }
         if (__ballot(act) == 0) {
             if (!more && buf_lo >= buf_hi) break;  // partition drained, every lane idle
@@ -1199,17 +1101,17 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
           for (int it = 0; it < kNodeSteps; it++) {
             bool need_pop = false;
             if (ref >= 0) {
-              RAY_STEP_NODE();
-              tot_n++;
+              if constexpr (kCount) tot_n++;
               const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;  // slow-path slab only
               if constexpr (kW == 4) {
                 // 4-wide node: test the four child boxes, visit the nearest hit, push the
                 // other hits far-to-near with their entry t (popped nearest-first)
                 const float4* nd = sc.nodes + 8 * ref;
                 const float4 mnx = nd[0], mxx = nd[1], mny = nd[2], mxy = nd[3], mnz = nd[4], mxz = nd[5], rf = nd[6];
+                const float4 wq = nd[7];  // the children's margins
                 float t0[4], t1[4];
                 bool hk[4];
-                if (fin) {
+                if (__builtin_fabsf(io) < K_INF_F) {  // finite inverse: pair arithmetic
                     quad_axis(mnx, mxx, o.x, inv.x, t0, t1, true);
                     quad_axis(mny, mxy, o.y, inv.y, t0, t1, false);
                     quad_axis(mnz, mxz, o.z, inv.z, t0, t1, false);
@@ -1225,13 +1127,16 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                                      t1[k]);
                 }
                 int rr[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+                const float wk[4] = {wq.x, wq.y, wq.z, wq.w};
                 float key[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const bool h = hk[k] && rr[k] != kEnd && keep_box(t0[k], t1[k], cut);
-                    // sort key: entry t (a NaN entry from the NaN-passing slab sorts first and
-                    // is never culled on pop), misses last
-                    key[k] = h ? (t0[k] == t0[k] ? t0[k] : -K_INF_F) : K_INF_F;
+                    float ck;
+                    const bool kb = keep_box(t0[k], t1[k], wk[k] * io, cut, ck);
+                    const bool h = hk[k] && rr[k] != kEnd && kb;
+                    // sort key: the cull key t0 - W iota (a NaN key from the NaN-passing slab sorts
+                    // first and is never culled on pop), misses last
+                    key[k] = h ? (ck == ck ? ck : -K_INF_F) : K_INF_F;
                     rr[k] = h ? rr[k] : kEnd;
                 }
 #define MCPT_CAS(i, j)                                                   \
@@ -1260,8 +1165,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 float a0, b0, a1, b1;
                 bool h0, h1;
                 // node layout (SoA pairs): q0 = (mn.x, mn.x', mx.x, mx.x'), q1 = y, q2 = z,
-                // q3 = (child ref, child ref', axis, -); unprimed = first child
-                if (fin) {
+                // q3 = (child ref, child ref', margin, margin'); unprimed = first child
+                if (__builtin_fabsf(io) < K_INF_F) {  // finite inverse: pair arithmetic
                     pair_slab(q0, q1, q2, o, inv, a0, b0, a1, b1);
                     h0 = a0 <= b0;
                     h1 = a1 <= b1;
@@ -1269,13 +1174,19 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     h0 = slab(q0.x, q1.x, q2.x, q0.z, q1.z, q2.z, o, inv, nx, ny, nz, a0, b0);
                     h1 = slab(q0.y, q1.y, q2.y, q0.w, q1.w, q2.w, o, inv, nx, ny, nz, a1, b1);
                 }
-                h0 = h0 && keep_box(a0, b0, cut);
-                h1 = h1 && keep_box(a1, b1, cut);
+                // the children's margins ride in q3.z / q3.w (see keep_box)
+                // (evaluated unconditionally: a key assigned only under h0 / h1 costs the
+                // allocator a live range per step -- 7 -> 23 spilled VGPRs)
+                float k0, k1;
+                const bool kb0 = keep_box(a0, b0, q3.z * io, cut, k0);
+                const bool kb1 = keep_box(a1, b1, q3.w * io, cut, k1);
+                h0 = h0 && kb0;
+                h1 = h1 && kb1;
                 const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
                 need_pop = !(h0 | h1);
                 if (h0 && h1) {
-                    const bool first0 = !(a1 < a0);
-                    const int2 e = make_int2(first0 ? c1 : c0, __float_as_int(first0 ? a1 : a0));
+                    const bool first0 = !(k1 < k0);
+                    const int2 e = make_int2(first0 ? c1 : c0, __float_as_int(first0 ? k1 : k0));
                     if (sp < kLdsStack) stk[sp][lane] = e;
                     else spill[sp - kLdsStack] = e;
                     sp++;
@@ -1291,11 +1202,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 leaf = ref;
                 need_pop = true;
             }
-#ifdef MCPT_TRACE_PROF
-            PROF_ADD(7, __ballot(need_pop) != 0);
-            PROF_ADD(8, (uint32_t)__popcll(__ballot(need_pop)));
-            PROF_ADD(9, __ballot(!fin && ref >= 0) != 0);
-#endif
             if (need_pop) ref = pop();
             if (ref < 0) break;  // parked-leaf slot full or traversal done: wait for the triangle phase
           }
@@ -1304,12 +1210,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         // leaf, or no lane has node work left, each parked leaf tests one triangle
         const uint32_t n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
         const uint32_t n_node = (uint32_t)__popcll(__ballot(act && ref >= 0));
-        PROF_ADD(2, n_node);
-        PROF_ADD(6, (uint32_t)__popcll(__ballot(!act)));
         if (n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node)) {
-            PROF_ADD(3, 1);
-            PROF_ADD(4, n_tri);
             if (leaf != kEnd) {
+                if constexpr (kCount) tot_t++;
                 const int id = leaf & 0xffffff;
                 const float4* tp = sc.tri + kTriF4 * id;
                 const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
@@ -1318,16 +1221,14 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 // for a second, dependent fetch of the same record.
                 __asm__ volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z),
                                  "v"(w1.w), "v"(w2.x), "v"(w2.y));
-                RAY_STEP_TRI();
-                tot_t++;
                 float t;
                 bool done = false;
                 if (tri_test_t(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t) &&
                     !(t < 0.f) &&
-                    (kind ? t < K_HUGE
+                    (best < 0.f ? t < K_HUGE
                           : (t < best ||
                              (t == best && tri >= 0 && __float_as_int(w2.y) < __float_as_int(sc.tri[kTriF4 * tri + 2].y))))) {
-                    if (kind) {
+                    if (best < 0.f) {
                         tri = id;  // occluded (tmax 1e32)
                         done = true;
                     } else {
@@ -1335,7 +1236,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                         // third float4), whatever order the BVH build stored triangles in
                         best = t;
                         tri = id;
-                        cut = best + best * kCullRel;
+                        cut = best * __builtin_fmaf(__builtin_fabsf(io), sc.cull_p, kCullSlackF);
                     }
                 }
                 if (done) {  // any hit: drop the rest of the traversal
@@ -1346,10 +1247,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 }
             }
         }
-#ifdef MCPT_TRACE_PROF
-        PROF_ADD(5, __ballot(act && ref == kEnd && leaf == kEnd) != 0);
-        PROF_ADD(10, (uint32_t)__popcll(__ballot(act && ref == kEnd && leaf == kEnd)));
-#endif
         if (act && ref == kEnd && leaf == kEnd) finish();
     }
     // ---- partition scan: read every counter (one lane each) and join the first
@@ -1372,18 +1269,10 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         enter(63u - (__builtin_amdgcn_readfirstlane(key) & 63u));
     }
     }
-#ifdef MCPT_TRACE_PROF
-    if (lane == 0)
-        for (int i = 0; i < 12; i++) atomicAdd(&g_trace_prof[i], (unsigned long long)prof[i]);
-#endif
-    wave_stats(a.set[0].stats, lane, tot_n - tot_n1, tot_t - tot_t1, tot_h - tot_h1);
-    wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);
-#ifdef MCPT_WAVE_TIMES
-    if (threadIdx.x == 0 && blockIdx.x < 16384) {
-        g_wave_t[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-        g_wave_t[4 * blockIdx.x + 2] = part;
+    if constexpr (kCount) {
+        wave_stats(a.set[0].stats, lane, tot_n - tot_n1, tot_t - tot_t1, tot_h - tot_h1);
+        wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);
     }
-#endif
 }
 
 // Light-sample table of an HRDI env light (EnvView::ltab / lrow / lcol): entry (y, x + 1)
@@ -1536,6 +1425,8 @@ __global__ void k_accumulate(CounterBlock* c, uint32_t nparts, uint32_t* occ_gat
             }
         }
         c->tot_vis += v[C_VIS];
+        c->tot_ext_q += v[C_EXT];
+        c->tot_any_q += v[C_ANY];
         c->last_ext = v[C_EXT];
         c->last_live = er;
         if (er == 0) c->idle = 1;  // no path alive and none generated: every later iteration is a no-op
@@ -1598,10 +1489,10 @@ int launch_geometry(int dev, LaunchGeom& g) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
     if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess) nx = 1;
     int occ[2][2] = {};  // [width 2 / 4][LDS stack 8 / deep]
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0][0], k_trace<2, kLdsStack>, kTraceBlock, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0][1], k_trace<2, kLdsStackDeep>, kTraceBlock, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1][0], k_trace<4, kLdsStack>, kTraceBlock, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1][1], k_trace<4, kLdsStackDeep>, kTraceBlock, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0][0], k_trace<2, kLdsStack, false>, kTraceBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0][1], k_trace<2, kLdsStackDeep, false>, kTraceBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1][0], k_trace<4, kLdsStack, false>, kTraceBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1][1], k_trace<4, kLdsStackDeep, false>, kTraceBlock, 0) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat0, k_material<false>, kBlock, 0) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat1, k_material<true>, kBlock, 0) != hipSuccess)
         return -1;
@@ -1670,15 +1561,24 @@ void launch_trace(const TraceArgs& args, const LaunchGeom& g, hipStream_t s) {
     //   4-wide, deep stack (config 5): 24 -- 16 / 20 / 24 / 28 / 32 / 40: 15.16 / 15.14 / 14.87
     //     / 14.88 / 14.99 / 15.61.
     // Waves that refill less often spend fewer trips on the refill's dependent loads; too high
-    // a threshold leaves lanes idle (tools/gpu_knobs2.sh, tools/gpu_cfg_refill.sh).
+    // a threshold leaves lanes idle (round-2 sweeps; tools/gpu/run.sh abenv repeats them).
     static const uint32_t kRefill[2][2] = {{20u, 32u}, {24u, 24u}};  // [width 2/4][stack 8/deep]
     a.refill_min = g.refill_min ? g.refill_min : kRefill[w][k];
     const uint32_t wps = std::max<uint32_t>(1, g.trace_waves[w][k] / nsh);
     const dim3 grid(wps * nsh), block(kTraceBlock);
-    if (w == 0 && k == 0) hipLaunchKernelGGL((k_trace<2, kLdsStack>), grid, block, 0, s, a);
-    else if (w == 0) hipLaunchKernelGGL((k_trace<2, kLdsStackDeep>), grid, block, 0, s, a);
-    else if (k == 0) hipLaunchKernelGGL((k_trace<4, kLdsStack>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_trace<4, kLdsStackDeep>), grid, block, 0, s, a);
+    // The counting instantiation (work counters, mcpt_set_work_counters) runs on the same grid;
+    // a persistent wave that finds its partitions drained simply exits.
+    if (a.set[0].stats || a.set[1].stats) {
+        if (w == 0 && k == 0) hipLaunchKernelGGL((k_trace<2, kLdsStack, true>), grid, block, 0, s, a);
+        else if (w == 0) hipLaunchKernelGGL((k_trace<2, kLdsStackDeep, true>), grid, block, 0, s, a);
+        else if (k == 0) hipLaunchKernelGGL((k_trace<4, kLdsStack, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_trace<4, kLdsStackDeep, true>), grid, block, 0, s, a);
+        return;
+    }
+    if (w == 0 && k == 0) hipLaunchKernelGGL((k_trace<2, kLdsStack, false>), grid, block, 0, s, a);
+    else if (w == 0) hipLaunchKernelGGL((k_trace<2, kLdsStackDeep, false>), grid, block, 0, s, a);
+    else if (k == 0) hipLaunchKernelGGL((k_trace<4, kLdsStack, false>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_trace<4, kLdsStackDeep, false>), grid, block, 0, s, a);
 }
 __global__ void k_quot(const float* a, const float* b, float* out, uint32_t n) {  // mcpt_debug_quot
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1703,65 +1603,98 @@ void launch_copy(const float4* src, float4* dst, size_t n, hipStream_t s) {
     if (n) hipLaunchKernelGGL(k_copy, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, n);
 }
 
-int wave_times(unsigned long long* out, int n) {  // diagnostics build only (MCPT_WAVE_TIMES)
-#ifdef MCPT_WAVE_TIMES
-    n = n < 16384 ? n : 16384;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), 4 * n * sizeof(unsigned long long)) != hipSuccess) return -1;
-    return n;
-#else
+// The round-2/3 diagnostics builds (per-section wave clocks of k_shade / k_material, k_trace loop
+// profiles, wave lifetimes, per-ray step counts) are gone from the kernels (they are in git
+// history); rocprofv3 counter passes (tools/gpu/run.sh pmc) replace them.  The ABI entries stay
+// and report that nothing was collected.
+int wave_times(unsigned long long* out, int n) {
     (void)out;
     (void)n;
     return 0;
-#endif
 }
-int trace_profile(unsigned long long* out, int reset) {  // diagnostics build only
-#if defined(MCPT_SHADE_PROF)
-    static unsigned long long v[64 * 12];
-    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_trace_prof), sizeof(v)) != hipSuccess) return -1;
-    for (int i = 0; i < 12; i++) { out[i] = 0; for (int s = 0; s < 64; s++) out[i] += v[s * 12 + i]; }
-    if (reset) {
-        static unsigned long long z[64 * 12] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_trace_prof), z, sizeof(z)) != hipSuccess) return -1;
-    }
-    return 12;
-#elif defined(MCPT_TRACE_PROF)
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace_prof), sizeof(g_trace_prof)) != hipSuccess) return -1;
-    if (reset) {
-        unsigned long long z[12] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_trace_prof), z, sizeof(z)) != hipSuccess) return -1;
-    }
-    return 12;
-#else
+int trace_profile(unsigned long long* out, int reset) {
     (void)out;
     (void)reset;
     return 0;
-#endif
 }
 __global__ void k_leaf_boxes(DevScene sc, uint32_t nnodes, float4* out) {  // see launch_leaf_boxes
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    auto put = [&](int ref, float mnx, float mny, float mnz, float mxx, float mxy, float mxz) {
+    auto put = [&](int ref, float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float w) {
         if (ref >= 0 || ref == kEnd) return;
         const uint32_t off = (uint32_t)ref & 0xffffffu, cnt = (((uint32_t)ref >> 24) & 7u) + 1u;
         for (uint32_t k = off; k < off + cnt && k < sc.ntri; k++) {
-            out[2 * k] = make_float4(mnx, mny, mnz, 0.f);
+            out[2 * k] = make_float4(mnx, mny, mnz, w);  // .w: the leaf's culling margin
             out[2 * k + 1] = make_float4(mxx, mxy, mxz, 0.f);
         }
     };
     if (i == 0 && sc.root_ref < 0)  // the whole tree is one leaf: its box is the root box
-        put(sc.root_ref, sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1], sc.root_mx[2]);
+        put(sc.root_ref, sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0], sc.root_mx[1], sc.root_mx[2],
+            sc.root_w);
     if (i >= nnodes) return;
-    if (sc.width == 4) {  // mn.x[4], mx.x[4], mn.y[4], mx.y[4], mn.z[4], mx.z[4], refs[4]
+    if (sc.width == 4) {  // mn.x[4], mx.x[4], mn.y[4], mx.y[4], mn.z[4], mx.z[4], refs[4], margins[4]
         const float4* nd = sc.nodes + 8 * (size_t)i;
-        const float4 mnx = nd[0], mxx = nd[1], mny = nd[2], mxy = nd[3], mnz = nd[4], mxz = nd[5], rf = nd[6];
+        const float4 mnx = nd[0], mxx = nd[1], mny = nd[2], mxy = nd[3], mnz = nd[4], mxz = nd[5], rf = nd[6], wq = nd[7];
         const float* a0 = &mnx.x; const float* a1 = &mxx.x; const float* b0 = &mny.x;
         const float* b1 = &mxy.x; const float* c0 = &mnz.x; const float* c1 = &mxz.x; const float* r = &rf.x;
-        for (int k = 0; k < 4; k++) put(__float_as_int(r[k]), a0[k], b0[k], c0[k], a1[k], b1[k], c1[k]);
-    } else {  // per axis (mn0, mn1, mx0, mx1), then (ref0, ref1, -, -)
+        const float* w = &wq.x;
+        for (int k = 0; k < 4; k++) put(__float_as_int(r[k]), a0[k], b0[k], c0[k], a1[k], b1[k], c1[k], w[k]);
+    } else {  // per axis (mn0, mn1, mx0, mx1), then (ref0, ref1, margin0, margin1)
         const float4* nd = sc.nodes + 4 * (size_t)i;
         const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-        put(__float_as_int(q3.x), q0.x, q1.x, q2.x, q0.z, q1.z, q2.z);
-        put(__float_as_int(q3.y), q0.y, q1.y, q2.y, q0.w, q1.w, q2.w);
+        put(__float_as_int(q3.x), q0.x, q1.x, q2.x, q0.z, q1.z, q2.z, q3.z);
+        put(__float_as_int(q3.y), q0.y, q1.y, q2.y, q0.w, q1.w, q2.w, q3.w);
     }
+}
+
+// Culling margins (mcpt_core.hpp "conservative box culling").  k_cull_tri: W'_T of every triangle
+// record (float, rounded up) and the far coefficient P (positive floats order as their bits).
+__global__ void k_cull_tri(const float4* tri, uint32_t ntri, float* tw, uint32_t* pmax) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ntri) return;
+    const float4* r = tri + kTriF4 * (size_t)i;
+    const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+    double far;
+    tw[i] = cull_to_float_up(cull_tri_margin(v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), &far));
+    if (far > 0.0) atomicMax(pmax, __float_as_uint(cull_to_float_up(far)));
+}
+// One bottom-up pass over child-pair nodes: each child's word (q3.z / q3.w) = the largest W'_T
+// under it -- its triangles for a leaf, the child node's two words for an interior child.  Words
+// start at 0 and only grow toward the subtree maxima, so a word read before or after its own
+// update in the same pass is either way a lower bound, and depth + 1 passes reach the fixed point.
+__global__ void k_cull_pairs(float4* nodes, uint32_t npairs, const float* tw, uint32_t ntri) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    const float4 q3 = nodes[4 * (size_t)i + 3];
+    float w[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int ref = __float_as_int(k ? q3.y : q3.x);
+        float v = 0.f;
+        if (ref >= 0) {
+            const float4 c = nodes[4 * (size_t)ref + 3];
+            v = __builtin_fmaxf(c.z, c.w);
+        } else if (ref != kEnd) {
+            const uint32_t off = (uint32_t)ref & 0xffffffu, cnt = (((uint32_t)ref >> 24) & 7u) + 1u;
+            for (uint32_t t = off; t < off + cnt && t < ntri; t++) v = __builtin_fmaxf(v, tw[t]);
+        }
+        w[k] = v;
+    }
+    nodes[4 * (size_t)i + 3] = make_float4(q3.x, q3.y, w[0], w[1]);
+}
+__global__ void k_cull_zero(float4* nodes, uint32_t npairs) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    float4 q3 = nodes[4 * (size_t)i + 3];
+    q3.z = q3.w = 0.f;
+    nodes[4 * (size_t)i + 3] = q3;
+}
+void launch_cull_margins(float4* nodes, uint32_t npairs, const float4* tri, uint32_t ntri, float* tri_w,
+                         uint32_t* pmax, int passes, hipStream_t s) {
+    if (ntri) hipLaunchKernelGGL(k_cull_tri, dim3((ntri + 255) / 256), dim3(256), 0, s, tri, ntri, tri_w, pmax);
+    if (!npairs) return;
+    hipLaunchKernelGGL(k_cull_zero, dim3((npairs + 255) / 256), dim3(256), 0, s, nodes, npairs);
+    for (int p = 0; p < passes; p++)
+        hipLaunchKernelGGL(k_cull_pairs, dim3((npairs + 255) / 256), dim3(256), 0, s, nodes, npairs, tri_w, ntri);
 }
 void launch_leaf_boxes(const DevScene& sc, uint32_t nnodes, float4* leaf_box, hipStream_t s) {
     hipLaunchKernelGGL(k_leaf_boxes, dim3(nnodes / 256 + 1), dim3(256), 0, s, sc, nnodes, leaf_box);

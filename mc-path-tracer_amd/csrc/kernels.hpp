@@ -99,6 +99,12 @@ struct DevScene {
     uint32_t ntri;
     int occ_g, occ_b;       // origin cells per axis, direction bins per face coordinate
     float occ_inv[3];       // occ_g / root box extent, per axis
+    // Conservative culling (mcpt_core.hpp "conservative box culling"): every node holds each
+    // child's margin W (pair nodes: q3.z / q3.w; 4-wide nodes: float4 7; leaf_box[2t].w), P is the
+    // scene's far coefficient, root_w the root box's margin.  cull_ok = 0 (a caller BVH whose boxes
+    // do not contain their triangles, or MCPT_CULL=0): nothing is culled.
+    float cull_p, root_w;
+    int cull_ok;
 };
 constexpr uint32_t kOccEmpty = 0xffffffffu;
 constexpr uint32_t kOccWays = 2;      // entries per cell: k_trace writes way tri mod 2, k_material tests both
@@ -133,6 +139,7 @@ struct CounterBlock {
     uint32_t grab[kMaxParts][C_WORDS];  // k_trace ray hand-out, one counter line per partition
     unsigned long long tot_ext, tot_any, tot_vis, tot_occ;
     unsigned long long tot_stats[6];
+    unsigned long long tot_ext_q, tot_any_q;  // rays queued to k_trace (the rest were resolved in place)
 };
 
 struct ShadeArgs {
@@ -210,8 +217,13 @@ void launch_shade_stage(bool material_stage, const ShadeArgs& a, int nblocks, co
 void launch_trace(const TraceArgs& a, const LaunchGeom& g, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
 // leaf_box[2t], [2t + 1] = the box of the leaf that holds triangle record t (nodes: nnodes nodes
-// of the given width; a root that is itself a leaf gets the root box)
+// of the given width; a root that is itself a leaf gets the root box); leaf_box[2t].w = its margin
 void launch_leaf_boxes(const DevScene& sc, uint32_t nnodes, float4* leaf_box, hipStream_t s);
+// Culling margins of a child-pair tree (mcpt_core.hpp cull_*): tri_w[t] = W'_T of record t,
+// *pmax = the far coefficient P's bits (max), then `passes` bottom-up passes writing every
+// child's subtree maximum into q3.z / q3.w (passes >= tree depth + 1 reach the fixed point).
+void launch_cull_margins(float4* nodes, uint32_t npairs, const float4* tri, uint32_t ntri, float* tri_w,
+                         uint32_t* pmax, int passes, hipStream_t s);
 void launch_env_table(const mcpt::EnvView& e, bool fixed_mode, float4* out, float2* row, float2* col, hipStream_t s);
 // HRDI tables on the device (env_build.hip), bit-identical to the host build: scratch holds
 // env_build_scratch_floats(W, H) floats; W * H < 2^31.

@@ -43,6 +43,10 @@ struct mcpt_ctx {
     int32_t ntri = 0;               // triangles of the uploaded scene
     size_t occ_entries_n = 0;       // occluder-cache table entries (DevScene::occ; + 2 gate words)
     int pair_depth = 0;
+    bool cull_ok = true, occ_nest_ok = true;  // last upload: boxes contain their triangles / nest (scene_upload)
+    // traversal work counters (mcpt_set_work_counters): k_trace's counting instantiation, whose six
+    // per-lane counters cost the fast one its spill-free registers -- off by default
+    bool count_work = getenv("MCPT_WORK_COUNTERS") != nullptr;
     int node_layout = 0;  // pair-node numbering the last upload used (mcpt_debug_node_layout)
     // camera
     mcpt::CamView cam{};
@@ -215,17 +219,19 @@ static int pairs_to_quads(const std::vector<float4>& pn, int root_ref, std::vect
     push_depth.push_back(0);
     for (size_t h = 0; h < order.size(); h++) {
         const int p = order[h];
-        struct Slot { float mn[3], mx[3]; int ref; };
+        struct Slot { float mn[3], mx[3], w; int ref; };  // w: the child's culling margin (q3.z / q3.w)
         Slot sl[4];
         int n = 0;
         for (int k = 0; k < 2; k++) {
             const int r = ref_at(p, k);
             if (r < 0) {  // leaf child of the pair node: its box is in p
                 for (int a = 0; a < 3; a++) { sl[n].mn[a] = comp(pn[4 * p + a], k); sl[n].mx[a] = comp(pn[4 * p + a], 2 + k); }
+                sl[n].w = comp(pn[4 * p + 3], 2 + k);
                 sl[n++].ref = r;
             } else {      // interior child: take its two children
                 for (int j = 0; j < 2; j++) {
                     for (int a = 0; a < 3; a++) { sl[n].mn[a] = comp(pn[4 * r + a], j); sl[n].mx[a] = comp(pn[4 * r + a], 2 + j); }
+                    sl[n].w = comp(pn[4 * r + 3], 2 + j);
                     sl[n++].ref = ref_at(r, j);
                 }
             }
@@ -254,6 +260,7 @@ static int pairs_to_quads(const std::vector<float4>& pn, int root_ref, std::vect
             }
             int r = used ? sl[k].ref : -1;  // kEnd: empty slot
             memcpy(&f[6 * 4 + k], &r, 4);
+            f[7 * 4 + k] = used ? sl[k].w : 0.f;  // margins (float4 7)
         }
         qn.insert(qn.end(), q, q + 8);
     }
@@ -401,12 +408,10 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         q[1] = make_float4(a0[1], a1[1], b0[1], b1[1]);
         q[2] = make_float4(a0[2], a1[2], b0[2], b1[2]);
         int r0 = ref_of(c0), r1 = ref_of(c1);
-        float fr0, fr1, fax;
-        int ax = d->axis[i];
+        float fr0, fr1;
         memcpy(&fr0, &r0, 4);
         memcpy(&fr1, &r1, 4);
-        memcpy(&fax, &ax, 4);
-        q[3] = make_float4(fr0, fr1, fax, 0.f);
+        q[3] = make_float4(fr0, fr1, 0.f, 0.f);  // .z / .w: the children's culling margins (launch_cull_margins)
     }
     pn.insert(pn.end(), xn.begin(), xn.end());
     // depth of the tree = bound on stack pushes
@@ -466,6 +471,69 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         dsh = lb.tri_sh;
         c->pair_depth = lb.depth;
     }
+    // Conservative culling (mcpt_core.hpp "conservative box culling").  The bound holds for a box
+    // that contains its triangles: a caller BVH whose node boxes miss some of their subtree's
+    // vertices is traversed without culling (cull_ok 0).  The occluder cache also needs every box
+    // inside its parent's (occ_test tests a leaf box in place of its ancestors): nest_ok.
+    bool cull_ok = true, nest_ok = true;
+    if (!gpu_bvh && N > 0) {
+        std::vector<float> lo(3 * (size_t)N, 3.402823466e+38f), hi(3 * (size_t)N, -3.402823466e+38f);
+        for (int i = N - 1; i >= 0; i--) {  // children follow their parent (offset[i] > i, i + 1)
+            float* l = &lo[3 * (size_t)i];
+            float* h = &hi[3 * (size_t)i];
+            if (d->nprims[i] > 0) {
+                for (int t = d->offset[i]; t < d->offset[i] + d->nprims[i]; t++)
+                    for (const float* v : {d->v0 + 3 * (size_t)t, d->v1 + 3 * (size_t)t, d->v2 + 3 * (size_t)t})
+                        for (int k = 0; k < 3; k++) { l[k] = std::fmin(l[k], v[k]); h[k] = std::fmax(h[k], v[k]); }
+            } else {
+                for (int ch : {i + 1, d->offset[i]}) {
+                    for (int k = 0; k < 3; k++) {
+                        l[k] = std::fmin(l[k], lo[3 * (size_t)ch + k]);
+                        h[k] = std::fmax(h[k], hi[3 * (size_t)ch + k]);
+                        if (!(d->bmin[3 * (size_t)ch + k] >= d->bmin[3 * (size_t)i + k]) ||
+                            !(d->bmax[3 * (size_t)ch + k] <= d->bmax[3 * (size_t)i + k]))
+                            nest_ok = false;
+                    }
+                }
+            }
+            for (int k = 0; k < 3; k++)
+                if (!(l[k] >= d->bmin[3 * (size_t)i + k]) || !(h[k] <= d->bmax[3 * (size_t)i + k])) cull_ok = false;
+        }
+        nest_ok = nest_ok && cull_ok;
+    }
+    if (const char* e = getenv("MCPT_CULL"))  // 0: no culling at all (A/B, and a reference-order traversal)
+        if (e[0] == '0' && e[1] == 0) cull_ok = false;
+    c->cull_ok = cull_ok;
+    c->occ_nest_ok = nest_ok;
+    float cull_p = 0.f, root_w = __builtin_huge_valf();
+    {
+        const uint32_t npairs = (uint32_t)(gpu_bvh ? lb.nnodes : pn.size() / 4);
+        const int proot = gpu_bvh ? lb.root_ref : (N > 0 ? ref_of(0) : 0);
+        float* tw = nullptr;
+        uint32_t* pm = nullptr;
+        if (d->ntri > 0) {
+            if ((rc = dalloc(c, c->tmp_bufs, &tw, (size_t)d->ntri)) || (rc = dalloc(c, c->tmp_bufs, &pm, 1))) return rc;
+            HIPCHK(c, hipMemsetAsync(pm, 0, sizeof(uint32_t), c->stream));
+            mcpt_dev::launch_cull_margins(dn, npairs, dt, (uint32_t)d->ntri, tw, pm, c->pair_depth + 2, c->stream);
+            HIPCHK(c, hipGetLastError());
+            uint32_t pb = 0;
+            HIPCHK(c, hipMemcpyAsync(&pb, pm, sizeof(pb), hipMemcpyDeviceToHost, c->stream));
+            float4 rq = make_float4(0.f, 0.f, 0.f, 0.f);
+            std::vector<float> leaf_w;
+            if (proot >= 0 && npairs > 0) {
+                HIPCHK(c, hipMemcpyAsync(&rq, dn + 4 * (size_t)proot + 3, sizeof(rq), hipMemcpyDeviceToHost, c->stream));
+            } else if (proot < 0) {  // the whole tree is one leaf
+                const uint32_t off = (uint32_t)proot & 0xffffffu, cnt = (((uint32_t)proot >> 24) & 7u) + 1u;
+                leaf_w.resize(cnt);
+                HIPCHK(c, hipMemcpyAsync(leaf_w.data(), tw + off, cnt * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+            }
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            memcpy(&cull_p, &pb, 4);
+            root_w = proot >= 0 ? std::fmax(rq.z, rq.w) : 0.f;
+            for (float w : leaf_w) root_w = std::fmax(root_w, w);
+            free_list(c->tmp_bufs);
+        }
+    }
     if ((rc = dupload(c, c->scene_bufs, &dm, d->mat_params, (size_t)d->nmat * 8))) return rc;
     if ((rc = dupload(c, c->scene_bufs, &dd, d->dir_params, (size_t)d->ndir * 7))) return rc;
     s.nodes = dn; s.tri = dt; s.tri_sh = dsh; s.mats = dm; s.dirs = dd;
@@ -488,8 +556,9 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             pairs.resize((size_t)lb.nnodes * 4);
             if (lb.nnodes) HIPCHK(c, hipMemcpy(pairs.data(), lb.nodes, pairs.size() * sizeof(float4), hipMemcpyDeviceToHost));
             proot = lb.root_ref;
-        } else {
-            pairs = pn;
+        } else {  // the uploaded pairs, with the margins launch_cull_margins wrote
+            pairs.resize(pn.size());
+            if (!pn.empty()) HIPCHK(c, hipMemcpy(pairs.data(), dn, pairs.size() * sizeof(float4), hipMemcpyDeviceToHost));
             proot = N > 0 ? ref_of(0) : 0;
         }
         std::vector<float4> quads;
@@ -610,6 +679,9 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     }
     s.depth = width == 4 ? quad_push : c->pair_depth;
     s.width = width;
+    s.cull_p = cull_p;
+    s.root_w = root_w;
+    s.cull_ok = cull_ok ? 1 : 0;
     // Any-hit occluder cache (kernels.hip occ_hit2): every triangle record's leaf box and the
     // (origin cell x direction bin) table, empty at upload.  MCPT_OCC_G=0 turns it off;
     // MCPT_OCC_G / MCPT_OCC_B set the cells per axis / bins per face coordinate.
@@ -624,7 +696,9 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         if (const char* e = getenv("MCPT_OCC_G")) G = atoi(e);
         if (const char* e = getenv("MCPT_OCC_B")) B = atoi(e);
         // the index G^3 * 6 * B^2 must fit 32 bits
-        if (G > 0 && G <= 64 && B > 0 && B <= 64 && (uint64_t)G * G * G * 6 * B * B <= 0xffffffffull && d->ntri > 0) {
+        // (off unless every box nests in its parent's: occ_test relies on it, see cull_ok above)
+        if (G > 0 && G <= 64 && B > 0 && B <= 64 && (uint64_t)G * G * G * 6 * B * B <= 0xffffffffull && d->ntri > 0 &&
+            c->occ_nest_ok) {
             float4* lbx;
             uint32_t* occ;
             const size_t ne = occ_entries(G, B);
@@ -681,6 +755,17 @@ int mcpt_debug_env_tables(mcpt_ctx* c, float* marginal_y, float* conds_y, float*
     return MCPT_OK;
 }
 int mcpt_debug_node_layout(const mcpt_ctx* c) { return c ? c->node_layout : MCPT_E_INVALID; }
+int mcpt_debug_ray_counts(const mcpt_ctx* c, uint64_t* out) {
+    if (!c || !out) return MCPT_E_INVALID;
+    const CounterBlock& t = c->totals;
+    const bool ok = c->totals_ok;
+    out[0] = ok ? t.tot_ext : 0;    // extension rays (queued + resolved in place)
+    out[1] = ok ? t.tot_ext_q : 0;  // extension rays k_trace traversed
+    out[2] = ok ? t.tot_any : 0;    // shadow + BRDF visibility rays
+    out[3] = ok ? t.tot_any_q : 0;  // any-hit rays k_trace traversed
+    out[4] = ok ? t.tot_occ : 0;    // any-hit rays the occluder cache resolved in k_material
+    return MCPT_OK;
+}
 int mcpt_debug_occ_stats(const mcpt_ctx* c, uint64_t* resolved, int32_t* enabled) {
     if (!c) return MCPT_E_INVALID;
     if (resolved) *resolved = c->totals_ok ? c->totals.tot_occ : 0;
@@ -886,7 +971,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     e.queue = c->ext_q;
     e.count_ptr = &c->cnt->shard[0][C_EXT];
     e.shard_cap = c->ext_cap;
-    e.stats = &c->cnt->shard[0][C_STATS];
+    e.stats = c->count_work ? &c->cnt->shard[0][C_STATS] : nullptr;  // mcpt_set_work_counters
     e.prefiltered = 1;  // k_shade queues only rays that enter the root box
     TraceSet& v = ta.set[1];
     v.ro = c->p.sray_o;
@@ -894,7 +979,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     v.queue = c->any_q;
     v.count_ptr = &c->cnt->shard[0][C_ANY];
     v.shard_cap = c->any_cap;
-    v.stats = &c->cnt->shard[0][C_STATS + 3];
+    v.stats = c->count_work ? &c->cnt->shard[0][C_STATS + 3] : nullptr;
     v.prefiltered = 1;
     v.ray_at_slot = 1;  // k_material stores the any-hit rays at their queue positions
     ta.hit_tri = c->p.hit_tri;
@@ -1335,7 +1420,7 @@ static int film_view(mcpt_ctx* c, const float4** Ld, const uint32_t** samples) {
 }
 
 int mcpt_set_path_slots(mcpt_ctx* c, uint32_t slots) {
-    if (!c || slots < 1 || slots > 64) return set_err(c, MCPT_E_INVALID, "path slots must be 1..64");
+    if (!c || slots < 1 || slots > 256) return set_err(c, MCPT_E_INVALID, "path slots must be 1..256");
     if (slots == c->slots) return MCPT_OK;
     if (!c->P) {
         c->slots = slots;
@@ -1352,6 +1437,12 @@ int mcpt_set_path_slots(mcpt_ctx* c, uint32_t slots) {
         (void)mcpt_film_resize(c, c->W, c->H, c->tile_w, c->tile_h);
         return set_err(c, rc, err);
     }
+    return MCPT_OK;
+}
+
+int mcpt_set_work_counters(mcpt_ctx* c, int32_t on) {
+    if (!c) return MCPT_E_INVALID;
+    c->count_work = on != 0;
     return MCPT_OK;
 }
 

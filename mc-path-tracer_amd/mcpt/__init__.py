@@ -139,6 +139,8 @@ ABI = {
     "mcpt_debug_env_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _i]),
     "mcpt_debug_node_layout": (C.c_int, [C.c_void_p]),
     "mcpt_debug_occ_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]),
+    "mcpt_debug_ray_counts": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "mcpt_set_work_counters": (C.c_int, [C.c_void_p, C.c_int32]),
     "mcpt_scene_upload_gpu_bvh": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mcpt_set_gpu_bvh_builder": (C.c_int, [C.c_void_p, C.c_int32]),
     "mcpt_film_size": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
@@ -179,7 +181,7 @@ def lib() -> C.CDLL:
         for name, (res, args) in ABI.items():
             fn = getattr(l, name, None)
             if fn is None and os.environ.get("MCPT_LIB"):
-                continue  # an older experimental variant library (tools/ab.py)
+                continue  # an older experimental variant library (tools/gpu/ab_libs.sh)
             if fn is None:
                 raise RuntimeError(f"{LIB_PATH} does not export {name}: rebuild it")
             fn.restype = res
@@ -410,6 +412,14 @@ class PathTracer:
         else:
             self._ck(lib().mcpt_scene_upload(self.h, C.byref(d)))
 
+    def ray_counts(self) -> dict:
+        """Ray counts since the last film clear (mcpt_debug_ray_counts)."""
+        v = (C.c_uint64 * 5)()
+        if hasattr(lib(), "mcpt_debug_ray_counts") or not os.environ.get("MCPT_LIB"):
+            self._ck(lib().mcpt_debug_ray_counts(self.h, v))  # (an older variant library: zeros)
+        return dict(zip(("extension", "extension_traversed", "any_hit", "any_hit_traversed", "any_hit_occluder_cache"),
+                        [int(x) for x in v]))
+
     def occ_stats(self):
         """(any-hit rays the occluder cache resolved since the last film clear, cache enabled)."""
         r, e = C.c_uint64(0), C.c_int32(0)
@@ -449,6 +459,12 @@ class PathTracer:
     def set_path_slots(self, slots):
         """Paths in flight per pixel (mcpt_set_path_slots); re-allocates and clears the film."""
         self._ck(lib().mcpt_set_path_slots(self.h, slots))
+
+    def set_work_counters(self, on=True):
+        """Traversal work counters in StageStats (mcpt_set_work_counters; off by default: the
+        counting k_trace build is slower)."""
+        if hasattr(lib(), "mcpt_set_work_counters") or not os.environ.get("MCPT_LIB"):
+            self._ck(lib().mcpt_set_work_counters(self.h, int(bool(on))))  # (an older variant library counts always)
 
     def set_trace_partitions(self, nparts=0):
         """k_trace work partitions (mcpt_set_trace_partitions); 0 = the device default, two per XCD."""

@@ -26,6 +26,22 @@ def tiles_for_rank(rank, world, W, H, tile=256):
     return [(tx, ty) for ty in range(ny) for tx in range(nx) if (tx + ty) % world == rank]
 
 
+# Path state per path (126 B) and the budget the strong split may give it per GPU.
+PATH_BYTES = 126
+SLOT_BUDGET_BYTES = 32 << 30
+
+
+def strong_slots(base_slots, world, W, H, spp, budget=SLOT_BUDGET_BYTES):
+    """Path slots for a frame split over `world` ranks: every rank keeps the paths in flight of the
+    one-GPU run (base_slots x W x H) over its 1/world of the pixels, so slots scale with world --
+    bounded by spp (a slot renders >= 1 sample) and by the state budget (the film's path state is
+    allocated for the whole W x H frame on every rank).  One value for every rank: the slot count
+    sets the film's summation order, so the gathered frame then equals a one-rank frame rendered
+    with the same slots bit for bit."""
+    cap = max(1, budget // (PATH_BYTES * W * H))
+    return int(max(base_slots, min(base_slots * world, spp, cap, 256)))  # mcpt_set_path_slots: 1..256
+
+
 def pack(Ld: np.ndarray, samples: np.ndarray, tiles, W, H, tile=256) -> np.ndarray:
     """Host restatement of mcpt_film_pack_tiles: a film's tile pixels as [n, 4] float32 (.w =
     samples bits), tile by tile, rows of tile_w pixels; pixels past the frame edge are zero."""
@@ -63,7 +79,10 @@ def gather_packed_to_root(local, rank, world, dist, W, H, tile=256):
     import torch
 
     if rank != 0:
-        dist.send(local.contiguous(), dst=0)
+        # a rank with no tiles (fewer tiles than ranks) sends nothing, as rank 0 posts no receive for
+        # it: an unmatched send would hang RCCL or leave a stray gloo message for a later collective
+        if local.shape[0]:
+            dist.send(local.contiguous(), dst=0)
         return None
     parts = [local]
     for r in range(1, world):

@@ -133,7 +133,19 @@ void or_gen_ray(const or_camera *cam, int32_t W, int32_t H, int32_t x, int32_t y
                 uint64_t seed, uint32_t pixel, uint32_t sample, float *o, float *d);
 const char *or_version(void);
 
+/* trav_model.c (test infrastructure): a model of the product traversal's box culling, checked
+ * against or_trace_closest / or_trace_any on adversarial rays (tests/test_cull_model.py).
+ * or_model_margins: per desc node and per triangle own-box margins and the far coefficient P;
+ * returns 0 when a node box does not contain its subtree's vertices.  or_model_trace: mode 0
+ * culls nothing, 1 the round-3 rule, 2 the round-4 rule; tri = closest triangle id or -1,
+ * t = its t, visible = any-hit result; *nodes = boxes tested. */
+int32_t or_model_margins(const or_scene *sc, float *node_w, float *tri_w, float *p);
+void or_model_trace(const or_scene *sc, int32_t n, const float *ro, const float *rd, int32_t mode,
+                    const float *node_w, const float *tri_w, float p, int32_t *tri, float *t, uint8_t *visible,
+                    uint64_t *nodes);
+
 #ifdef __cplusplus
 }
 #endif
+
 #endif

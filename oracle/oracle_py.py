@@ -74,6 +74,9 @@ def lib():
             "or_stage_material": (None, [C.POINTER(OrScene), C.POINTER(OrConfig), C.c_int32, _u, _i, _f, _f, _f,
                                          _f, _f, _f, _f, _f, _f]),
             "or_version": (C.c_char_p, []),
+            "or_model_margins": (C.c_int32, [C.POINTER(OrScene), _f, _f, _f]),
+            "or_model_trace": (None, [C.POINTER(OrScene), C.c_int32, _f, _f, C.c_int32, _f, _f, C.c_float, _i, _f,
+                                      C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)]),
         }
         for n, (r, a) in sig.items():
             fn = getattr(l, n)
@@ -182,6 +185,34 @@ def trace_any(arrays, ro, rd, traversal=0):
     vis = np.zeros(n, np.uint8)
     lib().or_trace_any(C.byref(s), n, fptr(ro), fptr(rd), traversal, vis.ctypes.data_as(C.POINTER(C.c_uint8)))
     return vis
+
+
+def model_margins(arrays):
+    """Margins of the product culling rule's model (trav_model.c): per desc node, per triangle own
+    box, the far coefficient P and whether every node box contains its subtree's vertices."""
+    s = scene_struct(arrays)
+    nw = np.zeros(max(1, s.nnodes), np.float32)
+    tw = np.zeros(max(1, s.ntri), np.float32)
+    p = np.zeros(1, np.float32)
+    ok = lib().or_model_margins(C.byref(s), fptr(nw), fptr(tw), fptr(p))
+    return {"node_w": nw, "tri_w": tw, "p": float(p[0]), "contained": bool(ok)}
+
+
+def model_trace(arrays, ro, rd, mode, margins=None):
+    """trav_model.c: closest (triangle id, t) and any-hit visibility under culling rule `mode`
+    (0 none, 1 round 3, 2 round 4) and the number of boxes tested."""
+    s = scene_struct(arrays)
+    m = margins or model_margins(arrays)
+    ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
+    rd = np.ascontiguousarray(rd, np.float32).reshape(-1, 3)
+    n = len(ro)
+    tri = np.zeros(n, np.int32)
+    t = np.zeros(n, np.float32)
+    vis = np.zeros(n, np.uint8)
+    nodes = C.c_uint64(0)
+    lib().or_model_trace(C.byref(s), n, fptr(ro), fptr(rd), mode, fptr(m["node_w"]), fptr(m["tri_w"]), m["p"],
+                         tri.ctypes.data_as(_i), fptr(t), vis.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(nodes))
+    return tri, t, vis, int(nodes.value)
 
 
 def env_build(tex: np.ndarray):

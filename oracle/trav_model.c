@@ -1,0 +1,300 @@
+/*
+ * trav_model.c -- TEST INFRASTRUCTURE ONLY: a scalar model of the *product* traversal's box
+ * culling, used by tests/test_cull_model.py to check the culling rule against the oracle's
+ * reference traversal (mcpt_oracle.c closest_hit / any_hit, which culls nothing, as
+ * Triangle.cu:144-243 with Bounds3f.h:121-153 does) on adversarial rays.  Nothing in the
+ * product links or calls this file.
+ *
+ * The reference visits every box the infinite line crosses; the product skips boxes that cannot
+ * hold the answer.  Two rules are modelled:
+ *   mode 1  the round-3 rule: a box is skipped when it lies behind the origin by more than an
+ *           absolute 1e-5 (t1 < -1e-5) or starts beyond (1 + 2^-8) * t_best.  It assumed that
+ *           Moller-Trumbore's computed t lies within 2^-8 * t of the box's slab interval, which a
+ *           grazing ray breaks;
+ *   mode 2  the round-4 rule (kernels.hip cull_*; DESIGN.md section 5 "culling bound"): every box
+ *           carries a margin W (position units) that bounds how far the point o + t d of an
+ *           accepted hit can lie outside the box, whatever the ray's angle to the triangle, from
+ *           the rounding error of the fp32 Moller-Trumbore expressions with the det >= 1e-6
+ *           acceptance threshold (Triangle.cu:17-21).  Skip when t1 (1 - 2^-18) + W i < 0 (behind)
+ *           or t0 - W i > t_best (1 + 2^-18 + i P) (beyond), i = max |1/d_a| (1 + 2^-18).
+ * The margins come from or_model_margins (a restatement of the product's k_cull_margins in C).
+ * Visit order: both children of an interior node are tested, the nearer (entry t) is visited
+ * first -- the product's order; a sound rule gives the reference's answer in any order.
+ * Leaves of several primitives test each triangle under its own box (the product's expansion
+ * into one-triangle leaves, runtime.cpp scene_upload), with the triangle's own margin.
+ */
+#include "mcpt_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define M_EPS 1e-6f
+#define M_HUGE 1e32f
+#define CULL_SLACK 3.814697265625e-06 /* 2^-18 */
+
+typedef struct { float x, y, z; } mv3;
+static mv3 mv(float x, float y, float z) { mv3 r = {x, y, z}; return r; }
+static mv3 mld(const float *p, int64_t i) { return mv(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
+static mv3 msub(mv3 a, mv3 b) { return mv(a.x - b.x, a.y - b.y, a.z - b.z); }
+static float mdot(mv3 a, mv3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static mv3 mcross(mv3 a, mv3 b) { return mv(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+
+/* the oracle's tri_intersect (Triangle.cu:9-65, TEST_CULL, fp64 det island), t only */
+static int m_tri(const or_scene *sc, int id, mv3 o, mv3 d, float *to) {
+    mv3 p0 = mld(sc->v0, id), p1 = mld(sc->v1, id), p2 = mld(sc->v2, id);
+    mv3 e1 = msub(p1, p0), e2 = msub(p2, p0);
+    mv3 pvec = mcross(d, e2);
+    double det = (double)mdot(e1, pvec);
+    if (det < (double)M_EPS) return 0;
+    mv3 tvec = msub(o, p0);
+    float u = mdot(tvec, pvec);
+    if ((double)u < 0.0 || (double)u > det) return 0;
+    mv3 qvec = mcross(tvec, e1);
+    float v = mdot(d, qvec);
+    if ((double)v < 0.0 || (double)(u + v) > det) return 0;
+    float t = mdot(e2, qvec);
+    *to = (float)((double)t * (1.0 / det));
+    return 1;
+}
+
+/* ---- margins (the product's k_cull_margins / cull_margin, mcpt_core.hpp) ---------------- */
+static const double U24 = 5.9604644775390625e-08; /* 2^-24 */
+
+/* per triangle: beta (coefficient of |tvec|) and omega (absolute term) of the bound
+ * |P' - conv(T)|_a <= omega + beta |o - p0| on an accepted hit */
+static void tri_beta_omega(mv3 e1, mv3 e2, double *beta, double *omega) {
+    const double n1 = sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+    const double n2 = sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+    const double alpha = 28.3 * U24 * n1 * n2 / (double)M_EPS;
+    *beta = alpha * (1.0 + 1.0 / 512.0) + 1.01 * U24;
+    *omega = 2.1 * U24 * (n1 > n2 ? n1 : n2);
+}
+/* a triangle's margin W'_T = (omega + beta diam_T) / (1 - sqrt3 beta) (+ slack); +inf when
+ * sqrt3 beta >= 1/2 (a triangle so large against the det threshold that no box holding it is
+ * ever culled).  A box's margin is the maximum over the triangles it holds. */
+static double tri_margin(double beta, double omega, double diam) {
+    if (!(1.7321 * beta * (1.0 + CULL_SLACK) < 0.5)) return INFINITY;
+    return (omega + beta * diam * (1.0 + 1e-12)) * (1.0 + CULL_SLACK) / (1.0 - 1.7321 * beta * (1.0 + CULL_SLACK));
+}
+static float to_f_up(double w) { return isinf(w) ? INFINITY : (float)(w * (1.0 + 1.0 / 1048576.0)) * (1.0f + 1.0f / 1048576.0f); }
+static double far_coef(double beta) {
+    return beta * (1.0 + 1.0 / 512.0) / (1.0 - 1.7321 * beta) * (1.0 + CULL_SLACK) * (1.0 + 1.0 / 1048576.0);
+}
+static double tri_w_of(const or_scene *sc, int t, double *beta_out) {
+    mv3 a = mld(sc->v0, t), b = mld(sc->v1, t), c = mld(sc->v2, t);
+    mv3 e1 = msub(b, a), e2 = msub(c, a), e3 = msub(c, b);
+    double be, om;
+    tri_beta_omega(e1, e2, &be, &om);
+    const double l1 = sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+    const double l2 = sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+    const double l3 = sqrt((double)e3.x * e3.x + (double)e3.y * e3.y + (double)e3.z * e3.z) * (1.0 + 1e-7);
+    const double diam = l1 > l2 ? (l1 > l3 ? l1 : l3) : (l2 > l3 ? l2 : l3);
+    *beta_out = be;
+    return tri_margin(be, om, diam);
+}
+
+/* node_w[n]: margin of desc node n's box; tri_w[t]: margin of triangle t's own box; *p: the
+ * scene's far-cut coefficient P.  contained: 0 when some node box fails to contain its
+ * subtree's vertices (the product then culls nothing). */
+int32_t or_model_margins(const or_scene *sc, float *node_w, float *tri_w, float *p) {
+    const int N = sc->nnodes;
+    double *nw = calloc((size_t)(N > 0 ? N : 1), sizeof(double));
+    float *lo = malloc(sizeof(float) * 3 * (size_t)(N > 0 ? N : 1)), *hi = malloc(sizeof(float) * 3 * (size_t)(N > 0 ? N : 1));
+    double pg = 0.0;
+    int contained = 1;
+    for (int t = 0; t < sc->ntri; t++) {
+        double be;
+        const double w = tri_w_of(sc, t, &be);
+        if (!isinf(w) && far_coef(be) > pg) pg = far_coef(be);
+        tri_w[t] = to_f_up(w);
+    }
+    /* subtree maxima, children before parents: desc nodes are depth-first (children after parent) */
+    for (int n = N - 1; n >= 0; n--) {
+        if (sc->nprims[n] > 0) {
+            double w = 0;
+            for (int k = 0; k < 3; k++) { lo[3 * n + k] = INFINITY; hi[3 * n + k] = -INFINITY; }
+            for (int i = 0; i < sc->nprims[n]; i++) {
+                const int t = sc->offset[n] + i;
+                double be;
+                const double wt = tri_w_of(sc, t, &be);
+                if (!(wt <= w)) w = wt;
+                const float *v[3] = {sc->v0 + 3 * (int64_t)t, sc->v1 + 3 * (int64_t)t, sc->v2 + 3 * (int64_t)t};
+                for (int j = 0; j < 3; j++)
+                    for (int k = 0; k < 3; k++) {
+                        lo[3 * n + k] = fminf(lo[3 * n + k], v[j][k]);
+                        hi[3 * n + k] = fmaxf(hi[3 * n + k], v[j][k]);
+                    }
+            }
+            nw[n] = w;
+        } else {
+            const int c0 = n + 1, c1 = sc->offset[n];
+            nw[n] = nw[c0] > nw[c1] ? nw[c0] : nw[c1];
+            for (int k = 0; k < 3; k++) {
+                lo[3 * n + k] = fminf(lo[3 * c0 + k], lo[3 * c1 + k]);
+                hi[3 * n + k] = fmaxf(hi[3 * c0 + k], hi[3 * c1 + k]);
+            }
+        }
+        for (int k = 0; k < 3; k++)
+            if (lo[3 * n + k] < sc->bmin[3 * n + k] || hi[3 * n + k] > sc->bmax[3 * n + k]) contained = 0;
+        node_w[n] = to_f_up(nw[n]);
+    }
+    *p = (float)pg;
+    free(nw); free(lo); free(hi);
+    return contained;
+}
+
+/* ---- traversal ------------------------------------------------------------------------ */
+typedef struct {
+    mv3 o, d, inv;
+    int fin, neg[3];
+    float iota, iota_b;  /* mode >= 2: far / behind scale */
+} mray;
+
+/* the product's box test: reference slab decisions (Bounds3f.h:121-153); t0/t1 = entry/exit */
+static int m_box(const float *mn, const float *mx, const mray *r, float *t0, float *t1) {
+    if (r->fin) {
+        const float ax = (mn[0] - r->o.x) * r->inv.x, bx = (mx[0] - r->o.x) * r->inv.x;
+        const float ay = (mn[1] - r->o.y) * r->inv.y, by = (mx[1] - r->o.y) * r->inv.y;
+        const float az = (mn[2] - r->o.z) * r->inv.z, bz = (mx[2] - r->o.z) * r->inv.z;
+        *t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+        *t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+        return *t0 <= *t1;
+    }
+    float bx0 = r->neg[0] ? mx[0] : mn[0], bx1 = r->neg[0] ? mn[0] : mx[0];
+    float by0 = r->neg[1] ? mx[1] : mn[1], by1 = r->neg[1] ? mn[1] : mx[1];
+    float bz0 = r->neg[2] ? mx[2] : mn[2], bz1 = r->neg[2] ? mn[2] : mx[2];
+    float tmin = (bx0 - r->o.x) * r->inv.x, tmax = (bx1 - r->o.x) * r->inv.x;
+    float tymin = (by0 - r->o.y) * r->inv.y, tymax = (by1 - r->o.y) * r->inv.y;
+    float tzmin = (bz0 - r->o.z) * r->inv.z, tzmax = (bz1 - r->o.z) * r->inv.z;
+    int miss = (tmin > tymax) || (tymin > tmax);
+    float a = (tymin > tmin) ? tymin : tmin, b = (tymax < tmax) ? tymax : tmax;
+    miss = miss || (a > tzmax) || (tzmin > b);
+    *t0 = (tzmin > a) ? tzmin : a;
+    *t1 = (tzmax < b) ? tzmax : b;
+    return !miss;
+}
+
+/* keep (visit) a box whose slab test passed; cut: mode 1 (1 + 2^-8) t_best, mode 2 t_best
+ * (1 + 2^-18 + iota P), +inf for any-hit rays.  Returns the entry key used for near-first order. */
+static int m_keep(int mode, float t0, float t1, float w, const mray *r, float cut, float *key) {
+    if (mode == 1) {
+        *key = t0;
+        return !(t1 < -1e-5f) && !(t0 > cut);
+    }
+    if (mode >= 2) {
+        const float m = w * r->iota, mb = w * r->iota_b;
+        const float e = mode == 4 ? t0 : t0 - m;
+        *key = e;
+        const int behind = mode == 3 ? t1 < -1e-5f : fmaf(t1, (float)(1.0 - CULL_SLACK), mb) < 0.f;
+        return !behind && !(e > cut);
+    }
+    *key = t0;
+    return 1;
+}
+
+static int tri_key(const or_scene *sc, int id) { return sc->tri_id ? sc->tri_id[id] : id; }
+
+/* kind 0: closest hit (index, t), kind 1: any hit (1 = occluded) */
+static int m_trace(const or_scene *sc, int mode, const float *node_w, const float *tri_w, float pg, mv3 o, mv3 d,
+                   int kind, float *tout, uint64_t *nodes) {
+    mray r;
+    r.o = o;
+    r.d = d;
+    r.inv = mv(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    r.neg[0] = r.inv.x < 0.f; r.neg[1] = r.inv.y < 0.f; r.neg[2] = r.inv.z < 0.f;
+    r.fin = fabsf(r.inv.x) < INFINITY && fabsf(r.inv.y) < INFINITY && fabsf(r.inv.z) < INFINITY;
+    const float n2 = mdot(d, d);
+    r.iota = INFINITY;
+    if (r.fin && n2 <= (float)(1.0 + 1.0 / 512.0))
+        r.iota = fmaxf(fmaxf(fabsf(r.inv.x), fabsf(r.inv.y)), fabsf(r.inv.z)) * (float)(1.0 + CULL_SLACK);
+    /* behind cut: valid only when every direction component is >= P |d| */
+    r.iota_b = r.iota * pg <= 1.0f ? r.iota : INFINITY;
+    const float cfac = (mode == 2 || mode == 3) ? fmaf(r.iota, pg, (float)(1.0 + CULL_SLACK)) : mode ? 1.0f + 1.0f / 256.0f : INFINITY;
+    float best = M_HUGE;
+    int bt = -1;
+    float cut = kind || mode == 0 ? INFINITY : best * cfac;
+    if (sc->nnodes <= 0) { *tout = best; return kind ? 0 : -1; }
+    int stack[130];
+    float skey[130];
+    int sp = 0;
+    float t0, t1, key;
+    /* root */
+    (*nodes)++;
+    if (!(m_box(sc->bmin, sc->bmax, &r, &t0, &t1) && m_keep(mode, t0, t1, node_w[0], &r, kind ? INFINITY : cut, &key))) {
+        *tout = best;
+        return kind ? 0 : -1;
+    }
+    int cur = 0;
+    for (;;) {
+        if (sc->nprims[cur] > 0) {
+            const int np = sc->nprims[cur];
+            for (int i = 0; i < np; i++) {
+                const int id = sc->offset[cur] + i;
+                if (np > 1) {  /* own box (the product's one-triangle leaves) */
+                    float mn[3], mx[3];
+                    const float *v[3] = {sc->v0 + 3 * (int64_t)id, sc->v1 + 3 * (int64_t)id, sc->v2 + 3 * (int64_t)id};
+                    for (int k = 0; k < 3; k++) {
+                        mn[k] = fminf(fminf(v[0][k], v[1][k]), v[2][k]);
+                        mx[k] = fmaxf(fmaxf(v[0][k], v[1][k]), v[2][k]);
+                    }
+                    (*nodes)++;
+                    if (!(m_box(mn, mx, &r, &t0, &t1) && m_keep(mode, t0, t1, tri_w[id], &r, cut, &key))) continue;
+                }
+                float t;
+                if (m_tri(sc, id, o, d, &t) && !(t < 0.f)) {
+                    if (kind) {
+                        if (t < M_HUGE) { *tout = t; return 1; }
+                    } else if (t < best || (t == best && bt >= 0 && tri_key(sc, id) < tri_key(sc, bt))) {
+                        best = t;
+                        bt = id;
+                        if (mode) cut = best * cfac;
+                    }
+                }
+            }
+        } else {
+            const int c[2] = {cur + 1, sc->offset[cur]};
+            int h[2];
+            float k2[2];
+            for (int j = 0; j < 2; j++) {
+                (*nodes)++;
+                h[j] = m_box(sc->bmin + 3 * (int64_t)c[j], sc->bmax + 3 * (int64_t)c[j], &r, &t0, &t1) &&
+                       m_keep(mode, t0, t1, node_w[c[j]], &r, cut, &k2[j]);
+            }
+            if (h[0] && h[1]) {
+                const int f = k2[1] < k2[0];
+                stack[sp] = c[1 - f];
+                skey[sp++] = k2[1 - f];
+                cur = c[f];
+                continue;
+            }
+            if (h[0] || h[1]) { cur = h[0] ? c[0] : c[1]; continue; }
+        }
+        /* pop the next entry still in front of the cut */
+        cur = -1;
+        while (sp > 0) {
+            sp--;
+            if (skey[sp] > cut) continue;
+            cur = stack[sp];
+            break;
+        }
+        if (cur < 0) break;
+    }
+    *tout = best;
+    return kind ? 0 : bt;
+}
+
+void or_model_trace(const or_scene *sc, int32_t n, const float *ro, const float *rd, int32_t mode,
+                    const float *node_w, const float *tri_w, float p, int32_t *tri, float *t, uint8_t *visible,
+                    uint64_t *nodes) {
+    uint64_t nn = 0;
+    for (int32_t i = 0; i < n; i++) {
+        mv3 o = mld(ro, i), d = mld(rd, i);
+        float tb;
+        const int id = m_trace(sc, mode, node_w, tri_w, p, o, d, 0, &tb, &nn);
+        tri[i] = id >= 0 ? tri_key(sc, id) : -1;
+        t[i] = tb;
+        visible[i] = (uint8_t)!m_trace(sc, mode, node_w, tri_w, p, o, d, 1, &tb, &nn);
+    }
+    *nodes = nn;
+}

@@ -90,6 +90,29 @@ def test_roofline_fields_never_exceed_one_and_bound_is_derived(tmp_path, monkeyp
         assert r[k] <= 1
 
 
+def test_extend_shade_roofline(tmp_path, monkeypatch):
+    """The metric's own fraction (extend + shade as a whole step): SURVEY 8(d) state bytes and the
+    PMC summary's HBM bytes of k_trace + k_shade + k_material per frame over the frame time."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    monkeypatch.setattr(bench, "source_hash", lambda: "abc")
+    # two frames of 64 iterations: 2.7 G rays per frame
+    st = _St(iterations=128, extend_rays=2 * 1_250_000_000, shadow_rays=2 * 730_000_000, vis_rays=2 * 720_000_000)
+    r = bench.extend_shade(st, 0.2886, 2, 2, 3)
+    state = 367 * 730_000_000 + 49 * 520_000_000 + 65 * 1_250_000_000 + 33 * 1_450_000_000
+    assert r["state_bytes_per_frame"] == state and abs(r["state_frac"] - state / 0.2886 / 8e12) < 1e-4
+    assert r["iterations_per_frame"] == 64 and r["pmc_stale"] and "traffic_frac" not in r
+    kern = {"void mcpt_dev::k_trace<2, 8>(mcpt_dev::TraceArgs)": {"hbm_bytes_per_launch": 1_970_000_000},
+            "void mcpt_dev::k_shade<false>(mcpt_dev::ShadeArgs)": {"hbm_bytes_per_launch": 2_650_000_000},
+            "void mcpt_dev::k_material<false>(mcpt_dev::ShadeArgs)": {"hbm_bytes_per_launch": 7_140_000_000}}
+    (prof / "pmc_r04.json").write_text(json.dumps({"stamp": _stamp(), "kernels": kern}))
+    r = bench.extend_shade(st, 0.2886, 2, 2, 3)
+    assert r["traffic_bytes_per_frame"] == int(11_760_000_000 * 64)
+    assert abs(r["traffic_frac"] - 11.76e9 * 64 / 0.2886 / 8e12) < 1e-4  # round 3's 0.33
+    assert r["traffic_frac"] <= 1 and r["state_frac"] <= 1
+
+
 def test_frame_and_slots_layout():
     import mcpt
 
@@ -97,7 +120,7 @@ def test_frame_and_slots_layout():
     assert bench.frame_size(rc2, 1, "weak") == (1920, 1080) and bench.frame_size(rc2, 8, "weak") == (1920, 8640)
     assert bench.frame_size(rc4, 8, "strong") == (3840, 2160)
     assert bench.BENCH_SLOTS[2] == 24 and set(bench.BENCH_SLOTS) == set(mcpt.CONFIGS)
-    assert all(1 <= s <= 64 for s in bench.BENCH_SLOTS.values())  # mcpt_set_path_slots' range
+    assert all(1 <= s <= 256 for s in bench.BENCH_SLOTS.values())  # mcpt_set_path_slots' range
     a = bench.parse(["--gpus", "4", "--config", "4", "--scaling", "strong"])
     assert (a.gpus, a.config, a.scaling, a.slots, a.steps) == (4, 4, "strong", None, 5)
 

@@ -90,3 +90,42 @@ def test_bench_layout_config2_scattered_rows(mcpt_mod, oracle, scene_c2):
         assert np.array_equal(smp[r], rs[r]), r
         ok, nbad = film_close(Ld[r:r + 1], rL[r:r + 1])
         assert ok, f"row {r}: {nbad} radiance values differ"
+
+
+@pytest.mark.parametrize("cid,tiles", [(4, [(7, 4), (3, 2)]), (5, [(8, 8)])], ids=["config4", "config5"])
+def test_full_spp_tiles_against_oracle(mcpt_mod, oracle, cid, tiles):
+    """Configs 4 and 5 at their full sample counts -- 1024 spp depth 8, 4096 spp depth 12 -- at the
+    bench's path slots (16: every slot renders 64 / 256 samples, sample indices up to 4095 keyed
+    into the RNG, wavefront_kernels.cu:124,219-222) on whole 256 x 256 tiles (mcpt_set_tiles), one
+    row of each tile against the oracle (the one tile alone: part=(tx + ty, a modulus larger than
+    any tx + ty))."""
+    rc = mcpt_mod.CONFIGS[cid]
+    scene = mcpt_mod.build_config_scene(cid)
+    arrays = scene.arrays()
+    cam = mcpt_mod.config_camera(rc)
+    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=rc.spp, max_depth=rc.max_depth))
+    pt.upload_scene(scene)
+    pt.set_camera(cam)
+    pt.set_path_slots(bench.BENCH_SLOTS[cid])
+    pt.resize(rc.width, rc.height)
+    pt.set_tiles(tiles)
+    t0 = time.perf_counter()
+    st = pt.render()
+    t_gpu = time.perf_counter() - t0
+    Ld, smp = pt.film()
+    pt.close()
+    big = rc.width // 256 + rc.height // 256 + 2
+    for tx, ty in tiles:
+        assert np.all(smp[ty * 256:(ty + 1) * 256, tx * 256:(tx + 1) * 256] == rc.spp)
+        r = ty * 256 + 128
+        t0 = time.perf_counter()
+        rL, rs, cnt = oracle.render(arrays, cam, rc.width, rc.height, rc.spp, rc.max_depth, rows=(r, r + 1),
+                                    part=(tx + ty, big))
+        t_cpu = time.perf_counter() - t0
+        cols = slice(tx * 256, (tx + 1) * 256)
+        assert np.array_equal(smp[r, cols], rs[r, cols]) and rs[r].sum() == 256 * rc.spp
+        ok, nbad = film_close(Ld[r, cols], rL[r, cols])
+        assert ok, f"config {cid} tile {(tx, ty)} row {r}: {nbad} radiance values differ"
+        assert Ld[r, cols].max() > 0
+        print(f"config {cid} tile {(tx, ty)} row {r}: {rc.spp} spp, {cnt['extend_rays']} oracle extension rays "
+              f"({t_cpu:.1f} s); GPU tiles {t_gpu:.2f} s, {st.rays} rays")

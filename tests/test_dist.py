@@ -129,3 +129,76 @@ def test_bench_gpus_flag_refuses_mismatched_world(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+
+
+def _gather_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        W, H, T = 300, 70, 256  # 2 x 1 tiles over 3 ranks: rank 2 owns none
+        tiles = parallel.tiles_for_rank(rank, world, W, H, T)
+        local = torch.full((len(tiles) * T * T, 4), float(rank + 1))
+        parts = parallel.gather_packed_to_root(local, rank, world, dist, W, H, T)
+        # a collective after the gather must see no stray point-to-point message
+        x = torch.tensor([rank + 1.0])
+        dist.all_reduce(x)
+        dist.barrier()
+        if rank == 0:
+            q.put(([tuple(p.shape) for p in parts], [float(p[0, 0]) if len(p) else None for p in parts], float(x)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_with_an_empty_rank_gloo_world3():
+    """More ranks than tiles: the rank without tiles sends nothing and rank 0 posts no receive for
+    it (an unmatched send hangs RCCL or leaves a stray gloo message); a collective
+    right after the gather completes with every rank's value."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    shapes, firsts, total = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+    assert shapes == [(65536, 4), (65536, 4), (0, 4)]
+    assert firsts == [1.0, 2.0, None] and total == 6.0
+
+
+def test_strong_split_slots():
+    """--scaling strong / the strong section of an N>1 run: path slots grow with the ranks so every
+    GPU keeps the one-GPU run's paths in flight, bounded by spp and by the per-GPU state budget
+    (the film is allocated for the whole frame on every rank); one value for all ranks."""
+    import bench
+
+    assert parallel.strong_slots(24, 1, 1920, 1080, 256) == 24
+    assert parallel.strong_slots(24, 2, 1920, 1080, 256) == 48
+    s8 = parallel.strong_slots(24, 8, 1920, 1080, 256)
+    assert 24 < s8 <= 192 and s8 * 1920 * 1080 * parallel.PATH_BYTES <= parallel.SLOT_BUDGET_BYTES
+    assert parallel.strong_slots(16, 8, 3840, 2160, 1024) * 3840 * 2160 * parallel.PATH_BYTES <= parallel.SLOT_BUDGET_BYTES
+    assert parallel.strong_slots(16, 8, 256, 256, 16) == 16  # spp bound: a slot renders at least one sample
+    a = bench.parse(["--gpus", "8", "--no-gather"])
+    assert a.no_gather and not a.no_strong and not a.no_verify_gather and a.scaling == "weak"
+
+
+def test_multi_gpu_tile_balances_pixels():
+    """bench.py's multi-GPU partition uses 64 x 64 film tiles (MULTI_TILE): every rank's pixel
+    count is within 2 % of the mean at N = 2 / 4 / 8 on the 1080p frame and on config 4's 4K frame
+    (with 256 x 256 tiles a 1080p rank at N = 8 owns 5 tiles, one diagonal; the time spread the
+    one-GPU rehearsal measured was 1.74x, profiles/partition_r04.json)."""
+    import bench
+
+    T = bench.MULTI_TILE
+    for W, H in ((1920, 1080), (3840, 2160)):
+        for world in (2, 4, 8):
+            counts = [sum(min(T, W - tx * T) * min(T, H - ty * T) for tx, ty in
+                          parallel.tiles_for_rank(r, world, W, H, T)) for r in range(world)]
+            assert sum(counts) == W * H and max(counts) / (W * H / world) < 1.02
+    assert bench.part_tile(1) == 256 and bench.part_tile(8) == T

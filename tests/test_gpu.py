@@ -168,6 +168,7 @@ def test_config2_1080p_band_parity_and_properties(mcpt_mod, oracle, scene_c2):
     W, H = rc.width, rc.height
     cam = mcpt_mod.config_camera(rc)
     pt = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, rc.max_depth)
+    pt.set_work_counters(True)  # the counting k_trace build: same hits, StageStats work counters filled
     st = pt.render()
     Ld, smp = pt.film()
     assert np.all(smp[:-1, :-1] == 2) and np.all(smp[-1] == 0) and np.all(smp[:, -1] == 0)

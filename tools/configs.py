@@ -35,6 +35,7 @@ for c in [int(x) for x in args.configs.split(",")]:
     a = scene.arrays()
     pt = mcpt.PathTracer(0, mcpt.default_config(spp=rc.spp, max_depth=rc.max_depth))
     pt.upload_scene(scene)
+    pt.set_work_counters(True)  # StageStats node / test counts
     pt.set_camera(mcpt.config_camera(rc))
     P = rc.width * rc.height
     S = AUTO_SLOTS.get(c, 1) if args.slots == "auto" else int(args.slots)

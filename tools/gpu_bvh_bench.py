@@ -17,8 +17,10 @@ for c in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "2,3,5").split(
     for b in ("sah", "ploc", "lbvh"):
         gpu = False if b == "sah" else b
         pt.upload_scene(s, gpu_bvh=gpu)
+        pt.set_work_counters(True)  # StageStats node / test counts
         if gpu:
-            pt.upload_scene(s, gpu_bvh=gpu)  # second build: warm
+            pt.upload_scene(s, gpu_bvh=gpu)
+            pt.set_work_counters(True)  # StageStats node / test counts  # second build: warm
             r[f"gpu_{b}_build_ms"] = round(pt.last_build_ms, 2)
         pt.set_camera(mcpt.config_camera(rc)); pt.resize(rc.width, rc.height)
         pt.iterate(20)

@@ -1,0 +1,75 @@
+"""Multi-GPU rehearsal on one GPU: render each rank's tile partition alone and time it.
+
+For N in (2, 4, 8), rank r's share of the frame -- the tiles with (tx + ty) mod N == r -- is
+rendered to the config's spp with the strong split's path slots (mcpt/parallel.py strong_slots),
+one rank after the other on one device.  The slowest partition sets an N-GPU frame's time, so
+max / mean of the per-rank times is the strong split's load imbalance.
+Tile sizes 256 (the reference's Film tile, Film.cu:17) and 128 / 64 are compared: results do not
+depend on the tiling (keyed RNG), only the balance does.
+
+Usage: python tools/partition_rehearsal.py [--configs 2 4] [--tiles 256 128] [--out profiles/partition_r04.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "mc-path-tracer_amd"))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", type=int, nargs="+", default=[2, 4])
+    ap.add_argument("--tiles", type=int, nargs="+", default=[256, 128, 64])
+    ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "partition_r04.json"))
+    args = ap.parse_args()
+    import mcpt
+    from mcpt import parallel
+
+    import bench
+
+    res = {"what": __doc__.split("\n\n")[1].replace("\n", " "), "runs": []}
+    for cid in args.configs:
+        rc = mcpt.CONFIGS[cid]
+        scene = mcpt.build_config_scene(cid)
+        cam = mcpt.config_camera(rc)
+        pt = mcpt.PathTracer(0, mcpt.default_config(spp=rc.spp, max_depth=rc.max_depth))
+        pt.upload_scene(scene)
+        pt.set_camera(cam)
+        W, H = rc.width, rc.height
+        for world in args.worlds:
+            slots = parallel.strong_slots(bench.BENCH_SLOTS[cid], world, W, H, rc.spp)
+            pt.set_path_slots(slots)
+            for tile in args.tiles:
+                pt.resize(W, H, tile, tile)
+                ms, rays, px = [], [], []
+                for r in range(world):
+                    tiles = parallel.tiles_for_rank(r, world, W, H, tile)
+                    pt.set_tiles(tiles)
+                    if r == 0:  # warmup: the first launches of this slot / tile layout
+                        pt.clear()
+                        pt.render()
+                    pt.clear()
+                    t0 = time.perf_counter()
+                    st = pt.render()
+                    ms.append((time.perf_counter() - t0) * 1e3)
+                    rays.append(st.rays)
+                    px.append(sum(min(tile, W - tx * tile) * min(tile, H - ty * tile) for tx, ty in tiles))
+                mean = sum(ms) / len(ms)
+                run = {"config": cid, "frame": [W, H], "spp": rc.spp, "world": world, "tile": tile, "slots": slots,
+                       "per_rank_ms": [round(x, 2) for x in ms], "per_rank_pixels": px, "per_rank_rays": rays,
+                       "max_over_mean": round(max(ms) / mean, 4), "ideal_ms": round(mean, 2),
+                       "max_ms": round(max(ms), 2)}
+                res["runs"].append(run)
+                print(json.dumps(run), flush=True)
+        pt.close()
+    with open(args.out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -50,7 +50,7 @@ cfg = int(os.environ.get("PMC_CONFIG", "2"))
 out = {"round": tag, "stamp": {"source_hash": bench.source_hash(), "config": cfg,
                                "slots": int(os.environ.get("PMC_SLOTS", str(bench.BENCH_SLOTS[cfg]))),
                                "step": bench.STEP},
-       "source": f"tools/pmc_trace.sh {label}: rocprofv3 --pmc passes (one counter group each) over "
+       "source": f"tools/gpu/run.sh pmc ({label}): rocprofv3 --pmc passes (one counter group each) over "
                  f"'python3 {os.environ.get('PROG', 'bench.py')}'",
        "formulas": __doc__.split("\n\n")[1].strip(), "kernels": out_k}
 name = os.environ.get("PMC_NAME", f"pmcdetail_{tag}")
