@@ -168,6 +168,7 @@ public:
     }
     void set_texture_filepath(const std::string& path) {
         path_ = path;
+        ++tex_rev_;  // re-read even for the same path: the file may have changed on disk
         notify();
     }
     std::string get_texture_filepath() const { return path_; }
@@ -177,11 +178,16 @@ public:
     // instead of on the host; bit-identical tables, for large maps.
     void set_device_tables(bool on) {
         device_tables_ = on;
+        ++tex_rev_;
         notify();
     }
     bool get_device_tables() const { return device_tables_; }
+    // Bumped by the edits that change the texture or its tables (path, table source) and not by
+    // set_ls / set_color / set_type, which Scene::desc applies without re-reading the .hdr.
+    uint64_t texture_revision() const { return tex_rev_; }
 
 private:
+    uint64_t tex_rev_ = 0;
     EnvironmentLightType type_ = Color;
     std::string path_;
     bool device_tables_ = false;
@@ -263,11 +269,12 @@ public:
     // The returned desc points into this Scene and `dir_params`; valid until the next edit.
     mcpt_scene_desc desc(std::vector<float>& dir_params) {
         const EnvironmentLight& env = *environment_light;
-        // The .hdr is (re)read only when the texture path or the table source changed: the other
-        // env edits (set_ls, set_color, set_type) only change the fields desc() fills in below.
-        // The env arrays live beside the BVH in the builder, so an env reload never rebuilds
-        // the geometry (built_ stays tied to geometry and BVH-parameter edits).
-        const std::pair<std::string, bool> env_key{env.get_texture_filepath(), env.get_device_tables()};
+        // The .hdr is (re)read when the light object or its texture revision changed (a path or
+        // table-source edit, the same path set again included): the other env edits (set_ls,
+        // set_color, set_type) only change the fields desc() fills in below.  The env arrays
+        // live beside the BVH in the builder, so an env reload never rebuilds the geometry
+        // (built_ stays tied to geometry and BVH-parameter edits).
+        const std::pair<int, uint64_t> env_key{env.get_id(), env.texture_revision()};  // ids are never reused
         if (!proxy_env_ && env.get_light_type() == HRDI && (!env_loaded_ || env_key != env_built_)) {
             if (env.get_texture_filepath().empty()) throw Error(MCPT_E_INVALID, "EnvironmentLight: HRDI without a texture");
             detail::check(mcpt_scene_set_env_hdr_ex(s_, env.get_texture_filepath().c_str(), 1,
@@ -311,7 +318,7 @@ private:
     mcpt_scene* s_;
     bool built_ = false;
     bool proxy_env_ = false;  // make_proxy set the environment (until set_environment_light)
-    std::pair<std::string, bool> env_built_{std::string(), false};  // texture path, device tables
+    std::pair<int, uint64_t> env_built_{-1, 0};  // light id, texture revision
     bool env_loaded_ = false;
     mcpt_bvh_params bvh_{MCPT_BVH_SAH3, 8, 128, 0.5f, 1.0f};
 };

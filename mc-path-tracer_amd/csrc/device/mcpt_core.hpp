@@ -352,10 +352,14 @@ struct EnvView {
     float color[3];
     float ls;
     int w, h;
-    const float4* tex;        // RGBA32F, row 0 = top (stbi_loadf, no flip: dTexture.cu:208)
+    // RGB32F + pdf, row 0 = top (stbi_loadf, no flip: dTexture.cu:208).  The device copy's
+    // alpha plane, which env_L never reads (tex2DLod<float4>(...).xyz, EnvironmentLight.cu:45),
+    // holds the pdf table (k_env_pack): a BRDF sample's pdf texel then shares the bilinear
+    // taps' lines, and the light's tables are 0.5 MiB smaller for the per-XCD L2.
+    const float4* tex;
     const float* marginal_y;  // h
     const float* conds_y;     // h*w
-    const float* pdf;         // h*w
+    const float* pdf;         // h*w (readback only: the shading kernels read tex[i].w)
     // Optional search guides (device only, built at upload when the CDFs are
     // sorted): guide_m[k] = upper_bound(marginal_y, h, k / kEnvGuide), k = 0..kEnvGuide,
     // and the same per conditional row at guide_c[y * (kEnvGuide + 1) + k].  16-bit
@@ -458,7 +462,7 @@ MCPT_HD float env_pdf_uv(const EnvView& e, float u, float v) {
         px = (fx == fx && fx >= 0.f && fx < (float)e.w) ? (int)fx : 0;
         py = (fy == fy && fy >= 0.f && fy < (float)e.h) ? (int)fy : 0;
     }
-    float pdf = e.pdf[(int64_t)py * e.w + px];
+    float pdf = e.tex[(int64_t)py * e.w + px].w;
     float sin_theta = dsin(PI_F * v);
     if (sin_theta == 0.f) return 0.f;
     return pdf * (float)((unsigned)e.w * (unsigned)e.h) / (((2.f * sin_theta) * PI_F) * PI_F);
@@ -811,7 +815,8 @@ MCPT_HD bool tri_test_t(V3 o, V3 d, V3 p0, V3 e1, V3 e2, float& t) {
 //   w <= W'_T + (beta_T / (1 - sqrt3 beta_T)) |d| t,   W'_T = (omega_T + beta_T diam_T) / (1 - sqrt3 beta_T).
 // A box's margin W is the largest W'_T of the triangles under it (+inf when one has sqrt3 beta_T
 // >= 1/2: a triangle so large against the det threshold that nothing near it is ever culled); P
-// is the scene's largest beta_T / (1 - sqrt3 beta_T).  With iota = max_a |1 / d_a| (1 + 2^-18), a
+// is the scene's largest (1 + 2^-9) beta_T / (1 - sqrt3 beta_T) (|d| <= 1 + 2^-10).  Triangles in an
+// axis plane have a bound without the threshold (cull_plane_b).  With iota = max_a |1 / d_a| (1 + 2^-18), a
 // box is skipped when
 //   behind:  t1 (1 - 2^-18) + W iota < 0      (only if iota P <= 1: the exit axis is not grazing)
 //   beyond:  t0 - W iota > t_best (1 + 2^-18 + iota P)     (closest hit only)
@@ -829,20 +834,57 @@ MCPT_HD double cull_beta(V3 e1, V3 e2) {
 }
 // true when no box holding the triangle may be culled (sqrt3 beta_T >= 1/2)
 MCPT_HD bool cull_unbounded(double beta) { return !(1.7321 * beta * kCullSlackD < 0.5); }
-// W'_T of a triangle record (+inf when unbounded), in double; far: its contribution to P
-MCPT_HD double cull_tri_margin(V3 e1, V3 e2, double* far) {
-    const double beta = cull_beta(e1, e2);
+MCPT_HD double cull_norm(V3 e) { return __builtin_sqrt((double)e.x * e.x + (double)e.y * e.y + (double)e.z * e.z); }
+// Axis-plane triangles (e1_a = e2_a = 0 for some axis a: walls, floors, the quads of boxes).  The
+// products that carry e1_a or e2_a are exact zeros, and each dot-of-cross error is then a multiple
+// of the same factor as the exact value: with G = the in-plane cross product of e1 and e2 and S =
+// the sum of its two products' magnitudes, |det - d_a G| <= c |d_a| S and |N - tvec_a G| <= c
+// |tvec_a| S (c = 5.0001 u), so det >= d_a (|G| - c S) = d_a G' and |tvec_a| <= |N| / G': the
+// quotients d_a / det and tvec_a / det are bounded by 1 / G' and |t| / G' without the 1e-6
+// threshold.  Carried through R:
+//   w <= omega_T + 1.01 u |tvec| + b_T (|tvec| + |t| |d|),   b_T = 15.0003 u |e1| |e2| / G'
+// -- a few u for a right-angled half of a quad, where the general bound is unbounded above an
+// edge product of ~0.17.  Returns b_T, or 0 when the triangle does not lie in an axis plane or is
+// too thin (G' < G / 2: then the general bound applies).
+MCPT_HD double cull_plane_b(V3 e1, V3 e2) {
+    double a1, a2, c1, c2;  // the in-plane components of e1 and e2
+    if (e1.x == 0.f && e2.x == 0.f) {
+        a1 = e1.y; c1 = e1.z; a2 = e2.y; c2 = e2.z;
+    } else if (e1.y == 0.f && e2.y == 0.f) {
+        a1 = e1.z; c1 = e1.x; a2 = e2.z; c2 = e2.x;
+    } else if (e1.z == 0.f && e2.z == 0.f) {
+        a1 = e1.x; c1 = e1.y; a2 = e2.x; c2 = e2.y;
+    } else {
+        return 0.0;
+    }
+    // float x float products are exact in double; one rounding in the difference and the sum
+    const double g = __builtin_fabs(a1 * c2 - c1 * a2) * (1.0 - 1.0 / 1099511627776.0);
+    const double sg = (__builtin_fabs(a1 * c2) + __builtin_fabs(c1 * a2)) * (1.0 + 1.0 / 1099511627776.0);
+    const double gp = g - 5.0002 * kCullU * sg;
+    if (!(gp > 0.5 * g)) return 0.0;
+    return 15.0003 * kCullU * cull_norm(e1) * cull_norm(e2) * (1.0 + 1e-12) / gp;
+}
+// W'_T of a triangle record (+inf when unbounded), in double; far: its contribution to P (the
+// coefficient of t_best in the far cut).  General triangles: w <= omega + beta |o - p0| with
+// |o - p0| <= t |d| + sqrt3 w + diam (header above).  Axis-plane triangles (cull_plane_b): beta =
+// (1.01 u + b)(1 + u), and the extra b |t| |d| adds b to the far coefficient.
+MCPT_HD double cull_tri_margin(V3 e1, V3 e2, double* far, bool plane = true) {
+    const double b = plane ? cull_plane_b(e1, e2) : 0.0;
+    const double beta = b > 0.0 ? (1.01 * kCullU + b) * (1.0 + 1.0 / 8388608.0) : cull_beta(e1, e2);
     *far = 0.0;
     if (cull_unbounded(beta)) return __builtin_huge_val();
     const V3 e3 = v3(e2.x - e1.x, e2.y - e1.y, e2.z - e1.z);
-    const double n1 = __builtin_sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
-    const double n2 = __builtin_sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
-    const double n3 = __builtin_sqrt((double)e3.x * e3.x + (double)e3.y * e3.y + (double)e3.z * e3.z) * (1.0 + 1e-7);
+    const double n1 = cull_norm(e1), n2 = cull_norm(e2), n3 = cull_norm(e3) * (1.0 + 1e-7);
     const double diam = n1 > n2 ? (n1 > n3 ? n1 : n3) : (n2 > n3 ? n2 : n3);
     const double omega = 2.1 * kCullU * (n1 > n2 ? n1 : n2);
     const double den = 1.0 - 1.7321 * beta * kCullSlackD;
-    *far = beta / den * kCullSlackD * (1.0 + 1.0 / 1048576.0);
+    // |d| <= 1 + 2^-10 turns the t |d| term into t: the (1 + 2^-9) factor
+    *far = (b > 0.0 ? beta + b : beta) * (1.0 + 1.0 / 512.0) / den * kCullSlackD * (1.0 + 1.0 / 1048576.0);
     return (omega + beta * diam * (1.0 + 1e-12)) * kCullSlackD / den;
+}
+MCPT_HD bool cull_tri_unbounded(V3 e1, V3 e2, bool plane = true) {
+    double far;
+    return !(cull_tri_margin(e1, e2, &far, plane) < __builtin_huge_val());
 }
 // double -> float rounded up (twice 2^-20 covers the conversion's rounding)
 MCPT_HD float cull_to_float_up(double w) {

@@ -849,19 +849,21 @@ int Scene::build(const mcpt_bvh_params& prm, std::string& err) {
         // MCPT_BVH_THREADS: worker threads for the subtrees (default min(16, cores); 1 = sequential)
         int nth = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
         if (const char* e = std::getenv("MCPT_BVH_THREADS")) nth = std::max(1, std::atoi(e));
-        // SAH3: triangles whose boxes the traversal may never cull (mcpt_core.hpp cull_unbounded:
-        // large against the det >= 1e-6 threshold, e.g. walls and ground quads) get a subtree of
+        // SAH3: triangles whose boxes the traversal may never cull (mcpt_core.hpp cull_tri_margin:
+        // large against the det >= 1e-6 threshold and not in an axis plane) get a subtree of
         // their own under the root.  Every ancestor of such a triangle is unbounded too, so mixed
         // into the tree they would keep whole subtrees of small triangles from being culled
         // (config 2's ten wall triangles sat under 7 interior nodes).  MCPT_BVH_ISOLATE=0: off.
         int nbig = 0;
         if (bld.mode == 1) {
             const char* iso = std::getenv("MCPT_BVH_ISOLATE");
+            const char* pl = std::getenv("MCPT_CULL_PLANE");  // as runtime.cpp's margins
+            const bool plane = !(pl && pl[0] == '0' && pl[1] == 0);
             if (!(iso && iso[0] == '0' && iso[1] == 0)) {
                 auto unbounded = [&](const PrimInfo& p) {
                     const V3* P = tris[(size_t)p.prim].p;
                     const V3 e1 = P[1] - P[0], e2 = P[2] - P[0];  // as the triangle record stores them
-                    return mcpt::cull_unbounded(mcpt::cull_beta(e1, e2));
+                    return mcpt::cull_tri_unbounded(e1, e2, plane);
                 };
                 auto it = std::stable_partition(info.begin(), info.end(), unbounded);
                 nbig = (int)(it - info.begin());

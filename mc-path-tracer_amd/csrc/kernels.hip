@@ -273,10 +273,10 @@ __device__ inline uint32_t occ_index(const DevScene& sc, V3 o, V3 d) {
     return ((((cz * G + cy) * G + cx) * 6u + face) * B + ub) * B + vb;
 }
 
-// true: (o, d) (reciprocal inv, all finite; signed culling scale io) is occluded by triangle record
-// w0..w2 under its leaf box (bmn.w: the leaf's margin)
-__device__ inline bool occ_test(V3 o, V3 d, V3 inv, float io, float4 bmn, float4 bmx, float4 w0, float4 w1,
-                                float4 w2) {
+// true: (o, d) (reciprocal inv, all finite; signed culling scale io) is occluded by the triangle of
+// occluder record r0..r3 (kOccRecF4: {leaf box mn, margin} {leaf box mx, v0.x} {v0.yz, e1.xy}
+// {e1.z, e2}) under its leaf box
+__device__ inline bool occ_test(V3 o, V3 d, V3 inv, float io, float4 bmn, float4 bmx, float4 r2, float4 r3) {
     // pair_slab's arithmetic for one box (its first lane)
     const float ax = (bmn.x - o.x) * inv.x, bx = (bmx.x - o.x) * inv.x;
     const float ay = (bmn.y - o.y) * inv.y, by = (bmx.y - o.y) * inv.y;
@@ -288,39 +288,40 @@ __device__ inline bool occ_test(V3 o, V3 d, V3 inv, float io, float4 bmn, float4
     float key;
     if (!(t0 <= t1) || !keep_box(t0, t1, bmn.w * io, K_INF_F, key)) return false;  // k_trace's any-hit cull
     float th;
-    return tri_test_t(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), th) && !(th < 0.f) &&
+    return tri_test_t(o, d, v3(bmx.w, r2.x, r2.y), v3(r2.z, r2.w, r3.x), v3(r3.y, r3.z, r3.w), th) && !(th < 0.f) &&
            th < K_HUGE;
 }
 // The cell's entries of (o, d): kOccWays triangle records (k_trace writes way tri mod kOccWays)
 __device__ inline uint2 occ_entry(const DevScene& sc, V3 o, V3 d) {
     return reinterpret_cast<const uint2*>(sc.occ)[occ_index(sc, o, d)];
 }
-// Both any-hit rays of a path against their cells' entries: all four candidates' leaf boxes and
-// records are fetched in one round trip (an empty way reads record 0 and is not tested).
+// Both any-hit rays of a path against their cells' entries: all four candidates' occluder records
+// (leaf box, margin and triangle in one aligned 64-B record: one half line each, where the leaf
+// box and the 48-B triangle record used to cost two or three) are fetched in one round trip (an
+// empty way reads record 0 and is not tested).
 __device__ inline void occ_hit2(const DevScene& sc, V3 ol, V3 dl, uint2 el, V3 ob, V3 db, uint2 eb, bool& hl,
                                 bool& hb) {
     hl = hb = false;
     const bool v0 = el.x < sc.ntri, v1 = el.y < sc.ntri, v2 = eb.x < sc.ntri, v3_ = eb.y < sc.ntri;
     if (!(v0 || v1 || v2 || v3_)) return;
     const uint32_t t[4] = {v0 ? el.x : 0u, v1 ? el.y : 0u, v2 ? eb.x : 0u, v3_ ? eb.y : 0u};
-    float4 bn[4], bx[4], r0[4], r1[4], r2[4];
+    float4 bn[4], bx[4], r2[4], r3[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        bn[k] = sc.leaf_box[2 * t[k]];
-        bx[k] = sc.leaf_box[2 * t[k] + 1];
-        const float4* p = sc.tri + kTriF4 * t[k];
-        r0[k] = p[0];
-        r1[k] = p[1];
+        const float4* p = sc.occ_rec + kOccRecF4 * (size_t)t[k];
+        bn[k] = p[0];
+        bx[k] = p[1];
         r2[k] = p[2];
+        r3[k] = p[3];
     }
     const V3 il = v3(1.f / dl.x, 1.f / dl.y, 1.f / dl.z), ib = v3(1.f / db.x, 1.f / db.y, 1.f / db.z);  // k_trace's
     const bool fl = __builtin_fabsf(il.x) < K_INF_F && __builtin_fabsf(il.y) < K_INF_F && __builtin_fabsf(il.z) < K_INF_F;
     const bool fb = __builtin_fabsf(ib.x) < K_INF_F && __builtin_fabsf(ib.y) < K_INF_F && __builtin_fabsf(ib.z) < K_INF_F;
     const float iol = cull_iota(sc, dl, il), iob = cull_iota(sc, db, ib);
-    hl = fl && ((v0 && occ_test(ol, dl, il, iol, bn[0], bx[0], r0[0], r1[0], r2[0])) ||
-                (v1 && occ_test(ol, dl, il, iol, bn[1], bx[1], r0[1], r1[1], r2[1])));
-    hb = fb && ((v2 && occ_test(ob, db, ib, iob, bn[2], bx[2], r0[2], r1[2], r2[2])) ||
-                (v3_ && occ_test(ob, db, ib, iob, bn[3], bx[3], r0[3], r1[3], r2[3])));
+    hl = fl && ((v0 && occ_test(ol, dl, il, iol, bn[0], bx[0], r2[0], r3[0])) ||
+                (v1 && occ_test(ol, dl, il, iol, bn[1], bx[1], r2[1], r3[1])));
+    hb = fb && ((v2 && occ_test(ob, db, ib, iob, bn[2], bx[2], r2[2], r3[2])) ||
+                (v3_ && occ_test(ob, db, ib, iob, bn[3], bx[3], r2[3], r3[3])));
 }
 
 // ---------------------------------------------------------------------------
@@ -1275,6 +1276,15 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     }
 }
 
+// The env texture's device copy takes the pdf table into its alpha plane (EnvView::tex)
+__global__ void k_env_pack(float4* tex, const float* __restrict__ pdf, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) tex[i].w = pdf[i];
+}
+void launch_env_pack(float4* tex, const float* pdf, size_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_env_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tex, pdf, n);
+}
+
 // Light-sample table of an HRDI env light (EnvView::ltab / lrow / lcol): entry (y, x + 1)
 // holds env_L / env_pdf at the direction env_dir returns for cell (x, y) -- computed by the
 // very functions the per-sample path calls, so the values are the same -- and the row /
@@ -1617,14 +1627,19 @@ int trace_profile(unsigned long long* out, int reset) {
     (void)reset;
     return 0;
 }
-__global__ void k_leaf_boxes(DevScene sc, uint32_t nnodes, float4* out) {  // see launch_leaf_boxes
+__global__ void k_occ_records(DevScene sc, uint32_t nnodes, float4* out) {  // see launch_occ_records
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     auto put = [&](int ref, float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float w) {
         if (ref >= 0 || ref == kEnd) return;
         const uint32_t off = (uint32_t)ref & 0xffffffu, cnt = (((uint32_t)ref >> 24) & 7u) + 1u;
         for (uint32_t k = off; k < off + cnt && k < sc.ntri; k++) {
-            out[2 * k] = make_float4(mnx, mny, mnz, w);  // .w: the leaf's culling margin
-            out[2 * k + 1] = make_float4(mxx, mxy, mxz, 0.f);
+            const float4* tr = sc.tri + kTriF4 * (size_t)k;  // (v0.xyz, e1.x) (e1.yz, e2.xy) (e2.z, ...)
+            const float4 a = tr[0], b = tr[1], c = tr[2];
+            float4* o = out + kOccRecF4 * (size_t)k;
+            o[0] = make_float4(mnx, mny, mnz, w);  // .w: the leaf's culling margin
+            o[1] = make_float4(mxx, mxy, mxz, a.x);
+            o[2] = make_float4(a.y, a.z, a.w, b.x);
+            o[3] = make_float4(b.y, b.z, b.w, c.x);
         }
     };
     if (i == 0 && sc.root_ref < 0)  // the whole tree is one leaf: its box is the root box
@@ -1648,13 +1663,13 @@ __global__ void k_leaf_boxes(DevScene sc, uint32_t nnodes, float4* out) {  // se
 
 // Culling margins (mcpt_core.hpp "conservative box culling").  k_cull_tri: W'_T of every triangle
 // record (float, rounded up) and the far coefficient P (positive floats order as their bits).
-__global__ void k_cull_tri(const float4* tri, uint32_t ntri, float* tw, uint32_t* pmax) {
+__global__ void k_cull_tri(const float4* tri, uint32_t ntri, float* tw, uint32_t* pmax, int plane) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ntri) return;
     const float4* r = tri + kTriF4 * (size_t)i;
     const float4 r0 = r[0], r1 = r[1], r2 = r[2];
     double far;
-    tw[i] = cull_to_float_up(cull_tri_margin(v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), &far));
+    tw[i] = cull_to_float_up(cull_tri_margin(v3(r0.w, r1.x, r1.y), v3(r1.z, r1.w, r2.x), &far, plane != 0));
     if (far > 0.0) atomicMax(pmax, __float_as_uint(cull_to_float_up(far)));
 }
 // One bottom-up pass over child-pair nodes: each child's word (q3.z / q3.w) = the largest W'_T
@@ -1689,15 +1704,15 @@ __global__ void k_cull_zero(float4* nodes, uint32_t npairs) {
     nodes[4 * (size_t)i + 3] = q3;
 }
 void launch_cull_margins(float4* nodes, uint32_t npairs, const float4* tri, uint32_t ntri, float* tri_w,
-                         uint32_t* pmax, int passes, hipStream_t s) {
-    if (ntri) hipLaunchKernelGGL(k_cull_tri, dim3((ntri + 255) / 256), dim3(256), 0, s, tri, ntri, tri_w, pmax);
+                         uint32_t* pmax, int passes, bool plane, hipStream_t s) {
+    if (ntri) hipLaunchKernelGGL(k_cull_tri, dim3((ntri + 255) / 256), dim3(256), 0, s, tri, ntri, tri_w, pmax, plane ? 1 : 0);
     if (!npairs) return;
     hipLaunchKernelGGL(k_cull_zero, dim3((npairs + 255) / 256), dim3(256), 0, s, nodes, npairs);
     for (int p = 0; p < passes; p++)
         hipLaunchKernelGGL(k_cull_pairs, dim3((npairs + 255) / 256), dim3(256), 0, s, nodes, npairs, tri_w, ntri);
 }
-void launch_leaf_boxes(const DevScene& sc, uint32_t nnodes, float4* leaf_box, hipStream_t s) {
-    hipLaunchKernelGGL(k_leaf_boxes, dim3(nnodes / 256 + 1), dim3(256), 0, s, sc, nnodes, leaf_box);
+void launch_occ_records(const DevScene& sc, uint32_t nnodes, float4* rec, hipStream_t s) {
+    hipLaunchKernelGGL(k_occ_records, dim3(nnodes / 256 + 1), dim3(256), 0, s, sc, nnodes, rec);
 }
 void launch_clear(const ClearArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_clear, dim3((a.n + 255) / 256), dim3(256), 0, s, a);

@@ -84,7 +84,8 @@ struct DevScene {
     mcpt::EnvView env;
     // Any-hit occluder cache: occ[kOccWays i + w] is a triangle record
     // that occluded an any-hit ray of cell i (origin cell of the root box x direction bin), or
-    // kOccEmpty; leaf_box[2t] / [2t + 1] are mn / mx of the BVH leaf box that holds record t.
+    // kOccEmpty; occ_rec[kOccRecF4 t ..] is triangle t's occluder record: the box of the BVH leaf
+    // that holds it with that leaf's culling margin, and the triangle (v0, e1, e2), 64 B.
     // k_material tests an any-hit ray against its cell's triangle under that leaf box first:
     // a hit there is one the traversal would find too, so the ray is resolved as occluded.
     // occ == nullptr: off.
@@ -95,12 +96,12 @@ struct DevScene {
     // so the next lookups meet a fresh table.  [1] backoff: 3, 7, 15, ... 255 after consecutive
     // failed lookup iterations, 0 while they pay.
     uint32_t* occ_gate;
-    const float4* leaf_box;
+    const float4* occ_rec;
     uint32_t ntri;
     int occ_g, occ_b;       // origin cells per axis, direction bins per face coordinate
     float occ_inv[3];       // occ_g / root box extent, per axis
     // Conservative culling (mcpt_core.hpp "conservative box culling"): every node holds each
-    // child's margin W (pair nodes: q3.z / q3.w; 4-wide nodes: float4 7; leaf_box[2t].w), P is the
+    // child's margin W (pair nodes: q3.z / q3.w; 4-wide nodes: float4 7; occ_rec[4t].w), P is the
     // scene's far coefficient, root_w the root box's margin.  cull_ok = 0 (a caller BVH whose boxes
     // do not contain their triangles, or MCPT_CULL=0): nothing is culled.
     float cull_p, root_w;
@@ -216,14 +217,19 @@ void launch_shade_stage(bool material_stage, const ShadeArgs& a, int nblocks, co
                         hipStream_t s);
 void launch_trace(const TraceArgs& a, const LaunchGeom& g, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
-// leaf_box[2t], [2t + 1] = the box of the leaf that holds triangle record t (nodes: nnodes nodes
-// of the given width; a root that is itself a leaf gets the root box); leaf_box[2t].w = its margin
-void launch_leaf_boxes(const DevScene& sc, uint32_t nnodes, float4* leaf_box, hipStream_t s);
+// Occluder records (DevScene::occ_rec): for each triangle record t, {leaf mn, margin} {leaf mx,
+// v0.x} {v0.yz, e1.xy} {e1.z, e2} of the leaf that holds it (nodes: nnodes nodes of the given
+// width; a root that is itself a leaf gets the root box)
+constexpr int kOccRecF4 = 4;
+void launch_occ_records(const DevScene& sc, uint32_t nnodes, float4* rec, hipStream_t s);
 // Culling margins of a child-pair tree (mcpt_core.hpp cull_*): tri_w[t] = W'_T of record t,
 // *pmax = the far coefficient P's bits (max), then `passes` bottom-up passes writing every
 // child's subtree maximum into q3.z / q3.w (passes >= tree depth + 1 reach the fixed point).
+// plane: the axis-plane bound (cull_plane_b) where it applies (false: the general bound only).
 void launch_cull_margins(float4* nodes, uint32_t npairs, const float4* tri, uint32_t ntri, float* tri_w,
-                         uint32_t* pmax, int passes, hipStream_t s);
+                         uint32_t* pmax, int passes, bool plane, hipStream_t s);
+// tex[i].w = pdf[i], i < n (EnvView::tex: the pdf in the texture's alpha plane)
+void launch_env_pack(float4* tex, const float* pdf, size_t n, hipStream_t s);
 void launch_env_table(const mcpt::EnvView& e, bool fixed_mode, float4* out, float2* row, float2* col, hipStream_t s);
 // HRDI tables on the device (env_build.hip), bit-identical to the host build: scratch holds
 // env_build_scratch_floats(W, H) floats; W * H < 2^31.

@@ -514,7 +514,11 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         if (d->ntri > 0) {
             if ((rc = dalloc(c, c->tmp_bufs, &tw, (size_t)d->ntri)) || (rc = dalloc(c, c->tmp_bufs, &pm, 1))) return rc;
             HIPCHK(c, hipMemsetAsync(pm, 0, sizeof(uint32_t), c->stream));
-            mcpt_dev::launch_cull_margins(dn, npairs, dt, (uint32_t)d->ntri, tw, pm, c->pair_depth + 2, c->stream);
+            // MCPT_CULL_PLANE=0: the general bound for axis-plane triangles too (A/B; the host
+            // builder's isolation of unbounded triangles reads the same variable)
+            const char* pl = std::getenv("MCPT_CULL_PLANE");
+            const bool plane = !(pl && pl[0] == '0' && pl[1] == 0);
+            mcpt_dev::launch_cull_margins(dn, npairs, dt, (uint32_t)d->ntri, tw, pm, c->pair_depth + 2, plane, c->stream);
             HIPCHK(c, hipGetLastError());
             uint32_t pb = 0;
             HIPCHK(c, hipMemcpyAsync(&pb, pm, sizeof(pb), hipMemcpyDeviceToHost, c->stream));
@@ -627,6 +631,8 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             c->last_env_build_ms = ms;
         }
         s.env.tex = tx; s.env.marginal_y = my; s.env.conds_y = cy; s.env.pdf = pd;
+        mcpt_dev::launch_env_pack(tx, pd, WH, c->stream);  // before the tables below read env_pdf
+        HIPCHK(c, hipGetLastError());
         // search guides for env_cell, on the device for either source of tables: valid on
         // a sorted, NaN-free marginal CDF and conditional rows that are sorted and NaN-free
         // or NaN throughout (upper_bound returns 0 on such a row for every value, and so
@@ -687,7 +693,7 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     // MCPT_OCC_G / MCPT_OCC_B set the cells per axis / bins per face coordinate.
     s.ntri = (uint32_t)d->ntri;
     s.occ = nullptr;
-    s.leaf_box = nullptr;
+    s.occ_rec = nullptr;
     {
         // 24^3 cells x 6 x 12^2 bins x 2 ways = 96 MB.  Config 2 with the table emptied at every film
         // clear: 62 % of the any-hit rays resolved (16^3 x 8^2: 60 %, 32^3 x 16^2: 64 %; frame rates
@@ -702,16 +708,17 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             float4* lbx;
             uint32_t* occ;
             const size_t ne = occ_entries(G, B);
-            if ((rc = dalloc(c, c->scene_bufs, &lbx, 2 * (size_t)d->ntri)) || (rc = dalloc(c, c->scene_bufs, &occ, ne + 2)))
+            if ((rc = dalloc(c, c->scene_bufs, &lbx, kOccRecF4 * (size_t)d->ntri)) ||
+                (rc = dalloc(c, c->scene_bufs, &occ, ne + 2)))
                 return rc;
             // NaN boxes (all-ones bytes) for a record no leaf holds: occ_test's slab then fails
-            HIPCHK(c, hipMemsetAsync(lbx, 0xff, 2 * (size_t)d->ntri * sizeof(float4), c->stream));
+            HIPCHK(c, hipMemsetAsync(lbx, 0xff, kOccRecF4 * (size_t)d->ntri * sizeof(float4), c->stream));
             HIPCHK(c, hipMemsetAsync(occ, 0xff, ne * sizeof(uint32_t), c->stream));
             HIPCHK(c, hipMemsetAsync(occ + ne, 0, 2 * sizeof(uint32_t), c->stream));  // the lookup gate: on
-            launch_leaf_boxes(s, nnodes, lbx, c->stream);
+            launch_occ_records(s, nnodes, lbx, c->stream);
             HIPCHK(c, hipGetLastError());
             HIPCHK(c, hipStreamSynchronize(c->stream));
-            s.leaf_box = lbx;
+            s.occ_rec = lbx;
             s.occ = occ;
             s.occ_gate = occ + ne;
             c->occ_entries_n = ne;

@@ -63,35 +63,48 @@ static const double U24 = 5.9604644775390625e-08; /* 2^-24 */
 
 /* per triangle: beta (coefficient of |tvec|) and omega (absolute term) of the bound
  * |P' - conv(T)|_a <= omega + beta |o - p0| on an accepted hit */
+static double nrm(mv3 e) { return sqrt((double)e.x * e.x + (double)e.y * e.y + (double)e.z * e.z); }
 static void tri_beta_omega(mv3 e1, mv3 e2, double *beta, double *omega) {
-    const double n1 = sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
-    const double n2 = sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+    const double n1 = nrm(e1), n2 = nrm(e2);
     const double alpha = 28.3 * U24 * n1 * n2 / (double)M_EPS;
     *beta = alpha * (1.0 + 1.0 / 512.0) + 1.01 * U24;
     *omega = 2.1 * U24 * (n1 > n2 ? n1 : n2);
 }
+/* axis-plane triangles (e1_a = e2_a = 0): b_T = 15.0003 u |e1| |e2| / G', G' = |G| - 5.0002 u S
+ * with G the in-plane cross product and S its products' magnitudes; the bound is then
+ * w <= omega + 1.01 u |tvec| + b_T (|tvec| + |t| |d|), independent of the det threshold.  0 when
+ * the triangle is not in an axis plane or G' < G / 2. */
+static double plane_b(mv3 e1, mv3 e2) {
+    double a1, c1, a2, c2;
+    if (e1.x == 0.f && e2.x == 0.f) { a1 = e1.y; c1 = e1.z; a2 = e2.y; c2 = e2.z; }
+    else if (e1.y == 0.f && e2.y == 0.f) { a1 = e1.z; c1 = e1.x; a2 = e2.z; c2 = e2.x; }
+    else if (e1.z == 0.f && e2.z == 0.f) { a1 = e1.x; c1 = e1.y; a2 = e2.x; c2 = e2.y; }
+    else return 0.0;
+    const double g = fabs(a1 * c2 - c1 * a2) * (1.0 - 1.0 / 1099511627776.0);
+    const double sg = (fabs(a1 * c2) + fabs(c1 * a2)) * (1.0 + 1.0 / 1099511627776.0);
+    const double gp = g - 5.0002 * U24 * sg;
+    if (!(gp > 0.5 * g)) return 0.0;
+    return 15.0003 * U24 * nrm(e1) * nrm(e2) * (1.0 + 1e-12) / gp;
+}
 /* a triangle's margin W'_T = (omega + beta diam_T) / (1 - sqrt3 beta) (+ slack); +inf when
  * sqrt3 beta >= 1/2 (a triangle so large against the det threshold that no box holding it is
- * ever culled).  A box's margin is the maximum over the triangles it holds. */
-static double tri_margin(double beta, double omega, double diam) {
-    if (!(1.7321 * beta * (1.0 + CULL_SLACK) < 0.5)) return INFINITY;
-    return (omega + beta * diam * (1.0 + 1e-12)) * (1.0 + CULL_SLACK) / (1.0 - 1.7321 * beta * (1.0 + CULL_SLACK));
-}
+ * ever culled).  A box's margin is the maximum over the triangles it holds.  *far: the
+ * triangle's coefficient of t_best in the far cut (P is their maximum). */
 static float to_f_up(double w) { return isinf(w) ? INFINITY : (float)(w * (1.0 + 1.0 / 1048576.0)) * (1.0f + 1.0f / 1048576.0f); }
-static double far_coef(double beta) {
-    return beta * (1.0 + 1.0 / 512.0) / (1.0 - 1.7321 * beta) * (1.0 + CULL_SLACK) * (1.0 + 1.0 / 1048576.0);
-}
-static double tri_w_of(const or_scene *sc, int t, double *beta_out) {
+static double tri_w_of(const or_scene *sc, int t, double *far) {
     mv3 a = mld(sc->v0, t), b = mld(sc->v1, t), c = mld(sc->v2, t);
     mv3 e1 = msub(b, a), e2 = msub(c, a), e3 = msub(c, b);
     double be, om;
     tri_beta_omega(e1, e2, &be, &om);
-    const double l1 = sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
-    const double l2 = sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
-    const double l3 = sqrt((double)e3.x * e3.x + (double)e3.y * e3.y + (double)e3.z * e3.z) * (1.0 + 1e-7);
+    const double pb = plane_b(e1, e2);
+    if (pb > 0.0) be = (1.01 * U24 + pb) * (1.0 + 1.0 / 8388608.0);
+    *far = 0.0;
+    if (!(1.7321 * be * (1.0 + CULL_SLACK) < 0.5)) return INFINITY;
+    const double l1 = nrm(e1), l2 = nrm(e2), l3 = nrm(e3) * (1.0 + 1e-7);
     const double diam = l1 > l2 ? (l1 > l3 ? l1 : l3) : (l2 > l3 ? l2 : l3);
-    *beta_out = be;
-    return tri_margin(be, om, diam);
+    const double den = 1.0 - 1.7321 * be * (1.0 + CULL_SLACK);
+    *far = (pb > 0.0 ? be + pb : be) * (1.0 + 1.0 / 512.0) / den * (1.0 + CULL_SLACK) * (1.0 + 1.0 / 1048576.0);
+    return (om + be * diam * (1.0 + 1e-12)) * (1.0 + CULL_SLACK) / den;
 }
 
 /* node_w[n]: margin of desc node n's box; tri_w[t]: margin of triangle t's own box; *p: the
@@ -104,9 +117,9 @@ int32_t or_model_margins(const or_scene *sc, float *node_w, float *tri_w, float 
     double pg = 0.0;
     int contained = 1;
     for (int t = 0; t < sc->ntri; t++) {
-        double be;
-        const double w = tri_w_of(sc, t, &be);
-        if (!isinf(w) && far_coef(be) > pg) pg = far_coef(be);
+        double fc;
+        const double w = tri_w_of(sc, t, &fc);
+        if (!isinf(w) && fc > pg) pg = fc;
         tri_w[t] = to_f_up(w);
     }
     /* subtree maxima, children before parents: desc nodes are depth-first (children after parent) */

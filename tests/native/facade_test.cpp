@@ -13,6 +13,7 @@
 //                                             batch mode == tile loop bit for bit, and the
 //                                             observer clears (camera edit, light edit).
 #include <cstdio>
+#include <unistd.h>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -99,6 +100,35 @@ static int run_cpu(const std::string& assets) {
     scene->remove_light(sun);
     d = scene->desc(dp);
     CHECK(d.ndir == 0);
+
+    // env texture reload: keyed on the light object and its texture revision, not the path
+    {
+        const std::string tmp = "/tmp/mcpt_facade_env_" + std::to_string((long)getpid()) + ".hdr";
+        auto write_hdr = [&](int w, int h) {  // flat (width < 8) RGBE, all texels (128, 64, 32) e 129
+            FILE* f = std::fopen(tmp.c_str(), "wb");
+            std::fprintf(f, "#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y %d +X %d\n", h, w);
+            for (int i = 0; i < w * h; i++) std::fputc(128, f), std::fputc(64, f), std::fputc(32, f), std::fputc(129, f);
+            std::fclose(f);
+        };
+        write_hdr(4, 2);
+        auto e1 = std::make_shared<EnvironmentLight>(tmp);
+        scene->set_environment_light(e1);
+        d = scene->desc(dp);
+        CHECK(d.env_mode == 1 && d.env_w == 4 && d.env_h == 2);
+        write_hdr(6, 3);  // the file changes on disk
+        e1->set_ls(2.f);  // not a texture edit: no re-read
+        d = scene->desc(dp);
+        CHECK(d.env_w == 4 && d.env_h == 2);
+        e1->set_texture_filepath(tmp);  // the same path set again: re-read
+        d = scene->desc(dp);
+        CHECK(d.env_w == 6 && d.env_h == 3);
+        write_hdr(2, 1);
+        scene->set_environment_light(std::make_shared<EnvironmentLight>(tmp));  // another object, same path
+        d = scene->desc(dp);
+        CHECK(d.env_w == 2 && d.env_h == 1);
+        std::remove(tmp.c_str());
+        scene->set_environment_light(grey);
+    }
     threw = false;
     try {
         grey->set_type(Atmosphere);

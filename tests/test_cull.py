@@ -129,6 +129,77 @@ def test_cull_bound_on_grazing_pairs(mcpt_mod):
     print(f"{checked} accepted grazing pairs, largest w / bound = {worst:.3g}")
 
 
+def test_plane_bound_on_grazing_pairs():
+    """Axis-plane triangles (mcpt_core.hpp cull_plane_b: walls, floors, box faces): for every
+    accepted pair, the point o + t' d lies within omega_T + 1.01 u |tvec| + b_T (|tvec| + |t'| |d|)
+    of the triangle's box, b_T = 15.0003 u |e1| |e2| / G', whatever the angle -- rays down to
+    |cos| = 1e-9, far below the det threshold's own angle for large triangles, which the general
+    bound (28.3 u |e1| |e2| / 1e-6) cannot cover.  Right-angled, general and thin triangles
+    (|e1| |e2| / G up to ~1e3), sizes 1e-3 .. 1e3, planes off the origin, every axis."""
+    rng = np.random.default_rng(11)
+    checked, worst = 0, 0.0
+    for rep in range(6):
+        m = 300000
+        ax = rng.integers(0, 3, m)
+        size = 10.0 ** rng.uniform(-3, 3, m)
+        kind = rng.integers(0, 3, m)
+        # in-plane edge vectors (a, c) of e1, e2: right angle, general, thin
+        e1p = np.stack([size, np.zeros(m)], 1)
+        e2p = np.where((kind == 0)[:, None], np.stack([np.zeros(m), size * rng.uniform(0.2, 5, m)], 1),
+                       rng.normal(size=(m, 2)) * size[:, None])
+        thin = kind == 2
+        e2p[thin] = e1p[thin] * rng.uniform(0.3, 2, thin.sum())[:, None] + \
+            np.stack([np.zeros(thin.sum()), size[thin] * 10.0 ** rng.uniform(-3, -1, thin.sum())], 1)
+        rot = rng.uniform(0, 2 * np.pi, m)
+        cr, sr = np.cos(rot), np.sin(rot)
+        def rotp(e):
+            return np.stack([cr * e[:, 0] - sr * e[:, 1], sr * e[:, 0] + cr * e[:, 1]], 1)
+        e1p, e2p = rotp(e1p), rotp(e2p)
+        off = rng.normal(size=(m, 3)) * size[:, None] * 10.0 ** rng.uniform(-1, 2, m)[:, None]
+        v0 = off.astype(np.float32)
+        v1 = v0.copy(); v2 = v0.copy()
+        ia, ic = (ax + 1) % 3, (ax + 2) % 3
+        r = np.arange(m)
+        v1[r, ia] += e1p[:, 0].astype(np.float32); v1[r, ic] += e1p[:, 1].astype(np.float32)
+        v2[r, ia] += e2p[:, 0].astype(np.float32); v2[r, ic] += e2p[:, 1].astype(np.float32)
+        e1, e2 = v1 - v0, v2 - v0
+        assert (e1[r, ax] == 0).all() and (e2[r, ax] == 0).all()
+        nrm = np.zeros((m, 3)); nrm[r, ax] = 1.0
+        n64 = np.cross(e1.astype(np.float64), e2.astype(np.float64))
+        nrm *= np.sign(n64[r, ax])[:, None]  # d . (e1 x e2) < 0 below: det > 0 (front face)
+        c = 10.0 ** rng.uniform(-9, -0.5, m)
+        tau = rng.normal(size=(m, 3)); tau[r, ax] = 0.0
+        tau /= np.linalg.norm(tau, axis=1, keepdims=True)
+        d = (tau * np.sqrt(1 - c * c)[:, None] - c[:, None] * nrm).astype(np.float32)
+        bu, bv = rng.random(m), rng.random(m)
+        flip = bu + bv > 1
+        bu[flip], bv[flip] = 1 - bu[flip], 1 - bv[flip]
+        q = v0 + bu[:, None] * e1 + bv[:, None] * e2
+        dist = size * 10.0 ** rng.uniform(-4, 3, m)
+        o = (q - dist[:, None] * d).astype(np.float32)
+        ok, det, nn = mt_fp32(o, d, v0, e1, e2)
+        tq = nn.astype(np.float64) / det.astype(np.float64)
+        P = o.astype(np.float64) + tq[:, None] * d.astype(np.float64)
+        lo = np.minimum(np.minimum(v0, v1), v2).astype(np.float64)
+        hi = np.maximum(np.maximum(v0, v1), v2).astype(np.float64)
+        w = np.maximum(np.maximum(lo - P, P - hi), 0.0).max(axis=1)
+        n1 = np.linalg.norm(e1.astype(np.float64), axis=1)
+        n2 = np.linalg.norm(e2.astype(np.float64), axis=1)
+        A1 = e1[r, ia].astype(np.float64); C1 = e1[r, ic].astype(np.float64)
+        A2 = e2[r, ia].astype(np.float64); C2 = e2[r, ic].astype(np.float64)
+        g = np.abs(A1 * C2 - C1 * A2)
+        gp = g - 5.0002 * U * (np.abs(A1 * C2) + np.abs(C1 * A2))
+        b = 15.0003 * U * n1 * n2 / gp
+        tv = np.linalg.norm(o.astype(np.float64) - v0.astype(np.float64), axis=1)
+        bound = 2.1 * U * np.maximum(n1, n2) + 1.01 * U * tv + b * (tv + np.abs(tq) * np.linalg.norm(d.astype(np.float64), axis=1))
+        sel = ok & np.isfinite(tq) & (gp > 0.5 * g)
+        assert (w[sel] <= bound[sel]).all(), f"bound violated on {(w[sel] > bound[sel]).sum()} pairs"
+        checked += int(sel.sum())
+        worst = max(worst, float((w[sel] / bound[sel]).max()))
+    assert checked > 500000, checked
+    print(f"{checked} accepted axis-plane pairs, largest w / bound = {worst:.3g}")
+
+
 # ---- the traversal model on adversarial rays ------------------------------------------------
 SCENES = [("c2", 1.0), ("c2", 1e3), ("c2", 1e-3), ("c3", 1.0), ("floor", 1.0)]
 
