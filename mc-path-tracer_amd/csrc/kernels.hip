@@ -295,33 +295,23 @@ __device__ inline bool occ_test(V3 o, V3 d, V3 inv, float io, float4 bmn, float4
 __device__ inline uint2 occ_entry(const DevScene& sc, V3 o, V3 d) {
     return reinterpret_cast<const uint2*>(sc.occ)[occ_index(sc, o, d)];
 }
-// Both any-hit rays of a path against their cells' entries: all four candidates' occluder records
-// (leaf box, margin and triangle in one aligned 64-B record: one half line each, where the leaf
-// box and the 48-B triangle record used to cost two or three) are fetched in one round trip (an
-// empty way reads record 0 and is not tested).
-__device__ inline void occ_hit2(const DevScene& sc, V3 ol, V3 dl, uint2 el, V3 ob, V3 db, uint2 eb, bool& hl,
-                                bool& hb) {
-    hl = hb = false;
-    const bool v0 = el.x < sc.ntri, v1 = el.y < sc.ntri, v2 = eb.x < sc.ntri, v3_ = eb.y < sc.ntri;
-    if (!(v0 || v1 || v2 || v3_)) return;
-    const uint32_t t[4] = {v0 ? el.x : 0u, v1 ? el.y : 0u, v2 ? eb.x : 0u, v3_ ? eb.y : 0u};
-    float4 bn[4], bx[4], r2[4], r3[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const float4* p = sc.occ_rec + kOccRecF4 * (size_t)t[k];
-        bn[k] = p[0];
-        bx[k] = p[1];
-        r2[k] = p[2];
-        r3[k] = p[3];
-    }
-    const V3 il = v3(1.f / dl.x, 1.f / dl.y, 1.f / dl.z), ib = v3(1.f / db.x, 1.f / db.y, 1.f / db.z);  // k_trace's
-    const bool fl = __builtin_fabsf(il.x) < K_INF_F && __builtin_fabsf(il.y) < K_INF_F && __builtin_fabsf(il.z) < K_INF_F;
-    const bool fb = __builtin_fabsf(ib.x) < K_INF_F && __builtin_fabsf(ib.y) < K_INF_F && __builtin_fabsf(ib.z) < K_INF_F;
-    const float iol = cull_iota(sc, dl, il), iob = cull_iota(sc, db, ib);
-    hl = fl && ((v0 && occ_test(ol, dl, il, iol, bn[0], bx[0], r2[0], r3[0])) ||
-                (v1 && occ_test(ol, dl, il, iol, bn[1], bx[1], r2[1], r3[1])));
-    hb = fb && ((v2 && occ_test(ob, db, ib, iob, bn[2], bx[2], r2[2], r3[2])) ||
-                (v3_ && occ_test(ob, db, ib, iob, bn[3], bx[3], r2[3], r3[3])));
+// An any-hit ray against its cell's entries: both candidates' occluder records (leaf box, margin
+// and triangle in one aligned 64-B record: one half line each, where the leaf box and the 48-B
+// triangle record used to cost two or three) are fetched in one round trip (an empty way reads
+// record 0 and is not tested).  k_material calls it for the light ray, then the BRDF ray: 32
+// VGPRs of records at a time, next to the BRDF sample's deferred state.
+__device__ inline bool occ_hit1(const DevScene& sc, V3 o, V3 d, uint2 e) {
+    const bool v0 = e.x < sc.ntri, v1 = e.y < sc.ntri;
+    if (!(v0 || v1)) return false;
+    const float4* p0 = sc.occ_rec + kOccRecF4 * (size_t)(v0 ? e.x : 0u);
+    const float4* p1 = sc.occ_rec + kOccRecF4 * (size_t)(v1 ? e.y : 0u);
+    const float4 bn0 = p0[0], bx0 = p0[1], r20 = p0[2], r30 = p0[3];
+    const float4 bn1 = p1[0], bx1 = p1[1], r21 = p1[2], r31 = p1[3];
+    const V3 inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);  // k_trace's
+    if (!(__builtin_fabsf(inv.x) < K_INF_F && __builtin_fabsf(inv.y) < K_INF_F && __builtin_fabsf(inv.z) < K_INF_F))
+        return false;
+    const float io = cull_iota(sc, d, inv);
+    return (v0 && occ_test(o, d, inv, io, bn0, bx0, r20, r30)) || (v1 && occ_test(o, d, inv, io, bn1, bx1, r21, r31));
 }
 
 // ---------------------------------------------------------------------------
@@ -339,9 +329,18 @@ __device__ inline void occ_hit2(const DevScene& sc, V3 ol, V3 dl, uint2 el, V3 o
 // does not change any result.
 // ---------------------------------------------------------------------------
 struct MatOut {
-    bool want_ext, want_l, want_b, trivial_ext, vis_ray;
+    bool want_ext, want_l, want_b, trivial_ext, vis_ray, need_cb;
     uint32_t trivial_any;
     uint2 el, eb;  // occluder-cache entries of the light / BRDF rays (loads issued inside material())
+    // the BRDF sample's light terms are finished by material_brdf_terms after the occluder cache
+    // (a visibility ray it resolves as occluded needs none: k_shade reads nee1.xyz only when
+    // vis = 1, wavefront_kernels.cu:336-343)
+    V3 n, wo, wi_b, ldir, Li_l;
+    int matid, light_id;
+    uint32_t flags;  // the flags word (F_CONDL / F_CONDB added by material_light_terms)
+    float rry, rrz;  // nee0.w, nee1.w
+    float pdfl_x;
+    bool need_cl;
 };
 
 // Light choice + wf_mat_mix for the continuing path pid (vertex len, sample index
@@ -356,7 +355,8 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
                                  int32_t htri, float4* stage, bool occ_on) {
     const DevScene& sc = a.scene;
     const uint2 none = make_uint2(kOccEmpty, kOccEmpty);
-    MatOut mo{false, false, false, false, false, 0u, none, none};
+    MatOut mo{};
+    mo.el = mo.eb = none;
     // path slot -> pixel; the sample index comes with the record (k_shade: slot k of a pixel
     // runs samples k, k + S, k + 2S, ...)
     const uint32_t npix = (uint32_t)a.W * (uint32_t)a.H;
@@ -373,7 +373,8 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
     // record, so they are evaluated in the order that lets each store its results at
     // once (short register live ranges): the continuation first (:353-358, its ratio
     // f_s/pdf_s rides in the .w slots of beta/nee0/nee1), then the light sample
-    // (:316-329), then the BRDF sample (:331-343).
+    // (:316-329), then the BRDF sample's direction (:331-334); its light terms
+    // (:335-343) wait for the occluder cache (material_brdf_terms).
     uint32_t nf = 0;
     V3 rr;
     {
@@ -420,15 +421,11 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
             else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
             light_L_pdf<FIXED>(sc, light_id, ldir, Li_l, pdfl_x);
         }
-        V3 f_l;
-        float pdf_bl;
-        brdf_f_pdf(m, n, ldir, wo, f_l, pdf_bl);
         if (FIXED) pdfl_x = pdfl_x * sel;
-        float pdfb_y = !delta ? pdf_bl : (FIXED ? 0.f : 1.f);
-        float wL = power_heuristic(pdfl_x, pdfb_y);
-        V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
-        if (wL > 0.f && pdfl_x > 0.f) nf |= F_CONDL;
-        a.p.nee0[pid] = f4(cL, rr.y);
+        mo.ldir = ldir;
+        mo.Li_l = Li_l;
+        mo.pdfl_x = pdfl_x;
+        mo.need_cl = true;
         const V3 so_l = pos + n * 0.01f;
         if (ray_misses_scene(sc, so_l, ldir)) {
             a.p.vis[2 * pid] = 1;
@@ -438,40 +435,72 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
             stage[0 * kBlock + threadIdx.x] = f4(so_l, 0.f);
             stage[1 * kBlock + threadIdx.x] = f4(ldir, 0.f);
             mo.want_l = true;
-            // the occluder-cache entry, loaded now and used after material(): its latency
-            // hides behind the BRDF sample below
+            // the occluder-cache entry, loaded now and used after material()
             if (occ_on) mo.el = occ_entry(sc, so_l, ldir);
         }
     }
-    V3 cB = v3(0.f, 0.f, 0.f);
+    // the BRDF sample's direction and visibility ray (its light terms come after the occluder
+    // cache, material_brdf_terms)
     if (!delta) {
-        V3 wi_b = brdf_sample_wi<FIXED>(m, n, wo, r, SL_MAT_E0, r(SL_MAT_LOBE) < 0.5f);  // spec : diff
+        const V3 wi_b = brdf_sample_wi<FIXED>(m, n, wo, r, SL_MAT_E0, r(SL_MAT_LOBE) < 0.5f);  // spec : diff
         const V3 so_b = pos + wi_b * 0.001f;
-        if (occ_on) mo.eb = occ_entry(sc, so_b, wi_b);  // (used only if the ray is queued)
-        V3 f_b;
-        float pdfb_x;
-        brdf_f_pdf(m, n, wi_b, wo, f_b, pdfb_x);
-        V3 Li_b;
-        float pdfl_y;
-        light_L_pdf<FIXED>(sc, light_id, wi_b, Li_b, pdfl_y);
-        if (FIXED) pdfl_y = pdfl_y * sel;
-        float wB = power_heuristic(pdfb_x, pdfl_y);
-        cB = ((f_b * Li_b) * wB) / pdfb_x;
-        if (wB > 0.f && pdfb_x > 0.f) nf |= F_CONDB;
         nf |= F_HASVIS;
         mo.vis_ray = true;
+        mo.need_cb = true;
+        mo.wi_b = wi_b;
         if (ray_misses_scene(sc, so_b, wi_b)) {
             a.p.vis[2 * pid + 1] = 1;
             mo.trivial_any++;
         } else {
+            if (occ_on) mo.eb = occ_entry(sc, so_b, wi_b);
             stage[2 * kBlock + threadIdx.x] = f4(so_b, 0.f);
             stage[3 * kBlock + threadIdx.x] = f4(wi_b, 0.f);
             mo.want_b = true;
         }
     }
-    a.p.nee1[pid] = f4(cB, rr.z);
-    a.p.flags[pid] = nf | ((len + 1) << F_LEN_SHIFT) | (sidx << F_SIDX_SHIFT);  // extend increments len (:270)
+    mo.n = n;
+    mo.wo = wo;
+    mo.matid = mat;
+    mo.light_id = light_id;
+    mo.rry = rr.y;
+    mo.rrz = rr.z;
+    mo.flags = nf | ((len + 1) << F_LEN_SHIFT) | (sidx << F_SIDX_SHIFT);  // extend increments len (:270)
     return mo;
+}
+// The BRDF sample's light terms (wavefront_kernels.cu:331-343) and the path's last two words:
+// nee1 = (cB, f_s / pdf_s .z) and the flags word (F_CONDB).  cB is evaluated only for a
+// visibility ray that may be unoccluded (need_cb): one the occluder cache resolved is never read.
+template <bool FIXED>
+__device__ inline void material_brdf_terms(const ShadeArgs& a, uint32_t pid, const MatOut& mo) {
+    const DevScene& sc = a.scene;
+    V3 cB = v3(0.f, 0.f, 0.f), cL = v3(0.f, 0.f, 0.f);
+    uint32_t nf = mo.flags;
+    const Mat m = load_mat(sc.mats + 8 * mo.matid);
+    if (mo.need_cl) {  // the light sample's terms (:322-329)
+        V3 f_l;
+        float pdf_bl;
+        brdf_f_pdf(m, mo.n, mo.ldir, mo.wo, f_l, pdf_bl);
+        const bool delta = mo.light_id > 0;
+        float pdfb_y = !delta ? pdf_bl : (FIXED ? 0.f : 1.f);
+        float wL = power_heuristic(mo.pdfl_x, pdfb_y);
+        cL = ((f_l * mo.Li_l) * wL) / mo.pdfl_x;
+        if (wL > 0.f && mo.pdfl_x > 0.f) nf |= F_CONDL;
+    }
+    a.p.nee0[pid] = f4(cL, mo.rry);
+    if (mo.need_cb) {
+        V3 f_b;
+        float pdfb_x;
+        brdf_f_pdf(m, mo.n, mo.wi_b, mo.wo, f_b, pdfb_x);
+        V3 Li_b;
+        float pdfl_y;
+        light_L_pdf<FIXED>(sc, mo.light_id, mo.wi_b, Li_b, pdfl_y);
+        if (FIXED) pdfl_y = pdfl_y * (1.f / (float)sc.nlights);
+        float wB = power_heuristic(pdfb_x, pdfl_y);
+        cB = ((f_b * Li_b) * wB) / pdfb_x;
+        if (wB > 0.f && pdfb_x > 0.f) nf |= F_CONDB;
+    }
+    a.p.nee1[pid] = f4(cB, mo.rrz);
+    a.p.flags[pid] = nf;
 }
 
 #ifdef MCPT_SHADE_WPE
@@ -694,7 +723,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
     __shared__ float4 s_any[4][kBlock];
     for (uint32_t base = w_in * kBlock; base < n; base += bps * kBlock) {  // block-uniform trip count
         const uint32_t i = base + threadIdx.x;
-        MatOut mo{false, false, false, false, false, 0u};
+        MatOut mo{};
         uint32_t mpid = 0;
         bool occ_l = false, occ_b = false, try_l = false, try_b = false;  // resolved by / tested against the occluder cache
         if (i < n) {
@@ -702,26 +731,29 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
             const float4 b4 = a.mat_beta[shard * a.ext_cap + i];
             mpid = q.x;
             mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w, &s_any[0][0], occ_on);
-            // the occluder cache (see occ_hit2), after the path's shading state is dead: a ray it
+            // the occluder cache (see occ_hit1), before the BRDF sample's light terms: a ray it
             // resolves gets its wf_shadow result here and is not queued
             if (occ_on) {
                 try_l = mo.want_l;
                 try_b = mo.want_b;
                 const V3 ol = xyz(s_any[0][threadIdx.x]), dl = xyz(s_any[1][threadIdx.x]);
                 const V3 ob = xyz(s_any[2][threadIdx.x]), db = xyz(s_any[3][threadIdx.x]);
-                occ_hit2(a.scene, ol, dl, mo.want_l ? mo.el : make_uint2(kOccEmpty, kOccEmpty), ob, db,
-                         mo.want_b ? mo.eb : make_uint2(kOccEmpty, kOccEmpty), occ_l, occ_b);
+                if (mo.want_l) occ_l = occ_hit1(a.scene, ol, dl, mo.el);
+                if (mo.want_b) occ_b = occ_hit1(a.scene, ob, db, mo.eb);
                 if (occ_l) {
                     a.p.vis[2 * mpid] = 0;
                     mo.want_l = false;
+                    mo.need_cl = false;
                     mo.trivial_any++;
                 }
                 if (occ_b) {
                     a.p.vis[2 * mpid + 1] = 0;
                     mo.want_b = false;
+                    mo.need_cb = false;
                     mo.trivial_any++;
                 }
             }
+            material_brdf_terms<FIXED>(a, mpid, mo);
         }
         bool want[3] = {mo.want_ext, mo.want_l, mo.want_b};
         uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
@@ -937,7 +969,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     };
     enter(home);
     const DevScene& sc = a.scene;
-    // occluder-cache records (see occ_hit2): off while k_material's lookups are gated off, except in
+    // occluder-cache records (see occ_hit1): off while k_material's lookups are gated off, except in
     // the iteration before the next lookups (DevScene::occ_gate)
     const bool occ_rec = sc.occ && sc.occ_gate[0] <= 1u;
 
@@ -989,7 +1021,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         }
         if (kind) {
             a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
-            if (tri >= 0 && occ_rec)  // the cell's occluder (occ_hit2)
+            if (tri >= 0 && occ_rec)  // the cell's occluder (occ_hit1)
                 sc.occ[(size_t)occ_index(sc, o, d) * kOccWays + (uint32_t)tri % kOccWays] = (uint32_t)tri;
         } else {
             a.hit_tri[rid] = tri;  // hit record rebuilt by the consumer (hit_record())
@@ -1274,6 +1306,98 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         wave_stats(a.set[0].stats, lane, tot_n - tot_n1, tot_t - tot_t1, tot_h - tot_h1);
         wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Coherence sort of the extension queue (experiment, SortArgs): counting sort per shard by
+// (octant, 8^3 origin cell) -- three passes: histogram (and keys), per-shard exclusive scan,
+// scatter (block-local ranks, one global reservation per bucket and block).  Order within a
+// bucket is not stable; k_trace's results do not depend on the queue order.
+constexpr int kSortChunk = 2048;  // entries per block (8 per thread)
+__device__ inline uint32_t sort_key(const SortArgs& a, float4 o, float4 d) {
+    const uint32_t oct = (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float v = ((&o.x)[k] - a.mn[k]) * a.inv[k];
+        const uint32_t c = (uint32_t)__builtin_fminf(__builtin_fmaxf(v, 0.f), 7.f);
+        m |= ((c & 1u) << k) | (((c >> 1) & 1u) << (3 + k)) | (((c >> 2) & 1u) << (6 + k));
+    }
+    return (oct << 9) | m;
+}
+__global__ __launch_bounds__(256) void k_sort_hist(SortArgs a, uint32_t bps) {
+    __shared__ uint32_t h[kSortBuckets];
+    const uint32_t sh = blockIdx.x / bps, b = blockIdx.x % bps;
+    const uint32_t n = a.count_ptr[sh * C_WORDS];
+    const uint32_t lo = b * kSortChunk;
+    if (lo >= n) return;  // block-uniform
+    for (uint32_t k = threadIdx.x; k < kSortBuckets; k += 256) h[k] = 0;
+    __syncthreads();
+    const size_t base = (size_t)sh * a.cap;
+    for (uint32_t i = lo + threadIdx.x; i < min(n, lo + kSortChunk); i += 256) {
+        const uint32_t pid = a.q_in[base + i];
+        const uint32_t key = sort_key(a, a.ro[pid], a.rd[pid]);
+        a.keys[base + i] = (uint16_t)key;
+        atomicAdd(&h[key], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kSortBuckets; k += 256)
+        if (h[k]) atomicAdd(&a.hist[(size_t)sh * kSortBuckets + k], h[k]);
+}
+__global__ __launch_bounds__(1024) void k_sort_scan(SortArgs a) {  // one block per shard
+    __shared__ uint32_t part[1024];
+    uint32_t* hh = a.hist + (size_t)blockIdx.x * kSortBuckets;
+    const uint32_t t = threadIdx.x;
+    const uint32_t v0 = hh[4 * t], v1 = hh[4 * t + 1], v2 = hh[4 * t + 2], v3 = hh[4 * t + 3];
+    part[t] = v0 + v1 + v2 + v3;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t x = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    const uint32_t ex = t ? part[t - 1] : 0u;
+    hh[4 * t] = ex;
+    hh[4 * t + 1] = ex + v0;
+    hh[4 * t + 2] = ex + v0 + v1;
+    hh[4 * t + 3] = ex + v0 + v1 + v2;
+}
+__global__ __launch_bounds__(256) void k_sort_scatter(SortArgs a, uint32_t bps) {
+    __shared__ uint32_t cnt[kSortBuckets];
+    __shared__ uint32_t off[kSortBuckets];
+    const uint32_t sh = blockIdx.x / bps, b = blockIdx.x % bps;
+    const uint32_t n = a.count_ptr[sh * C_WORDS];
+    const uint32_t lo = b * kSortChunk;
+    if (lo >= n) return;
+    for (uint32_t k = threadIdx.x; k < kSortBuckets; k += 256) cnt[k] = 0;
+    __syncthreads();
+    const size_t base = (size_t)sh * a.cap;
+    uint32_t key[kSortChunk / 256], rank[kSortChunk / 256], pid[kSortChunk / 256];
+#pragma unroll
+    for (int j = 0; j < kSortChunk / 256; j++) {
+        const uint32_t i = lo + threadIdx.x + 256u * j;
+        key[j] = kSortBuckets;
+        if (i < n) {
+            pid[j] = a.q_in[base + i];
+            key[j] = a.keys[base + i];
+            rank[j] = atomicAdd(&cnt[key[j]], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kSortBuckets; k += 256)
+        off[k] = cnt[k] ? atomicAdd(&a.hist[(size_t)sh * kSortBuckets + k], cnt[k]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kSortChunk / 256; j++)
+        if (key[j] < (uint32_t)kSortBuckets) a.q_out[base + off[key[j]] + rank[j]] = pid[j];
+}
+void launch_sort_ext(const SortArgs& a, hipStream_t s) {
+    const uint32_t bps = (a.cap + kSortChunk - 1) / kSortChunk;
+    (void)hipMemsetAsync(a.hist, 0, (size_t)kShards * kSortBuckets * sizeof(uint32_t), s);
+    hipLaunchKernelGGL(k_sort_hist, dim3(kShards * bps), dim3(256), 0, s, a, bps);
+    hipLaunchKernelGGL(k_sort_scan, dim3(kShards), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_sort_scatter, dim3(kShards * bps), dim3(256), 0, s, a, bps);
 }
 
 // The env texture's device copy takes the pdf table into its alpha plane (EnvView::tex)

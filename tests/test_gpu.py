@@ -283,7 +283,7 @@ def test_path_slots_ragged_and_resize(mcpt_mod, oracle, scene_c2):
 
 @pytest.mark.parametrize("which", ["scene_c2", "scene_cube", "scene_c1", "scene_c3"])
 def test_occluder_cache_same_film(request, mcpt_mod, which):
-    """The any-hit occluder cache (kernels.hip occ_hit2) decides only which any-hit rays skip the
+    """The any-hit occluder cache (kernels.hip occ_hit1) decides only which any-hit rays skip the
     traversal: a cached triangle counts only under its own leaf box with the traversal's slab
     arithmetic and cull, so every ray it resolves is one the traversal finds occluded too.  Films
     and ray counts with the cache (default; it starts empty with every film clear and fills during
@@ -1068,3 +1068,58 @@ def test_stage_fixed_mode_vs_oracle(mcpt_mod, oracle, stage):
     got = pt.stage(stage, inp, film=sf.FILM if stage != "material" else None)
     pt.close()
     _check_stage(stage, got, ref, a, oracle)
+
+
+def test_bvh_without_containment_disables_cull_and_cache(mcpt_mod, oracle, scene_c2):
+    """A caller-supplied BVH whose boxes do not contain their subtrees (here: an interior node's box
+    shrunk by a fifth per side, so some of its triangles stick out): the occluder cache's lemma
+    and the culling bound both assume containment, so mcpt_scene_upload turns
+    both off.  Hits then still equal the oracle's traversal of the same boxes, and films are
+    bit-identical with the cache requested (default) and switched off (MCPT_OCC_G=0)."""
+    _, a0 = scene_c2
+    a = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in a0.items()}
+    inner = np.nonzero(a["nprims"] == 0)[0]
+    n = int(inner[1])  # an interior node below the root
+    lo, hi = a["bmin"].reshape(-1, 3)[n].copy(), a["bmax"].reshape(-1, 3)[n].copy()
+    ext = hi - lo
+    a["bmin"].reshape(-1, 3)[n] = lo + 0.2 * ext
+    a["bmax"].reshape(-1, 3)[n] = hi - 0.2 * ext
+    d = mcpt_mod.desc_from_arrays(a)
+    pt = mcpt_mod.PathTracer(0)
+    pt.upload_scene(d)
+    ro, rd = random_rays(100000, 33)
+    gp, gn, gt = pt.trace_closest(ro, rd)
+    op_, on, ot = oracle.trace_closest(a, ro, rd)
+    assert np.array_equal(gt, ot)
+    assert np.array_equal(gp.view(np.uint32), op_.view(np.uint32))
+    assert np.array_equal(pt.trace_any(ro, rd), oracle.trace_any(a, ro, rd))
+    pt.close()
+
+    W, H = 160, 90
+    cam = mcpt_mod.config_camera(mcpt_mod.CONFIGS[2], W, H)
+
+    def run(env):
+        old = os.environ.get("MCPT_OCC_G")
+        if env is None:
+            os.environ.pop("MCPT_OCC_G", None)
+        else:
+            os.environ["MCPT_OCC_G"] = env
+        try:
+            p = make_pt(mcpt_mod, d, cam, W, H, 24, 5, tile=64)
+        finally:
+            if old is None:
+                os.environ.pop("MCPT_OCC_G", None)
+            else:
+                os.environ["MCPT_OCC_G"] = old
+        p.set_path_slots(2)
+        p.clear()
+        st = p.render()
+        L, smp = p.film()
+        out = (L.copy(), smp.copy(), (st.extend_rays, st.shadow_rays, st.vis_rays), p.occ_stats())
+        p.close()
+        return out
+
+    off, on = run("0"), run(None)
+    assert on[3] == (0, False), "the occluder cache must be off for a BVH that breaks containment"
+    assert np.array_equal(on[0].view(np.uint32), off[0].view(np.uint32))
+    assert np.array_equal(on[1], off[1]) and on[2] == off[2]

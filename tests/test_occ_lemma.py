@@ -1,4 +1,4 @@
-"""The lemma the any-hit occluder cache rests on (kernels.hip occ_test / occ_hit2):
+"""The lemma the any-hit occluder cache rests on (kernels.hip occ_test / occ_hit1):
 with the traversal's fp32 slab arithmetic (pair_slab: per axis min/max of (plane - o) * inv, then
 max3 of the entries and min3 of the exits), a box that contains another never has a later entry or
 an earlier exit, so if the leaf box of a cached triangle passes the slab test and keep_box's cull,

@@ -14,7 +14,7 @@
 #   ab         whole-frame A/B of library builds, interleaved (LIBS="a:path.so b:path.so", CONFIGS,
 #              ROUNDS; tools/gpu/ab_libs.sh)
 #   abenv      the same for environment settings (ENVS="A=1|A=0 B=2", '|'-separated)
-#   partition  tools/partition_rehearsal.py (PART_ARGS)
+#   partition  tools/partition_rehearsal.py (PART_ARGS)       -> gpurun_out/partition_$TAG.json
 #
 # Parameters (environment): CONFIG (2), TAG (r04), STEPS (bench frames, 3), BENCH_ARGS.
 set -o pipefail
@@ -64,7 +64,7 @@ PY
     done
     rm -rf $O/prof_kt && mkdir -p $O/prof_kt && cp $O/kernel_stats_$sfx.csv $O/prof_kt/ 2>/dev/null
     i=0
-    rm -rf $O/pmct_$sfx
+    rm -rf $O/pmct_$sfx && mkdir -p $O/pmct_$sfx
     for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_FLAT SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES" \
                "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE" \
                "SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_FLAT SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR" \
@@ -89,7 +89,7 @@ print('$e'.ljust(30), round(d['value'], 1), 'Mray/s', d['ms_per_step'], 'ms/fram
       done
     done ;;
   partition)
-    timeout -k 10 900 python -u tools/partition_rehearsal.py ${PART_ARGS} > $O/partition.log 2>&1 || fail partition 20 $O/partition.log
+    timeout -k 10 900 python -u tools/partition_rehearsal.py --out $O/partition_$TAG.json ${PART_ARGS} > $O/partition.log 2>&1 || fail partition 20 $O/partition.log
     cat $O/partition.log ;;
   *)
     echo "unknown step $step"; exit 2 ;;
