@@ -335,12 +335,10 @@ struct MatOut {
     // the BRDF sample's light terms are finished by material_brdf_terms after the occluder cache
     // (a visibility ray it resolves as occluded needs none: k_shade reads nee1.xyz only when
     // vis = 1, wavefront_kernels.cu:336-343)
-    V3 n, wo, wi_b, ldir, Li_l;
+    V3 n, wo, wi_b;
     int matid, light_id;
-    uint32_t flags;  // the flags word (F_CONDL / F_CONDB added by material_light_terms)
-    float rry, rrz;  // nee0.w, nee1.w
-    float pdfl_x;
-    bool need_cl;
+    uint32_t flags;  // the flags word (F_CONDB added by material_brdf_terms)
+    float rrz;       // nee1.w
 };
 
 // Light choice + wf_mat_mix for the continuing path pid (vertex len, sample index
@@ -421,11 +419,15 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
             else ldir = ld3(sc.dirs + 7 * (light_id - 1), 0);
             light_L_pdf<FIXED>(sc, light_id, ldir, Li_l, pdfl_x);
         }
+        V3 f_l;
+        float pdf_bl;
+        brdf_f_pdf(m, n, ldir, wo, f_l, pdf_bl);
         if (FIXED) pdfl_x = pdfl_x * sel;
-        mo.ldir = ldir;
-        mo.Li_l = Li_l;
-        mo.pdfl_x = pdfl_x;
-        mo.need_cl = true;
+        float pdfb_y = !delta ? pdf_bl : (FIXED ? 0.f : 1.f);
+        float wL = power_heuristic(pdfl_x, pdfb_y);
+        V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
+        if (wL > 0.f && pdfl_x > 0.f) nf |= F_CONDL;
+        a.p.nee0[pid] = f4(cL, rr.y);
         const V3 so_l = pos + n * 0.01f;
         if (ray_misses_scene(sc, so_l, ldir)) {
             a.p.vis[2 * pid] = 1;
@@ -462,7 +464,6 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
     mo.wo = wo;
     mo.matid = mat;
     mo.light_id = light_id;
-    mo.rry = rr.y;
     mo.rrz = rr.z;
     mo.flags = nf | ((len + 1) << F_LEN_SHIFT) | (sidx << F_SIDX_SHIFT);  // extend increments len (:270)
     return mo;
@@ -473,21 +474,10 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sid
 template <bool FIXED>
 __device__ inline void material_brdf_terms(const ShadeArgs& a, uint32_t pid, const MatOut& mo) {
     const DevScene& sc = a.scene;
-    V3 cB = v3(0.f, 0.f, 0.f), cL = v3(0.f, 0.f, 0.f);
+    V3 cB = v3(0.f, 0.f, 0.f);
     uint32_t nf = mo.flags;
-    const Mat m = load_mat(sc.mats + 8 * mo.matid);
-    if (mo.need_cl) {  // the light sample's terms (:322-329)
-        V3 f_l;
-        float pdf_bl;
-        brdf_f_pdf(m, mo.n, mo.ldir, mo.wo, f_l, pdf_bl);
-        const bool delta = mo.light_id > 0;
-        float pdfb_y = !delta ? pdf_bl : (FIXED ? 0.f : 1.f);
-        float wL = power_heuristic(mo.pdfl_x, pdfb_y);
-        cL = ((f_l * mo.Li_l) * wL) / mo.pdfl_x;
-        if (wL > 0.f && mo.pdfl_x > 0.f) nf |= F_CONDL;
-    }
-    a.p.nee0[pid] = f4(cL, mo.rry);
     if (mo.need_cb) {
+        const Mat m = load_mat(sc.mats + 8 * mo.matid);
         V3 f_b;
         float pdfb_x;
         brdf_f_pdf(m, mo.n, mo.wi_b, mo.wo, f_b, pdfb_x);
@@ -743,7 +733,6 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
                 if (occ_l) {
                     a.p.vis[2 * mpid] = 0;
                     mo.want_l = false;
-                    mo.need_cl = false;
                     mo.trivial_any++;
                 }
                 if (occ_b) {
@@ -1306,98 +1295,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         wave_stats(a.set[0].stats, lane, tot_n - tot_n1, tot_t - tot_t1, tot_h - tot_h1);
         wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);
     }
-}
-
-// ---------------------------------------------------------------------------
-// Coherence sort of the extension queue (experiment, SortArgs): counting sort per shard by
-// (octant, 8^3 origin cell) -- three passes: histogram (and keys), per-shard exclusive scan,
-// scatter (block-local ranks, one global reservation per bucket and block).  Order within a
-// bucket is not stable; k_trace's results do not depend on the queue order.
-constexpr int kSortChunk = 2048;  // entries per block (8 per thread)
-__device__ inline uint32_t sort_key(const SortArgs& a, float4 o, float4 d) {
-    const uint32_t oct = (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
-    uint32_t m = 0;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const float v = ((&o.x)[k] - a.mn[k]) * a.inv[k];
-        const uint32_t c = (uint32_t)__builtin_fminf(__builtin_fmaxf(v, 0.f), 7.f);
-        m |= ((c & 1u) << k) | (((c >> 1) & 1u) << (3 + k)) | (((c >> 2) & 1u) << (6 + k));
-    }
-    return (oct << 9) | m;
-}
-__global__ __launch_bounds__(256) void k_sort_hist(SortArgs a, uint32_t bps) {
-    __shared__ uint32_t h[kSortBuckets];
-    const uint32_t sh = blockIdx.x / bps, b = blockIdx.x % bps;
-    const uint32_t n = a.count_ptr[sh * C_WORDS];
-    const uint32_t lo = b * kSortChunk;
-    if (lo >= n) return;  // block-uniform
-    for (uint32_t k = threadIdx.x; k < kSortBuckets; k += 256) h[k] = 0;
-    __syncthreads();
-    const size_t base = (size_t)sh * a.cap;
-    for (uint32_t i = lo + threadIdx.x; i < min(n, lo + kSortChunk); i += 256) {
-        const uint32_t pid = a.q_in[base + i];
-        const uint32_t key = sort_key(a, a.ro[pid], a.rd[pid]);
-        a.keys[base + i] = (uint16_t)key;
-        atomicAdd(&h[key], 1u);
-    }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kSortBuckets; k += 256)
-        if (h[k]) atomicAdd(&a.hist[(size_t)sh * kSortBuckets + k], h[k]);
-}
-__global__ __launch_bounds__(1024) void k_sort_scan(SortArgs a) {  // one block per shard
-    __shared__ uint32_t part[1024];
-    uint32_t* hh = a.hist + (size_t)blockIdx.x * kSortBuckets;
-    const uint32_t t = threadIdx.x;
-    const uint32_t v0 = hh[4 * t], v1 = hh[4 * t + 1], v2 = hh[4 * t + 2], v3 = hh[4 * t + 3];
-    part[t] = v0 + v1 + v2 + v3;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t x = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += x;
-        __syncthreads();
-    }
-    const uint32_t ex = t ? part[t - 1] : 0u;
-    hh[4 * t] = ex;
-    hh[4 * t + 1] = ex + v0;
-    hh[4 * t + 2] = ex + v0 + v1;
-    hh[4 * t + 3] = ex + v0 + v1 + v2;
-}
-__global__ __launch_bounds__(256) void k_sort_scatter(SortArgs a, uint32_t bps) {
-    __shared__ uint32_t cnt[kSortBuckets];
-    __shared__ uint32_t off[kSortBuckets];
-    const uint32_t sh = blockIdx.x / bps, b = blockIdx.x % bps;
-    const uint32_t n = a.count_ptr[sh * C_WORDS];
-    const uint32_t lo = b * kSortChunk;
-    if (lo >= n) return;
-    for (uint32_t k = threadIdx.x; k < kSortBuckets; k += 256) cnt[k] = 0;
-    __syncthreads();
-    const size_t base = (size_t)sh * a.cap;
-    uint32_t key[kSortChunk / 256], rank[kSortChunk / 256], pid[kSortChunk / 256];
-#pragma unroll
-    for (int j = 0; j < kSortChunk / 256; j++) {
-        const uint32_t i = lo + threadIdx.x + 256u * j;
-        key[j] = kSortBuckets;
-        if (i < n) {
-            pid[j] = a.q_in[base + i];
-            key[j] = a.keys[base + i];
-            rank[j] = atomicAdd(&cnt[key[j]], 1u);
-        }
-    }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kSortBuckets; k += 256)
-        off[k] = cnt[k] ? atomicAdd(&a.hist[(size_t)sh * kSortBuckets + k], cnt[k]) : 0u;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kSortChunk / 256; j++)
-        if (key[j] < (uint32_t)kSortBuckets) a.q_out[base + off[key[j]] + rank[j]] = pid[j];
-}
-void launch_sort_ext(const SortArgs& a, hipStream_t s) {
-    const uint32_t bps = (a.cap + kSortChunk - 1) / kSortChunk;
-    (void)hipMemsetAsync(a.hist, 0, (size_t)kShards * kSortBuckets * sizeof(uint32_t), s);
-    hipLaunchKernelGGL(k_sort_hist, dim3(kShards * bps), dim3(256), 0, s, a, bps);
-    hipLaunchKernelGGL(k_sort_scan, dim3(kShards), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_sort_scatter, dim3(kShards * bps), dim3(256), 0, s, a, bps);
 }
 
 // The env texture's device copy takes the pdf table into its alpha plane (EnvView::tex)

@@ -216,22 +216,6 @@ void launch_shade(const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fix
 void launch_shade_stage(bool material_stage, const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fixed_mode,
                         hipStream_t s);
 void launch_trace(const TraceArgs& a, const LaunchGeom& g, hipStream_t s);
-// Coherence sort of the extension queue (MCPT_SORT_EXT=1, experiment): each shard's queue
-// entries (pids) are reordered by (direction octant, origin cell of an 8^3 grid over the root
-// box) into q_out, which k_trace then reads; counts are unchanged.  hist: kShards x
-// kSortBuckets words, zeroed by the call; keys: one uint16 per queue entry.
-constexpr int kSortBuckets = 4096;
-struct SortArgs {
-    const uint32_t* q_in;
-    uint32_t* q_out;
-    const uint32_t* count_ptr;  // shard s: count_ptr[s * C_WORDS]
-    uint32_t cap;               // entries per shard
-    const float4 *ro, *rd;
-    uint32_t* hist;
-    uint16_t* keys;
-    float mn[3], inv[3];        // root box min, 8 / extent
-};
-void launch_sort_ext(const SortArgs& a, hipStream_t s);
 void launch_clear(const ClearArgs& a, hipStream_t s);
 // Occluder records (DevScene::occ_rec): for each triangle record t, {leaf mn, margin} {leaf mx,
 // v0.x} {v0.yz, e1.xy} {e1.z, e2} of the leaf that holds it (nodes: nnodes nodes of the given

@@ -68,12 +68,6 @@ struct mcpt_ctx {
     DevPaths p{};
     uint32_t *ext_q = nullptr, *any_q = nullptr, *mat_q = nullptr;
     float4* any_ray = nullptr;          // any-hit rays at their queue positions: o [2 queue_alloc], then d
-    // MCPT_SORT_EXT=1 (experiment): the extension queue sorted per shard by (octant, origin cell)
-    // into sort_q before k_trace (launch_sort_ext)
-    bool sort_ext = [] { const char* e = getenv("MCPT_SORT_EXT"); return e && e[0] == '1'; }();
-    uint32_t* sort_q = nullptr;
-    uint16_t* sort_keys = nullptr;
-    uint32_t* sort_hist = nullptr;
     uint32_t ext_cap = 0, any_cap = 0;  // per-shard capacities
     size_t queue_alloc = 0;             // entries allocated for ext_q (any_q holds twice)
     CounterBlock* cnt = nullptr;
@@ -191,9 +185,6 @@ void mcpt_destroy(mcpt_ctx* c) {
     if (c->any_q) (void)hipFree(c->any_q);
     if (c->mat_q) (void)hipFree(c->mat_q);
     if (c->any_ray) (void)hipFree(c->any_ray);
-    if (c->sort_q) (void)hipFree(c->sort_q);
-    if (c->sort_keys) (void)hipFree(c->sort_keys);
-    if (c->sort_hist) (void)hipFree(c->sort_hist);
     for (auto e : c->events) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -814,24 +805,14 @@ static int set_tiles_internal(mcpt_ctx* c, const std::vector<int2>& t) {
         if (c->any_q) (void)hipFree(c->any_q);
         if (c->mat_q) (void)hipFree(c->mat_q);
         if (c->any_ray) (void)hipFree(c->any_ray);
-        if (c->sort_q) (void)hipFree(c->sort_q);
-        if (c->sort_keys) (void)hipFree(c->sort_keys);
-        if (c->sort_hist) (void)hipFree(c->sort_hist);
         c->ext_q = c->any_q = c->mat_q = nullptr;
         c->any_ray = nullptr;
-        c->sort_q = nullptr;
-        c->sort_keys = nullptr;
-        c->sort_hist = nullptr;
         c->queue_alloc = 0;
         if (hipMalloc(&c->ext_q, need * sizeof(uint32_t)) != hipSuccess ||
             hipMalloc(&c->any_q, 2 * need * sizeof(uint32_t)) != hipSuccess ||
             hipMalloc(&c->mat_q, need * 8 * sizeof(uint32_t)) != hipSuccess ||  // MatRec + beta per slot
             hipMalloc(&c->any_ray, 4 * need * sizeof(float4)) != hipSuccess)    // o + d per any-queue entry
             return set_err(c, MCPT_E_NOMEM, "queue allocation failed");
-        if (c->sort_ext && (hipMalloc(&c->sort_q, need * sizeof(uint32_t)) != hipSuccess ||
-                            hipMalloc(&c->sort_keys, need * sizeof(uint16_t)) != hipSuccess ||
-                            hipMalloc(&c->sort_hist, (size_t)kShards * kSortBuckets * sizeof(uint32_t)) != hipSuccess))
-            return set_err(c, MCPT_E_NOMEM, "sort queue allocation failed");
         c->queue_alloc = need;
     }
     c->p.sray_o = c->any_ray;  // indexed by any-queue position (kShards * any_cap = 2 * need entries)
@@ -995,24 +976,6 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     e.ro = c->p.ray_o;
     e.rd = c->p.ray_d;
     e.queue = c->ext_q;
-    if (c->sort_ext && c->sort_q && sa.ntiles > 0) {
-        SortArgs so{};
-        so.q_in = c->ext_q;
-        so.q_out = c->sort_q;
-        so.count_ptr = &c->cnt->shard[0][C_EXT];
-        so.cap = c->ext_cap;
-        so.ro = c->p.ray_o;
-        so.rd = c->p.ray_d;
-        so.hist = c->sort_hist;
-        so.keys = c->sort_keys;
-        for (int k = 0; k < 3; k++) {
-            so.mn[k] = c->scene.root_mn[k];
-            const float ext = c->scene.root_mx[k] - c->scene.root_mn[k];
-            so.inv[k] = ext > 0.f ? 8.f / ext : 0.f;
-        }
-        launch_sort_ext(so, c->stream);
-        e.queue = c->sort_q;
-    }
     e.count_ptr = &c->cnt->shard[0][C_EXT];
     e.shard_cap = c->ext_cap;
     e.stats = c->count_work ? &c->cnt->shard[0][C_STATS] : nullptr;  // mcpt_set_work_counters

@@ -4,10 +4,12 @@ For N in (2, 4, 8), rank r's share of the frame -- the tiles with (tx + ty) mod 
 rendered to the config's spp with the strong split's path slots (mcpt/parallel.py strong_slots),
 one rank after the other on one device.  The slowest partition sets an N-GPU frame's time, so
 max / mean of the per-rank times is the strong split's load imbalance.
-Tile sizes 256 (the reference's Film tile, Film.cu:17) and 128 / 64 are compared: results do not
-depend on the tiling (keyed RNG), only the balance does.
+Tile sizes 256 (the reference's Film tile, Film.cu:17) and 64 (bench.MULTI_TILE) are compared:
+results do not depend on the tiling (keyed RNG), only the balance does.  The whole frame on one
+"rank" (N = 1, the config's bench slots) is timed too, so efficiency = t_1 / (N max_r t_r), and at
+64 px tiles the base slot count is compared with the strong split's (--slot-choices).
 
-Usage: python tools/partition_rehearsal.py [--configs 2 4] [--tiles 256 128] [--out profiles/partition_r04.json]
+Usage: python tools/partition_rehearsal.py [--configs 2 4] [--tiles 256 64] [--out profiles/partition_r04.json]
 """
 import argparse
 import json
@@ -23,7 +25,8 @@ sys.path.insert(0, REPO)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", type=int, nargs="+", default=[2, 4])
-    ap.add_argument("--tiles", type=int, nargs="+", default=[256, 128, 64])
+    ap.add_argument("--tiles", type=int, nargs="+", default=[256, 64])
+    ap.add_argument("--slot-choices", default="strong,base", help="at the smallest tile: strong_slots and/or base")
     ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "partition_r04.json"))
     args = ap.parse_args()
@@ -41,29 +44,45 @@ def main():
         pt.upload_scene(scene)
         pt.set_camera(cam)
         W, H = rc.width, rc.height
+        base = bench.BENCH_SLOTS[cid]
+
+        def frame_ms(tiles):
+            pt.set_tiles(tiles)
+            pt.clear()
+            t0 = time.perf_counter()
+            st = pt.render()
+            return (time.perf_counter() - t0) * 1e3, st.rays
+
+        pt.set_path_slots(base)
+        pt.resize(W, H, 256, 256)
+        frame_ms(None)  # warmup
+        t1, rays1 = frame_ms(None)
+        res["runs"].append({"config": cid, "frame": [W, H], "spp": rc.spp, "world": 1, "tile": 256, "slots": base,
+                            "per_rank_ms": [round(t1, 2)], "rays": rays1})
+        print(json.dumps(res["runs"][-1]), flush=True)
         for world in args.worlds:
-            slots = parallel.strong_slots(bench.BENCH_SLOTS[cid], world, W, H, rc.spp)
-            pt.set_path_slots(slots)
+            choices = []
             for tile in args.tiles:
+                choices.append((tile, parallel.strong_slots(base, world, W, H, rc.spp)))
+            if "base" in args.slot_choices and base != choices[-1][1]:
+                choices.append((min(args.tiles), base))
+            for tile, slots in choices:
+                pt.set_path_slots(slots)
                 pt.resize(W, H, tile, tile)
                 ms, rays, px = [], [], []
                 for r in range(world):
                     tiles = parallel.tiles_for_rank(r, world, W, H, tile)
-                    pt.set_tiles(tiles)
                     if r == 0:  # warmup: the first launches of this slot / tile layout
-                        pt.clear()
-                        pt.render()
-                    pt.clear()
-                    t0 = time.perf_counter()
-                    st = pt.render()
-                    ms.append((time.perf_counter() - t0) * 1e3)
-                    rays.append(st.rays)
+                        frame_ms(tiles)
+                    t, ry = frame_ms(tiles)
+                    ms.append(t)
+                    rays.append(ry)
                     px.append(sum(min(tile, W - tx * tile) * min(tile, H - ty * tile) for tx, ty in tiles))
                 mean = sum(ms) / len(ms)
                 run = {"config": cid, "frame": [W, H], "spp": rc.spp, "world": world, "tile": tile, "slots": slots,
                        "per_rank_ms": [round(x, 2) for x in ms], "per_rank_pixels": px, "per_rank_rays": rays,
                        "max_over_mean": round(max(ms) / mean, 4), "ideal_ms": round(mean, 2),
-                       "max_ms": round(max(ms), 2)}
+                       "max_ms": round(max(ms), 2), "efficiency_vs_one_gpu": round(t1 / (world * max(ms)), 4)}
                 res["runs"].append(run)
                 print(json.dumps(run), flush=True)
         pt.close()
