@@ -62,7 +62,7 @@ PY
       timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace -d $d -o p --output-format csv -- python3 bench.py $BARGS \
         > $d.log 2>&1 || fail "pmc $c" 20 $d.log
     done
-    rm -rf $O/prof_kt && mkdir -p $O/prof_kt && cp $O/kernel_stats_$sfx.csv $O/prof_kt/ 2>/dev/null
+    rm -rf $O/prof_kt && mkdir -p $O/prof_kt && cp $O/kernel_stats_$sfx.csv $O/prof_kt/kt_kernel_stats.csv 2>/dev/null
     i=0
     rm -rf $O/pmct_$sfx && mkdir -p $O/pmct_$sfx
     for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_FLAT SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES" \

@@ -20,12 +20,11 @@ os.makedirs(dst, exist_ok=True)
 
 
 def find(sub, suffix):
+    # the newest match: gpurun merges a call's gpurun_out/ into the local one, so older runs'
+    # files can sit beside the current ones
     d = os.path.join(src, sub)
-    for root, _, files in os.walk(d):
-        for f in files:
-            if f.endswith(suffix):
-                return os.path.join(root, f)
-    return None
+    hits = [os.path.join(root, f) for root, _, files in os.walk(d) for f in files if f.endswith(suffix)]
+    return max(hits, key=os.path.getmtime) if hits else None
 
 
 stats = find("prof_kt", "kernel_stats.csv")
