@@ -146,13 +146,20 @@ def pmc_summary(config, slots, kind="pmc"):
     return d, ("; ".join(why) or None)
 
 
+def _timed_kernel(name, kernel_prefix):
+    """A summary entry of one of the timed frames' kernels: the prefix matches, and it is not
+    k_trace's work-counting instantiation (k_trace<W, S, true>, launched only in the extra
+    counting frame)."""
+    hit = any(name.startswith(p) or name.startswith("void " + p) for p in kernel_prefix)
+    return hit and not (name.split("(")[0].endswith(", true>") and "k_trace<" in name)
+
+
 def pmc_traffic(summary, kernel_prefix):
     """Per-iteration HBM bytes of a stage from a PMC summary: the sum over the stage's kernels
     (each launched once per iteration) of their bytes per launch."""
     if not summary:
         return None
-    got = [v.get("hbm_bytes_per_launch") for k, v in summary.get("kernels", {}).items()
-           if any(k.startswith(p) or k.startswith("void " + p) for p in kernel_prefix)]
+    got = [v.get("hbm_bytes_per_launch") for k, v in summary.get("kernels", {}).items() if _timed_kernel(k, kernel_prefix)]
     return int(sum(got)) if got and None not in got else None
 
 
@@ -161,7 +168,7 @@ def pmc_detail(summary, kernel_prefix):
     if not summary:
         return None
     for k, v in summary.get("kernels", {}).items():
-        if any(k.startswith(p) or k.startswith("void " + p) for p in kernel_prefix):
+        if _timed_kernel(k, kernel_prefix):
             return v.get("ratios")
     return None
 

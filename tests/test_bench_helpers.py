@@ -130,3 +130,16 @@ def test_cpu_baseline_threads(monkeypatch):
     assert bench.cpu_threads() == min(3, len(os.sched_getaffinity(0)))
     monkeypatch.delenv("OMP_NUM_THREADS")
     assert bench.cpu_threads() == len(os.sched_getaffinity(0))
+
+
+def test_pmc_lookup_skips_the_counting_instantiation():
+    """The bench's extra counting frame launches k_trace<W, S, true>; its traffic and counters
+    must not be added to (or stand in for) the timed frames' k_trace<W, S, false>."""
+    import bench
+
+    s = {"kernels": {"void mcpt_dev::k_trace<2, 8, false>(mcpt_dev::TraceArgs)": {"hbm_bytes_per_launch": 100, "ratios": {"a": 1}},
+                     "void mcpt_dev::k_trace<2, 8, true>(mcpt_dev::TraceArgs)": {"hbm_bytes_per_launch": 120, "ratios": {"a": 2}},
+                     "void mcpt_dev::k_material<true>(mcpt_dev::ShadeArgs)": {"hbm_bytes_per_launch": 7}}}
+    assert bench.pmc_traffic(s, ("mcpt_dev::k_trace<",)) == 100
+    assert bench.pmc_detail(s, ("mcpt_dev::k_trace<",)) == {"a": 1}
+    assert bench.pmc_traffic(s, ("mcpt_dev::k_material<",)) == 7  # quality mode's <true> is a timed kernel

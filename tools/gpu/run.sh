@@ -8,9 +8,11 @@
 #   smoke      __graft_entry__.smoke()
 #   bench      bench.py $BENCH_ARGS                      -> gpurun_out/bench_$TAG.json
 #   kstats     rocprofv3 --kernel-trace --stats of bench  -> gpurun_out/kt_$TAG/
-#   pmc        FETCH_SIZE and WRITE_SIZE passes (separate runs) + four SQ / TCC counter passes of the
-#              same bench command, summarised by tools/pmc.py / tools/pmc_detail.py into profiles/
-#              (kernel_stats_*, pmc_*, pmcdetail_* named by TAG and CONFIG)
+#   pmc        FETCH_SIZE and WRITE_SIZE passes (separate runs, gpurun_out/pmcraw_<sfx>/) + four SQ /
+#              TCC counter passes of the same bench command (gpurun_out/pmct_<sfx>/), summarised by
+#              tools/pmc.py / tools/pmc_detail.py into profiles/ (kernel_stats_*, pmc_*, pmcdetail_*
+#              named by TAG and CONFIG; profiles/ on the box is not copied back: re-run both tools
+#              here on the merged gpurun_out/).  FETCH_ONLY=1: the two traffic passes only
 #   ab         whole-frame A/B of library builds, interleaved (LIBS="a:path.so b:path.so", CONFIGS,
 #              ROUNDS; tools/gpu/ab_libs.sh)
 #   abenv      the same for environment settings (ENVS="A=1|A=0 B=2", '|'-separated)
@@ -56,13 +58,15 @@ for r in csv.DictReader(open(sys.argv[1])):
 PY
     ;;
   pmc)
+    R=$O/pmcraw_$sfx  # per config: one call's configs must not overwrite each other's raw passes
+    rm -rf $R && mkdir -p $R
     for c in FETCH_SIZE WRITE_SIZE; do
-      d=$O/prof_$([[ $c == FETCH_SIZE ]] && echo fetch || echo write)
-      rm -rf $d
+      d=$R/prof_$([[ $c == FETCH_SIZE ]] && echo fetch || echo write)
       timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace -d $d -o p --output-format csv -- python3 bench.py $BARGS \
         > $d.log 2>&1 || fail "pmc $c" 20 $d.log
     done
-    rm -rf $O/prof_kt && mkdir -p $O/prof_kt && cp $O/kernel_stats_$sfx.csv $O/prof_kt/kt_kernel_stats.csv 2>/dev/null
+    if [[ "$FETCH_ONLY" == 1 ]]; then echo "fetch/write passes only"; continue; fi
+    mkdir -p $R/prof_kt && cp $O/kernel_stats_$sfx.csv $R/prof_kt/kt_kernel_stats.csv 2>/dev/null
     i=0
     rm -rf $O/pmct_$sfx && mkdir -p $O/pmct_$sfx
     for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_FLAT SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES" \
@@ -73,7 +77,7 @@ PY
       timeout -k 10 600 rocprofv3 --pmc $set --kernel-trace -d $O/pmct_$sfx/p$i -o p$i --output-format csv -- python3 bench.py $BARGS \
         > $O/pmct_$sfx/p$i.log 2>&1 || fail "pmc pass $i" 10 $O/pmct_$sfx/p$i.log
     done
-    PMC_CONFIG=$CONFIG PMC_ARGS="$BARGS" STATS_NAME=kernel_stats_$sfx python3 tools/pmc.py $sfx $O > /dev/null &&
+    PMC_CONFIG=$CONFIG PMC_ARGS="$BARGS" STATS_NAME=kernel_stats_$sfx python3 tools/pmc.py $sfx $R > /dev/null &&
       PMC_CONFIG=$CONFIG python3 tools/pmc_detail.py $sfx $sfx $O || fail "pmc summary" 5 /dev/null
     ls profiles/*_$sfx* ;;
   ab)
