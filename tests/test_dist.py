@@ -192,7 +192,7 @@ def test_multi_gpu_tile_balances_pixels():
     """bench.py's multi-GPU partition uses 64 x 64 film tiles (MULTI_TILE): every rank's pixel
     count is within 2 % of the mean at N = 2 / 4 / 8 on the 1080p frame and on config 4's 4K frame
     (with 256 x 256 tiles a 1080p rank at N = 8 owns 5 tiles, one diagonal; the time spread the
-    one-GPU rehearsal measured was 1.74x, profiles/partition_r04.json)."""
+    one-GPU rehearsal measured was 1.71x, profiles/partition_r04.json)."""
     import bench
 
     T = bench.MULTI_TILE
