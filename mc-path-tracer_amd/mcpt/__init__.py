@@ -641,6 +641,10 @@ def write_pfm(path, rgb):
 # The build's default BVH: binned SAH over all three axes (mcpt_scene_build_ex).  On config 2 it
 # traces ~14% faster than BVHAccel's single-axis 12-bucket SAH; films are identical for any tree.
 DEFAULT_BVH = dict(builder="sah3", buckets=128, trav_cost=0.5, isect_cost=1.0, max_prims=8)
+# A/B knobs for the builder's cost model (films do not depend on the tree)
+for _k, _env, _t in (("trav_cost", "MCPT_BVH_TRAV_COST", float), ("max_prims", "MCPT_BVH_MAX_PRIMS", int)):
+    if os.environ.get(_env):
+        DEFAULT_BVH[_k] = _t(os.environ[_env])
 
 
 def build_config_scene(cid: int, asset_dir=ASSET_DIR, **build_kw) -> Scene:
