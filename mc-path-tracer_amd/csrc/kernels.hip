@@ -779,57 +779,6 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
     }
 }
 
-// The unbounded set (DevScene::useg) for a starting ray.  Every triangle whose own box passes the
-// ray's slab test (the traversal's arithmetic; these boxes are never culled: their margin is +inf)
-// is tested as the triangle phase tests it, except those the ray provably meets from behind
-// (bf: the ray is one the bound covers; mcpt_core.hpp cull_back_tau).  A subtree's own box
-// passing implies its ancestors' (containment, the occluder cache's lemma), so this reaches the
-// triangles the isolated subtree's traversal would.  best / tri / cut as the triangle phase
-// updates them; true: an any-hit ray (best < 0) found its occluder.
-__device__ inline bool u_prepass(const DevScene& sc, V3 o, V3 d, V3 inv, float io, bool bf, float& best, int& tri,
-                                 float& cut, uint32_t& tests) {
-    const bool fin = __builtin_fabsf(io) < K_INF_F;
-    const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;
-    for (uint32_t k = 0; k < sc.nu; k++) {
-        const float4 nt = sc.useg[3 * k + 2];
-        if (bf && (d.x * nt.x + d.y * nt.y) + d.z * nt.z < nt.w) continue;
-        const float4 mn = sc.useg[3 * k], mx = sc.useg[3 * k + 1];
-        bool hit;
-        if (fin) {  // pair_slab's arithmetic for one box
-            const float ax = (mn.x - o.x) * inv.x, bx = (mx.x - o.x) * inv.x;
-            const float ay = (mn.y - o.y) * inv.y, by = (mx.y - o.y) * inv.y;
-            const float az = (mn.z - o.z) * inv.z, bz = (mx.z - o.z) * inv.z;
-            const float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax, bx), __builtin_fminf(ay, by)),
-                                             __builtin_fminf(az, bz));
-            const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by)),
-                                             __builtin_fmaxf(az, bz));
-            hit = t0 <= t1;
-        } else {
-            float t0, t1;
-            hit = slab(mn.x, mn.y, mn.z, mx.x, mx.y, mx.z, o, inv, nx, ny, nz, t0, t1);
-        }
-        if (!hit) continue;
-        tests++;
-        const int id = __float_as_int(mx.w);
-        const float4* tp = sc.tri + kTriF4 * id;
-        const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
-        float t;
-        if (!tri_test_t(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t) || t < 0.f) continue;
-        if (best < 0.f) {
-            if (t < K_HUGE) {
-                tri = id;
-                return true;
-            }
-        } else if (t < best ||
-                   (t == best && tri >= 0 && __float_as_int(w2.y) < __float_as_int(sc.tri[kTriF4 * tri + 2].y))) {
-            best = t;
-            tri = id;
-            cut = best * __builtin_fmaf(__builtin_fabsf(io), sc.cull_p, kCullSlackF);
-        }
-    }
-    return false;
-}
-
 // ---------------------------------------------------------------------------
 // BVH traversal (BVH.cu:115-207 closest hit, Triangle.cu:157-205 any hit).
 // Child-pair nodes (both child boxes in the parent, 64 B) with the reference's
@@ -1155,20 +1104,10 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                         if (!pre && (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0],
                                            sc.root_mx[1], sc.root_mx[2], o, inv, inv.x < 0.f, inv.y < 0.f, inv.z < 0.f,
                                            t0, t1) ||
-                                     !keep_box(t0, t1, sc.root_w * io, cut, key))) {
+                                     !keep_box(t0, t1, sc.root_w * io, cut, key)))
                             finish();
-                        } else {
+                        else
                             ref = sc.root_ref;
-                            if constexpr (kW == 2) {  // (runtime.cpp selects the set for child-pair trees only)
-                                if (sc.nu) {  // the isolated unbounded triangles, before the traversal
-                                    const bool bf = sc.cull_ok && d.x * d.x + d.y * d.y + d.z * d.z <= kCullNormMax;
-                                    uint32_t ut = 0;
-                                    const bool occluded = u_prepass(sc, o, d, inv, io, bf, best, tri, cut, ut);
-                                    if constexpr (kCount) tot_t += ut;
-                                    if (occluded) finish();
-                                }
-                            }
-                        }
                     }
                 }
             }

@@ -106,15 +106,7 @@ struct DevScene {
     // do not contain their triangles, or MCPT_CULL=0): nothing is culled.
     float cull_p, root_w;
     int cull_ok;
-    // Unbounded set (mcpt_core.hpp cull_plane_back): the triangles no box bound covers, when the
-    // SAH builder isolated them under one child of the root (config 2's walls).  k_trace tests
-    // them at every ray's start (u_prepass) instead of traversing their subtree, skipping each one
-    // the ray provably meets from behind; root_ref is then the other child.  Entry k: useg[3k] =
-    // (own box mn, 0), [3k + 1] = (own box mx, record index bits), [3k + 2] = (n, tau).
-    const float4* useg;
-    uint32_t nu;
 };
-constexpr uint32_t kMaxUnbounded = 64;
 constexpr uint32_t kOccEmpty = 0xffffffffu;
 constexpr uint32_t kOccWays = 2;      // entries per cell: k_trace writes way tri mod 2, k_material tests both
                                       // (1 way resolved 52 % of config 2's any-hit rays, 2 ways 64 %)

@@ -47,7 +47,6 @@ struct mcpt_ctx {
     // traversal work counters (mcpt_set_work_counters): k_trace's counting instantiation, whose six
     // per-lane counters cost the fast one its spill-free registers -- off by default
     bool count_work = getenv("MCPT_WORK_COUNTERS") != nullptr;
-    uint32_t unbounded_set = 0;  // triangles k_trace tests ahead of the traversal (DevScene::nu)
     int node_layout = 0;  // pair-node numbering the last upload used (mcpt_debug_node_layout)
     // camera
     mcpt::CamView cam{};
@@ -589,78 +588,6 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         // empty scene: a root box that no ray can enter
         for (int k = 0; k < 3; k++) { s.root_mn[k] = 1.f; s.root_mx[k] = -1.f; }
         s.root_ref = 0;
-    }
-    // Unbounded set (DevScene::useg): when one child of the root holds only triangles no box bound
-    // covers (the SAH builder's isolation, scene.cpp) and few of them, k_trace tests them directly at
-    // each ray's start with a back-facing skip, and the traversal starts at the other child.  Needs
-    // child-pair nodes (width 2), a host BVH and nested boxes (an own box passing implies its
-    // ancestors').  MCPT_UNBOUNDED_SET=0 turns it off.
-    s.useg = nullptr;
-    s.nu = 0;
-    c->unbounded_set = 0;
-    {
-        const char* ue = std::getenv("MCPT_UNBOUNDED_SET");
-        const char* pl = std::getenv("MCPT_CULL_PLANE");
-        const bool plane = !(pl && pl[0] == '0' && pl[1] == 0);
-        if (!(ue && ue[0] == '0' && ue[1] == 0) && !gpu_bvh && N > 0 && width == 2 && d->nprims[0] == 0 && nest_ok) {
-            std::vector<int> tlo(N), thi(N), tcnt(N);
-            for (int i = N - 1; i >= 0; i--) {
-                if (d->nprims[i] > 0) {
-                    tlo[i] = d->offset[i];
-                    thi[i] = d->offset[i] + d->nprims[i];
-                    tcnt[i] = d->nprims[i];
-                } else {
-                    const int c0 = i + 1, c1 = d->offset[i];
-                    tlo[i] = std::min(tlo[c0], tlo[c1]);
-                    thi[i] = std::max(thi[c0], thi[c1]);
-                    tcnt[i] = tcnt[c0] + tcnt[c1];
-                }
-            }
-            auto rec = [&](int t, mcpt::V3& v0, mcpt::V3& e1, mcpt::V3& e2) {
-                const float *a0 = d->v0 + 3 * (size_t)t, *a1 = d->v1 + 3 * (size_t)t, *a2 = d->v2 + 3 * (size_t)t;
-                v0 = mcpt::v3(a0[0], a0[1], a0[2]);
-                e1 = mcpt::v3(a1[0] - a0[0], a1[1] - a0[1], a1[2] - a0[2]);  // as the triangle record stores them
-                e2 = mcpt::v3(a2[0] - a0[0], a2[1] - a0[1], a2[2] - a0[2]);
-            };
-            const int ch[2] = {1, d->offset[0]};
-            for (int k = 0; k < 2 && !c->unbounded_set; k++) {
-                const int cu = ch[k], co = ch[1 - k];
-                if (thi[cu] - tlo[cu] != tcnt[cu] || thi[co] - tlo[co] != tcnt[co] || tcnt[cu] > (int)kMaxUnbounded ||
-                    tcnt[co] == 0)
-                    continue;
-                bool all = true;
-                for (int t = tlo[cu]; t < thi[cu] && all; t++) {
-                    mcpt::V3 v0, e1, e2;
-                    rec(t, v0, e1, e2);
-                    all = mcpt::cull_tri_unbounded(e1, e2, plane);
-                }
-                if (!all) continue;
-                std::vector<float4> u;
-                for (int t = tlo[cu]; t < thi[cu]; t++) {
-                    const float* v[3] = {d->v0 + 3 * (size_t)t, d->v1 + 3 * (size_t)t, d->v2 + 3 * (size_t)t};
-                    float mn[3], mx[3];
-                    for (int a = 0; a < 3; a++) {
-                        mn[a] = std::fmin(std::fmin(v[0][a], v[1][a]), v[2][a]);
-                        mx[a] = std::fmax(std::fmax(v[0][a], v[1][a]), v[2][a]);
-                    }
-                    mcpt::V3 v0, e1, e2;
-                    rec(t, v0, e1, e2);
-                    float nf[3];
-                    const float tau = mcpt::cull_back_tau(e1, e2, nf);
-                    float ft;
-                    memcpy(&ft, &t, 4);
-                    u.push_back(make_float4(mn[0], mn[1], mn[2], 0.f));
-                    u.push_back(make_float4(mx[0], mx[1], mx[2], ft));
-                    u.push_back(make_float4(nf[0], nf[1], nf[2], tau));
-                }
-                float4* du;
-                if ((rc = dupload(c, c->scene_bufs, &du, u.data(), u.size()))) return rc;
-                s.useg = du;
-                s.nu = (uint32_t)(u.size() / 3);
-                s.root_ref = ref_of(co);
-                c->unbounded_set = s.nu;
-            }
-        }
     }
     s.env.mode = d->env_mode;
     for (int k = 0; k < 3; k++) s.env.color[k] = d->env_color[k];

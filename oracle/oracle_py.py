@@ -200,7 +200,7 @@ def model_margins(arrays):
 
 def model_trace(arrays, ro, rd, mode, margins=None):
     """trav_model.c: closest (triangle id, t) and any-hit visibility under culling rule `mode`
-    (0 none, 1 round 3, 2 round 4, 5 round 4 + the unbounded set) and the number of boxes tested."""
+    (0 none, 1 round 3, 2 round 4) and the number of boxes tested."""
     s = scene_struct(arrays)
     m = margins or model_margins(arrays)
     ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)

@@ -17,11 +17,6 @@
  *           the rounding error of the fp32 Moller-Trumbore expressions with the det >= 1e-6
  *           acceptance threshold (Triangle.cu:17-21).  Skip when t1 (1 - 2^-18) + W i < 0 (behind)
  *           or t0 - W i > t_best (1 + 2^-18 + i P) (beyond), i = max |1/d_a| (1 + 2^-18).
- *   mode 5  mode 2 plus the unbounded set (kernels.hip u_prepass, runtime.cpp): when one child of
- *           the root holds only unbounded triangles (at most 64, a contiguous range), they are
- *           tested at the ray's start under their own boxes, each skipped when fl(d . n) < tau (the
- *           ray meets it from behind: mcpt_core.hpp cull_back_tau), and the traversal starts at the
- *           other child.
  * The margins come from or_model_margins (a restatement of the product's k_cull_margins in C).
  * Visit order: both children of an interior node are tested, the nearer (entry t) is visited
  * first -- the product's order; a sound rule gives the reference's answer in any order.
@@ -162,58 +157,6 @@ int32_t or_model_margins(const or_scene *sc, float *node_w, float *tri_w, float 
     return contained;
 }
 
-/* mcpt_core.hpp cull_back_tau restated: n (float) and tau for one triangle record */
-static float back_tau(mv3 e1, mv3 e2, float nf[3]) {
-    const double a[3] = {e1.x, e1.y, e1.z}, b[3] = {e2.x, e2.y, e2.z};
-    const double m[3] = {b[1] * a[2] - b[2] * a[1], b[2] * a[0] - b[0] * a[2], b[0] * a[1] - b[1] * a[0]};
-    const double mm = sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
-    nf[0] = nf[1] = nf[2] = 0.f;
-    if (!(mm > 0.0) || !(mm < 1e300)) return -INFINITY;
-    double dn = 0.0, nn = 0.0;
-    for (int k = 0; k < 3; k++) {
-        nf[k] = (float)(m[k] / mm);
-        const double e = (double)nf[k] - m[k] / mm;
-        dn += e * e;
-        nn += (double)nf[k] * nf[k];
-    }
-    const double fd = 1.0 + 1.0 / 1024.0;
-    double tau = ((double)M_EPS - 7.0712 * U24 * nrm(e1) * nrm(e2) * fd) / mm - fd * (sqrt(dn) * (1.0 + 1e-6) + 1e-30 + 3.0002 * U24 * sqrt(nn));
-    tau -= fabs(tau) * 1e-9 + 1e-30;
-    float t = (float)tau;
-    if ((double)t > tau) t = nextafterf(t, -INFINITY);
-    return t;
-}
-
-/* the unbounded set of mode 5: [lo, hi) and the node the traversal starts at, or hi = lo */
-typedef struct { int lo, hi, start; } uset;
-static uset find_uset(const or_scene *sc, const float *tri_w) {
-    uset u = {0, 0, 0};
-    const int N = sc->nnodes;
-    if (N <= 0 || sc->nprims[0] != 0) return u;
-    int *lo = malloc(sizeof(int) * N), *hi = malloc(sizeof(int) * N), *cnt = malloc(sizeof(int) * N);
-    for (int i = N - 1; i >= 0; i--) {
-        if (sc->nprims[i] > 0) { lo[i] = sc->offset[i]; hi[i] = sc->offset[i] + sc->nprims[i]; cnt[i] = sc->nprims[i]; }
-        else {
-            const int c0 = i + 1, c1 = sc->offset[i];
-            lo[i] = lo[c0] < lo[c1] ? lo[c0] : lo[c1];
-            hi[i] = hi[c0] > hi[c1] ? hi[c0] : hi[c1];
-            cnt[i] = cnt[c0] + cnt[c1];
-        }
-    }
-    const int ch[2] = {1, sc->offset[0]};
-    for (int k = 0; k < 2; k++) {
-        const int cu = ch[k], co = ch[1 - k];
-        if (hi[cu] - lo[cu] != cnt[cu] || hi[co] - lo[co] != cnt[co] || cnt[cu] > 64 || cnt[co] == 0) continue;
-        int all = 1;
-        for (int t = lo[cu]; t < hi[cu]; t++) all = all && isinf(tri_w[t]);
-        if (!all) continue;
-        u.lo = lo[cu]; u.hi = hi[cu]; u.start = co;
-        break;
-    }
-    free(lo); free(hi); free(cnt);
-    return u;
-}
-
 /* ---- traversal ------------------------------------------------------------------------ */
 typedef struct {
     mv3 o, d, inv;
@@ -266,8 +209,8 @@ static int m_keep(int mode, float t0, float t1, float w, const mray *r, float cu
 static int tri_key(const or_scene *sc, int id) { return sc->tri_id ? sc->tri_id[id] : id; }
 
 /* kind 0: closest hit (index, t), kind 1: any hit (1 = occluded) */
-static int m_trace(const or_scene *sc, int mode, const float *node_w, const float *tri_w, float pg, const uset *us,
-                   mv3 o, mv3 d, int kind, float *tout, uint64_t *nodes) {
+static int m_trace(const or_scene *sc, int mode, const float *node_w, const float *tri_w, float pg, mv3 o, mv3 d,
+                   int kind, float *tout, uint64_t *nodes) {
     mray r;
     r.o = o;
     r.d = d;
@@ -280,7 +223,7 @@ static int m_trace(const or_scene *sc, int mode, const float *node_w, const floa
         r.iota = fmaxf(fmaxf(fabsf(r.inv.x), fabsf(r.inv.y)), fabsf(r.inv.z)) * (float)(1.0 + CULL_SLACK);
     /* behind cut: valid only when every direction component is >= P |d| */
     r.iota_b = r.iota * pg <= 1.0f ? r.iota : INFINITY;
-    const float cfac = (mode == 2 || mode == 3 || mode == 5) ? fmaf(r.iota, pg, (float)(1.0 + CULL_SLACK)) : mode ? 1.0f + 1.0f / 256.0f : INFINITY;
+    const float cfac = (mode == 2 || mode == 3) ? fmaf(r.iota, pg, (float)(1.0 + CULL_SLACK)) : mode ? 1.0f + 1.0f / 256.0f : INFINITY;
     float best = M_HUGE;
     int bt = -1;
     float cut = kind || mode == 0 ? INFINITY : best * cfac;
@@ -296,34 +239,6 @@ static int m_trace(const or_scene *sc, int mode, const float *node_w, const floa
         return kind ? 0 : -1;
     }
     int cur = 0;
-    if (mode == 5 && us->hi > us->lo) {  /* the unbounded set first, then the other child */
-        const int bf = n2 <= (float)(1.0 + 1.0 / 512.0);
-        for (int id = us->lo; id < us->hi; id++) {
-            mv3 p0 = mld(sc->v0, id), e1 = msub(mld(sc->v1, id), p0), e2 = msub(mld(sc->v2, id), p0);
-            float nf[3];
-            const float tau = back_tau(e1, e2, nf);
-            if (bf && (d.x * nf[0] + d.y * nf[1]) + d.z * nf[2] < tau) continue;
-            float mn[3], mx[3];
-            const float *v[3] = {sc->v0 + 3 * (int64_t)id, sc->v1 + 3 * (int64_t)id, sc->v2 + 3 * (int64_t)id};
-            for (int k = 0; k < 3; k++) {
-                mn[k] = fminf(fminf(v[0][k], v[1][k]), v[2][k]);
-                mx[k] = fmaxf(fmaxf(v[0][k], v[1][k]), v[2][k]);
-            }
-            (*nodes)++;
-            if (!m_box(mn, mx, &r, &t0, &t1)) continue;
-            float t;
-            if (m_tri(sc, id, o, d, &t) && !(t < 0.f)) {
-                if (kind) {
-                    if (t < M_HUGE) { *tout = t; return 1; }
-                } else if (t < best || (t == best && bt >= 0 && tri_key(sc, id) < tri_key(sc, bt))) {
-                    best = t;
-                    bt = id;
-                    cut = best * cfac;
-                }
-            }
-        }
-        cur = us->start;
-    }
     for (;;) {
         if (sc->nprims[cur] > 0) {
             const int np = sc->nprims[cur];
@@ -386,14 +301,13 @@ void or_model_trace(const or_scene *sc, int32_t n, const float *ro, const float 
                     const float *node_w, const float *tri_w, float p, int32_t *tri, float *t, uint8_t *visible,
                     uint64_t *nodes) {
     uint64_t nn = 0;
-    const uset us = mode == 5 ? find_uset(sc, tri_w) : (uset){0, 0, 0};
     for (int32_t i = 0; i < n; i++) {
         mv3 o = mld(ro, i), d = mld(rd, i);
         float tb;
-        const int id = m_trace(sc, mode, node_w, tri_w, p, &us, o, d, 0, &tb, &nn);
+        const int id = m_trace(sc, mode, node_w, tri_w, p, o, d, 0, &tb, &nn);
         tri[i] = id >= 0 ? tri_key(sc, id) : -1;
         t[i] = tb;
-        visible[i] = (uint8_t)!m_trace(sc, mode, node_w, tri_w, p, &us, o, d, 1, &tb, &nn);
+        visible[i] = (uint8_t)!m_trace(sc, mode, node_w, tri_w, p, o, d, 1, &tb, &nn);
     }
     *nodes = nn;
 }

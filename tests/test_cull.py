@@ -200,73 +200,6 @@ def test_plane_bound_on_grazing_pairs():
     print(f"{checked} accepted axis-plane pairs, largest w / bound = {worst:.3g}")
 
 
-def back_tau(e1, e2):
-    """mcpt_core.hpp cull_back_tau in numpy (float64), per row: (n as float32, tau as float32)."""
-    a, b = e1.astype(np.float64), e2.astype(np.float64)
-    m = np.cross(b, a)
-    mm = np.linalg.norm(m, axis=1)
-    nf = (m / mm[:, None]).astype(np.float32)
-    dn = np.linalg.norm(nf.astype(np.float64) - m / mm[:, None], axis=1)
-    nn = np.linalg.norm(nf.astype(np.float64), axis=1)
-    fd = 1 + 1 / 1024
-    tau = ((np.float64(np.float32(1e-6)) - 7.0712 * U * np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1) * fd) / mm
-           - fd * (dn * (1 + 1e-6) + 1e-30 + 3.0002 * U * nn))
-    tau -= np.abs(tau) * 1e-9 + 1e-30
-    t = tau.astype(np.float32)
-    t = np.where(t.astype(np.float64) > tau, np.nextafter(t, np.float32(-np.inf)), t)
-    return nf, t
-
-
-def test_back_facing_skip_bound():
-    """The unbounded set's pre-pass (kernels.hip u_prepass) skips a triangle when fl(d . n) < tau
-    (mcpt_core.hpp cull_back_tau): then its fp32 det can never reach the 1e-6 acceptance
-    threshold.  Checked on rays at and around the det threshold's angle of large triangles (config
-    2's walls, config 3's ground quad, random large ones, |d| up to 1 + 2^-10): every pair whose
-    det is accepted has fl(d . n) >= tau, and rays a little more back-facing are skipped."""
-    rng = np.random.default_rng(17)
-    f = np.float32
-    checked, skipped = 0, 0
-    worst = -np.inf
-    pools = []
-    for cid in (2, 3):
-        import mcpt
-        a = mcpt.build_config_scene(cid).arrays()
-        big, _ = triangle_pools(a, n_big=12)
-        pools.append((np.asarray(a["v0"], f)[big], np.asarray(a["v1"], f)[big], np.asarray(a["v2"], f)[big]))
-    m = 20000
-    sz = (10.0 ** rng.uniform(-2, 3, m))[:, None]
-    v0 = (rng.normal(size=(m, 3)) * sz).astype(f)
-    pools.append((v0, (v0 + rng.normal(size=(m, 3)) * sz).astype(f), (v0 + rng.normal(size=(m, 3)) * sz).astype(f)))
-    for V0, V1, V2 in pools:
-        n_rows = 400000
-        T = rng.integers(0, len(V0), n_rows)
-        v0, v1, v2 = V0[T], V1[T], V2[T]
-        e1, e2 = v1 - v0, v2 - v0
-        nf, tau = back_tau(e1, e2)
-        mm = np.linalg.norm(np.cross(e2.astype(np.float64), e1.astype(np.float64)), axis=1)
-        # d . m^ around the det threshold: c * (1e-6 / |m|) with c in [-30, 30], plus exact-grazing
-        c = rng.uniform(-30, 30, n_rows) * (1e-6 / mm)
-        c[: n_rows // 10] = 0.0
-        r = rng.normal(size=(n_rows, 3))
-        mh = nf.astype(np.float64)
-        tang = r - np.sum(r * mh, 1, keepdims=True) * mh
-        tang /= np.linalg.norm(tang, axis=1, keepdims=True)
-        d = tang * np.sqrt(np.maximum(1 - c * c, 0))[:, None] + c[:, None] * mh
-        d *= (1 + rng.uniform(-1, 1, n_rows) / 1024)[:, None]  # |d| up to 1 + 2^-10
-        d = d.astype(f)
-        o = (v0 - d * f(1.0)).astype(f)
-        ok, det, _ = mt_fp32(o, d, v0, e1, e2)
-        acc = det.astype(np.float64) >= np.float64(f(1e-6))
-        g = (d[:, 0] * nf[:, 0] + d[:, 1] * nf[:, 1]) + d[:, 2] * nf[:, 2]
-        assert (g[acc] >= tau[acc]).all(), f"{(g[acc] < tau[acc]).sum()} accepted dets below tau"
-        checked += int(acc.sum())
-        skipped += int((g < tau).sum())
-        if acc.any():
-            worst = max(worst, float(((tau[acc] - g[acc]) / np.maximum(np.abs(tau[acc]), 1e-30)).max()))
-    assert checked > 100000 and skipped > 100000, (checked, skipped)
-    print(f"{checked} accepted dets, all with fl(d . n) >= tau; {skipped} rays skipped")
-
-
 # ---- the traversal model on adversarial rays ------------------------------------------------
 SCENES = [("c2", 1.0), ("c2", 1e3), ("c2", 1e-3), ("c3", 1.0), ("floor", 1.0)]
 
@@ -287,8 +220,7 @@ def adv_scenes(mcpt_mod, scene_c3):
 
 @pytest.mark.parametrize("name,scale", SCENES)
 def test_round4_cull_model_equals_reference(oracle, adv_scenes, name, scale):
-    """The round-4 rule (mode 2 of oracle/trav_model.c, the product's keep_box; mode 5 with the
-    unbounded set tested ahead of the traversal, kernels.hip u_prepass) gives the
+    """The round-4 rule (mode 2 of oracle/trav_model.c, the product's keep_box) gives the
     reference's closest hit and visibility on every adversarial ray; mode 0 (no culling) is the
     model's own check against the oracle."""
     a = adv_scenes[(name, scale)]
@@ -299,7 +231,7 @@ def test_round4_cull_model_equals_reference(oracle, adv_scenes, name, scale):
     m = oracle.model_margins(a)
     assert m["contained"]
     pos_t, _, _ = oracle.trace_closest(a, ro, rd)
-    for mode in (0, 2, 5):
+    for mode in (0, 2):
         tri, t, vis, boxes = oracle.model_trace(a, ro, rd, mode, m)
         assert np.array_equal(tri, otri), f"mode {mode}: {(tri != otri).sum()} closest hits differ"
         assert np.array_equal(t.view(np.uint32), pos_t[:, 3].view(np.uint32))
