@@ -401,8 +401,11 @@ def run_strong(pt, rc, rank, world, dist, backend, spp, args, torch):
     W, H = rc.width, rc.height
     slots = parallel.strong_slots(args.slots or BENCH_SLOTS[args.config], world, W, H, spp)
     tile = part_tile(world)
-    pt.set_path_slots(slots)
+    # the strong frame first, at the weak run's slot count (frees the weak film), then its slots:
+    # set_path_slots re-allocates at the current film size, and the weak film with the strong
+    # split's slots would not fit (N = 8 on 1080p: 1920 x 8640 px x 131 slots, 274 GB)
     pt.resize(W, H, tile, tile)
+    pt.set_path_slots(slots)
     pt.set_tiles(tiles_for(rank, world, W, H, tile))
     dt, st = timed_frames(pt, args.steps, args.warmup, dist, torch)
     per = rank_times(dist, dev_of(backend), dt, st.rays, world, torch)

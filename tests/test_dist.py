@@ -202,3 +202,101 @@ def test_multi_gpu_tile_balances_pixels():
                           parallel.tiles_for_rank(r, world, W, H, T)) for r in range(world)]
             assert sum(counts) == W * H and max(counts) / (W * H / world) < 1.02
     assert bench.part_tile(1) == 256 and bench.part_tile(8) == T
+
+
+class _FakeStats:
+    def __init__(self, px):
+        for k in ("extend_rays", "shadow_rays", "vis_rays", "iterations", "ms_shade", "ms_extend", "ext_nodes",
+                  "ext_tests", "ext_hits", "any_nodes", "any_tests", "any_hits"):
+            setattr(self, k, 0)
+        self.extend_rays = px
+
+
+class _FakeTracer:
+    """The allocation rules of mcpt_film_resize / mcpt_set_path_slots (runtime.cpp): path state for
+    W x H x slots paths, refused at >= 2^31 paths, re-allocated at the current film size by
+    set_path_slots; plus a per-GPU memory cap (one MI355X: 288 GB) at ~234 B per path (state +
+    queues)."""
+    CAP = 288e9
+
+    def __init__(self):
+        self.W = self.H = 0
+        self.slots = 1
+        self.peak = 0.0
+        self.tiles = None
+
+    def _alloc(self, W, H, slots):
+        P = W * H * slots
+        assert P < 2 ** 31, f"film too large for the path slots: {W}x{H}x{slots}"
+        assert P * 234 <= self.CAP, f"out of memory: {W}x{H}x{slots}"
+        self.peak = max(self.peak, P * 234)
+
+    def set_path_slots(self, s):
+        if self.W:
+            self._alloc(self.W, self.H, s)
+        self.slots = s
+
+    def resize(self, W, H, tw, th):
+        self._alloc(W, H, self.slots)
+        self.W, self.H = W, H
+
+    def set_tiles(self, t):
+        self.tiles = t
+
+    def clear(self):
+        pass
+
+    def render(self):
+        import time
+        time.sleep(0.002)  # a frame takes time (per-rank seconds are rounded to 0.1 ms)
+        return _FakeStats(len(self.tiles or []))
+
+    def occ_stats(self):
+        return 0, True
+
+    def ray_counts(self):
+        return {}
+
+
+class _FakeDist:
+    def __init__(self, world):
+        self.world = world
+
+    def barrier(self):
+        pass
+
+    def all_gather(self, out, t):
+        for o in out:
+            o.copy_(t)
+
+    def get_backend(self):
+        return "gloo"
+
+
+def test_strong_split_fits_after_the_weak_frame():
+    """bench.py main renders the weak frame (1920 x 1080 N at the base slots), then run_strong
+    switches to the config's own frame with the strong split's slots.  The switch must shrink the
+    film before raising the slots: set_path_slots at the weak film's size would ask for
+    1920 x 8640 x 131 paths at N = 8 (2^31 and 274 GB: the round-4 rehearsal at N = 4 ran out of
+    memory this way).  Checked for N = 2 / 4 / 8 on configs 2 and 4 with the allocator's rules."""
+    import argparse
+    import types
+
+    import torch
+
+    import bench
+    import mcpt
+
+    fake_torch = types.SimpleNamespace(cuda=types.SimpleNamespace(synchronize=lambda: None), tensor=torch.tensor,
+                                       zeros_like=torch.zeros_like, float64=torch.float64)
+    for cid in (2, 4):
+        rc = mcpt.CONFIGS[cid]
+        for world in (2, 4, 8):
+            pt = _FakeTracer()
+            base = bench.BENCH_SLOTS[cid]
+            pt.set_path_slots(base)
+            pt.resize(rc.width, rc.height * world, bench.part_tile(world), bench.part_tile(world))  # the weak frame
+            args = argparse.Namespace(slots=None, config=cid, steps=1, warmup=0, no_gather=True, no_verify_gather=True)
+            out = bench.run_strong(pt, rc, 0, world, _FakeDist(world), "gloo", rc.spp, args, fake_torch)
+            assert (pt.W, pt.H) == (rc.width, rc.height) and out["slots"] == pt.slots
+            assert pt.peak <= _FakeTracer.CAP
