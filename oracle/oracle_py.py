@@ -75,6 +75,7 @@ def lib():
                                          _f, _f, _f, _f, _f, _f]),
             "or_version": (C.c_char_p, []),
             "or_model_margins": (C.c_int32, [C.POINTER(OrScene), _f, _f, _f]),
+            "or_model_set_safe": (None, [C.c_double]),
             "or_model_trace": (None, [C.POINTER(OrScene), C.c_int32, _f, _f, C.c_int32, _f, _f, C.c_float, _i, _f,
                                       C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)]),
         }
@@ -187,20 +188,24 @@ def trace_any(arrays, ro, rd, traversal=0):
     return vis
 
 
-def model_margins(arrays):
+def model_margins(arrays, safe_c=0.0):
     """Margins of the product culling rule's model (trav_model.c): per desc node, per triangle own
-    box, the far coefficient P and whether every node box contains its subtree's vertices."""
+    box, the far coefficient P and whether every node box contains its subtree's vertices.
+    safe_c > 0: mode 6's margins (unbounded triangles bounded for rays at |cos| >= safe_c)."""
+    lib().or_model_set_safe(float(safe_c))
     s = scene_struct(arrays)
     nw = np.zeros(max(1, s.nnodes), np.float32)
     tw = np.zeros(max(1, s.ntri), np.float32)
     p = np.zeros(1, np.float32)
     ok = lib().or_model_margins(C.byref(s), fptr(nw), fptr(tw), fptr(p))
+    lib().or_model_set_safe(0.0)
     return {"node_w": nw, "tri_w": tw, "p": float(p[0]), "contained": bool(ok)}
 
 
 def model_trace(arrays, ro, rd, mode, margins=None):
     """trav_model.c: closest (triangle id, t) and any-hit visibility under culling rule `mode`
-    (0 none, 1 round 3, 2 round 4) and the number of boxes tested."""
+    (0 none, 1 round 3, 2 round 4, 6 round-5 candidate with safe-ray margins) and the number of
+    boxes tested."""
     s = scene_struct(arrays)
     m = margins or model_margins(arrays)
     ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)

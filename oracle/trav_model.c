@@ -17,6 +17,11 @@
  *           the rounding error of the fp32 Moller-Trumbore expressions with the det >= 1e-6
  *           acceptance threshold (Triangle.cu:17-21).  Skip when t1 (1 - 2^-18) + W i < 0 (behind)
  *           or t0 - W i > t_best (1 + 2^-18 + i P) (beyond), i = max |1/d_a| (1 + 2^-18).
+ *   mode 6  a round-5 candidate (not in the product): margins from
+ *           or_model_set_safe(c) give the triangles the general bound leaves unbounded the margin
+ *           of rays with |d . m^| >= c |d| (then det >= |d| (c |m| - 7.0712 u |e1| |e2|), no
+ *           threshold needed); a ray within c of any such triangle's plane is traced with no
+ *           culling (mode 0), every other ray with mode 2's rule.
  * The margins come from or_model_margins (a restatement of the product's k_cull_margins in C).
  * Visit order: both children of an interior node are tested, the nearer (entry t) is visited
  * first -- the product's order; a sound rule gives the reference's answer in any order.
@@ -91,6 +96,17 @@ static double plane_b(mv3 e1, mv3 e2) {
  * ever culled).  A box's margin is the maximum over the triangles it holds.  *far: the
  * triangle's coefficient of t_best in the far cut (P is their maximum). */
 static float to_f_up(double w) { return isinf(w) ? INFINITY : (float)(w * (1.0 + 1.0 / 1048576.0)) * (1.0f + 1.0f / 1048576.0f); }
+static double g_safe_c = 0.0; /* or_model_set_safe: 0 = the product's margins */
+void or_model_set_safe(double c) { g_safe_c = c; }
+/* beta of the safe-ray bound: |R_a| / det <= 28.285 u |tvec| |e1| |e2| / K, K = c |m| - 7.0712 u |e1| |e2| */
+static double safe_beta(mv3 e1, mv3 e2, double c) {
+    const double a[3] = {e1.x, e1.y, e1.z}, b[3] = {e2.x, e2.y, e2.z};
+    const double m[3] = {b[1] * a[2] - b[2] * a[1], b[2] * a[0] - b[0] * a[2], b[0] * a[1] - b[1] * a[0]};
+    const double mm = sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]) * (1.0 - 1e-12);
+    const double k = c * mm - 7.0712 * U24 * nrm(e1) * nrm(e2) * (1.0 + 1e-12);
+    if (!(k > 0.0)) return INFINITY;
+    return 28.3 * U24 * nrm(e1) * nrm(e2) / k * (1.0 + 1e-9) + 1.01 * U24;
+}
 static double tri_w_of(const or_scene *sc, int t, double *far) {
     mv3 a = mld(sc->v0, t), b = mld(sc->v1, t), c = mld(sc->v2, t);
     mv3 e1 = msub(b, a), e2 = msub(c, a), e3 = msub(c, b);
@@ -99,6 +115,7 @@ static double tri_w_of(const or_scene *sc, int t, double *far) {
     const double pb = plane_b(e1, e2);
     if (pb > 0.0) be = (1.01 * U24 + pb) * (1.0 + 1.0 / 8388608.0);
     *far = 0.0;
+    if (!(1.7321 * be * (1.0 + CULL_SLACK) < 0.5) && g_safe_c > 0.0 && pb == 0.0) be = safe_beta(e1, e2, g_safe_c);
     if (!(1.7321 * be * (1.0 + CULL_SLACK) < 0.5)) return INFINITY;
     const double l1 = nrm(e1), l2 = nrm(e2), l3 = nrm(e3) * (1.0 + 1e-7);
     const double diam = l1 > l2 ? (l1 > l3 ? l1 : l3) : (l2 > l3 ? l2 : l3);
@@ -301,13 +318,51 @@ void or_model_trace(const or_scene *sc, int32_t n, const float *ro, const float 
                     const float *node_w, const float *tri_w, float p, int32_t *tri, float *t, uint8_t *visible,
                     uint64_t *nodes) {
     uint64_t nn = 0;
+    /* mode 6: the planes of the triangles the general bound leaves unbounded (n as float, thr) */
+    int np = 0;
+    float *pl = NULL;
+    if (mode == 6) {
+        pl = malloc(sizeof(float) * 4 * (size_t)(sc->ntri > 0 ? sc->ntri : 1));
+        for (int t = 0; t < sc->ntri; t++) {
+            mv3 p0 = mld(sc->v0, t), e1 = msub(mld(sc->v1, t), p0), e2 = msub(mld(sc->v2, t), p0);
+            double be, om;
+            tri_beta_omega(e1, e2, &be, &om);
+            if (1.7321 * be * (1.0 + CULL_SLACK) < 0.5 || plane_b(e1, e2) > 0.0) continue;
+            float nf[3];
+            const double a3[3] = {e1.x, e1.y, e1.z}, b3[3] = {e2.x, e2.y, e2.z};
+            const double m[3] = {b3[1] * a3[2] - b3[2] * a3[1], b3[2] * a3[0] - b3[0] * a3[2], b3[0] * a3[1] - b3[1] * a3[0]};
+            const double mm = sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+            double dn = 0.0, nn2 = 0.0;
+            for (int k = 0; k < 3; k++) {
+                nf[k] = mm > 0.0 ? (float)(m[k] / mm) : 0.f;
+                const double e = (double)nf[k] - (mm > 0.0 ? m[k] / mm : 0.0);
+                dn += e * e;
+                nn2 += (double)nf[k] * nf[k];
+            }
+            const double fd = 1.0 + 1.0 / 1024.0;
+            const double thr = g_safe_c * fd + fd * (sqrt(dn) * (1.0 + 1e-6) + 1e-30 + 3.0002 * U24 * sqrt(nn2));
+            float ft = (float)(thr * (1.0 + 1e-9));
+            if ((double)ft < thr) ft = nextafterf(ft, INFINITY);
+            pl[4 * np] = nf[0]; pl[4 * np + 1] = nf[1]; pl[4 * np + 2] = nf[2]; pl[4 * np + 3] = mm > 0.0 ? ft : INFINITY;
+            np++;
+        }
+    }
     for (int32_t i = 0; i < n; i++) {
         mv3 o = mld(ro, i), d = mld(rd, i);
         float tb;
-        const int id = m_trace(sc, mode, node_w, tri_w, p, o, d, 0, &tb, &nn);
+        int rmode = mode;
+        if (mode == 6) {
+            rmode = 2;
+            for (int k = 0; k < np; k++) {
+                const float g = (d.x * pl[4 * k] + d.y * pl[4 * k + 1]) + d.z * pl[4 * k + 2];
+                if (!(fabsf(g) >= pl[4 * k + 3])) { rmode = 0; break; }
+            }
+        }
+        const int id = m_trace(sc, rmode, node_w, tri_w, p, o, d, 0, &tb, &nn);
         tri[i] = id >= 0 ? tri_key(sc, id) : -1;
         t[i] = tb;
-        visible[i] = (uint8_t)!m_trace(sc, mode, node_w, tri_w, p, o, d, 1, &tb, &nn);
+        visible[i] = (uint8_t)!m_trace(sc, rmode, node_w, tri_w, p, o, d, 1, &tb, &nn);
     }
+    free(pl);
     *nodes = nn;
 }

@@ -121,13 +121,13 @@ def near_rays(a, m, seed, pool, scale=1.0):
     return o.astype(np.float32), d.astype(np.float32)
 
 
-def grazing_rays(a, m, seed, pool, scale=1.0):
+def grazing_rays(a, m, seed, pool, scale=1.0, band=(1e-6, 1e-3)):
     rng = np.random.default_rng(seed)
     T = pool[rng.integers(0, len(pool), m)]
     v0, v1, v2, n = _tri_frames(a, T)
     u, v = _bary(rng, m)
     q = v0 + u[:, None] * (v1 - v0) + v[:, None] * (v2 - v0)
-    d, _ = _grazing_dir(rng, n)
+    d, _ = _grazing_dir(rng, n, lo=band[0], hi=band[1])
     t = scale * rng.uniform(0.01, 3.0, m)
     o = q - t[:, None] * d + scale * 1e-5 * rng.normal(size=(m, 3))
     return o.astype(np.float32), d.astype(np.float32)

@@ -264,6 +264,85 @@ def test_cull_margins_monotone_and_scale_free(oracle, adv_scenes):
     assert np.isfinite(m["tri_w"]).mean() > 0.99
 
 
+# ---- a round-5 candidate, modelled on the CPU ---------------
+SAFE_C = 1e-3
+
+
+def test_safe_ray_bound_on_grazing_pairs():
+    """For rays with |d . m^| >= c |d| (m = e2 x e1) the det is either rejected or >= |d| K,
+    K = c |m| - 7.0712 u |e1| |e2|, so the accepted point lies within omega + beta |tvec| of the
+    triangle's box with beta = 28.3 u |e1| |e2| / K + 1.01 u -- no det threshold, and finite for
+    config 2's walls (the general bound is not).  Checked on config 2/3's largest triangles for rays
+    at |cos| in [c, 30 c], the band where the bound is tightest."""
+    import mcpt
+
+    rng = np.random.default_rng(23)
+    checked, worst = 0, 0.0
+    for cid in (2, 3):
+        a = mcpt.build_config_scene(cid).arrays()
+        big, _ = triangle_pools(a, n_big=12)
+        m = 300000
+        T = big[rng.integers(0, len(big), m)]
+        v0, v1, v2 = (np.asarray(a[k], np.float32)[T] for k in ("v0", "v1", "v2"))
+        e1, e2 = v1 - v0, v2 - v0
+        mvec = np.cross(e2.astype(np.float64), e1.astype(np.float64))
+        mm = np.linalg.norm(mvec, axis=1)
+        mh = mvec / mm[:, None]
+        c = SAFE_C * 10.0 ** rng.uniform(0, np.log10(30), m)
+        r = rng.normal(size=(m, 3))
+        tang = r - np.sum(r * mh, 1, keepdims=True) * mh
+        tang /= np.linalg.norm(tang, axis=1, keepdims=True)
+        d = (tang * np.sqrt(1 - c * c)[:, None] + c[:, None] * mh).astype(np.float32)  # front-facing
+        bu, bv = rng.random(m), rng.random(m)
+        flip = bu + bv > 1
+        bu[flip], bv[flip] = 1 - bu[flip], 1 - bv[flip]
+        q = v0 + bu[:, None] * e1 + bv[:, None] * e2
+        q = q + (rng.normal(size=(m, 3)) * 1e-3).astype(np.float32)
+        o = (q - rng.uniform(0.01, 4.0, m)[:, None] * d).astype(np.float32)
+        ok, det, nn = mt_fp32(o, d, v0, e1, e2)
+        tp = nn.astype(np.float64) / det.astype(np.float64)
+        P = o.astype(np.float64) + tp[:, None] * d.astype(np.float64)
+        lo = np.minimum(np.minimum(v0, v1), v2).astype(np.float64)
+        hi = np.maximum(np.maximum(v0, v1), v2).astype(np.float64)
+        w = np.maximum(np.maximum(lo - P, P - hi), 0.0).max(axis=1)
+        n1 = np.linalg.norm(e1.astype(np.float64), axis=1)
+        n2 = np.linalg.norm(e2.astype(np.float64), axis=1)
+        K = SAFE_C * mm - 7.0712 * U * n1 * n2
+        beta = 28.3 * U * n1 * n2 / K + 1.01 * U
+        bound = 2.1 * U * np.maximum(n1, n2) + beta * np.linalg.norm(o.astype(np.float64) - v0.astype(np.float64), axis=1)
+        sel = ok & np.isfinite(tp) & (K > 0)
+        assert (w[sel] <= bound[sel]).all(), f"bound violated on {(w[sel] > bound[sel]).sum()} pairs"
+        checked += int(sel.sum())
+        worst = max(worst, float((w[sel] / bound[sel]).max()))
+    assert checked > 200000, checked
+    print(f"{checked} accepted pairs at |cos| in [c, 30c], largest w / bound = {worst:.3g}")
+
+
+@pytest.mark.parametrize("name,scale", [("c2", 1.0), ("c2", 1e3), ("c2", 1e-3)])
+def test_safe_ray_margins_model_equals_reference(oracle, adv_scenes, name, scale):
+    """Mode 6 of oracle/trav_model.c (the walls' finite margins for rays at |cos| >= 1e-3 to every
+    wall plane, no culling for the others) against the cull-free reference, on the adversarial rays
+    plus grazing rays in the band [5e-4, 2e-2] around the switch; and its box tests against mode 2's."""
+    from adversarial import grazing_rays
+
+    a = adv_scenes[(name, scale)]
+    ro, rd = adversarial_rays(a, 200000, seed=31, scale=scale)
+    big, _ = triangle_pools(a)
+    o2, d2 = grazing_rays(a, 100000, 37, big, scale, band=(5e-4, 2e-2))
+    ro, rd = np.concatenate([ro, o2]), np.concatenate([rd, d2])
+    _, _, otri = oracle.trace_closest(a, ro, rd)
+    ovis = oracle.trace_any(a, ro, rd)
+    pos_t, _, _ = oracle.trace_closest(a, ro, rd)
+    m6 = oracle.model_margins(a, safe_c=SAFE_C)
+    assert np.isfinite(m6["tri_w"][big[:10]]).all()  # the walls are bounded for safe rays
+    tri, t, vis, boxes6 = oracle.model_trace(a, ro, rd, 6, m6)
+    assert np.array_equal(tri, otri), f"{(tri != otri).sum()} closest hits differ"
+    assert np.array_equal(t.view(np.uint32), pos_t[:, 3].view(np.uint32))
+    assert np.array_equal(vis, ovis), f"{(vis != ovis).sum()} visibilities differ"
+    _, _, _, boxes2 = oracle.model_trace(a, ro, rd, 2, oracle.model_margins(a))
+    print(f"box tests: mode 2 {boxes2}, mode 6 {boxes6}")
+
+
 # ---- the product on the GPU -----------------------------------------------------------------
 GPU_SCENES = [("c2", 1.0, 1000000), ("c2", 1e3, 1000000), ("c2", 1e-3, 1000000), ("c3", 1.0, 1000000),
               ("floor", 1.0, 1000000), ("c5", 1.0, 500000)]
