@@ -14,17 +14,19 @@ this exact layout).  `--steady` reports the steady-state iteration rate beside i
 Multi-GPU: one process per GPU.  `--gpus N` without an external launcher starts
 the N ranks itself (torch.distributed.run, before anything touches the GPU); under a launcher
 WORLD_SIZE must equal N.  Film tiles are dealt to ranks by (tx + ty) mod N (64 x 64 tiles for
-N > 1: MULTI_TILE).
-  --scaling weak (default): the frame is 1920 x 1080*N pixels of the same view (N-fold vertical
-      supersampling), so every rank owns ~one 1080p frame of pixels with the same sky / geometry
-      mix as the 1-GPU run;
-  --scaling strong: the config's own frame (e.g. --config 4: 3840x2160) split over the ranks.
-Under weak scaling an N>1 run then also times the strong split of the config's own frame
-("strong" in the JSON: per-rank times, path slots scaled by each rank's pixel share) and, after
-timing, gathers that frame into rank 0's device film (mcpt/parallel.py: point-to-point RCCL
-sends over xGMI) and checks it against rank 0 rendering the frame alone, bit for bit
-(--no-strong / --no-gather / --no-verify-gather skip these).  No collective runs inside a
-timed region: tiles are independent.
+N > 1: MULTI_TILE), and every rank holds path state for its own tiles only
+(mcpt_set_compact_paths).
+  --scaling strong (default): `value` is the metric's own frame (1920 x 1080 for config 2; 3840 x
+      2160 for --config 4) split over the ranks, path slots scaled by the rank's pixel share
+      (parallel.strong_slots) so every GPU keeps the one-GPU run's paths in flight;
+  --scaling weak: `value` is a 1920 x 1080*N frame of the same view (N-fold vertical
+      supersampling): every rank owns ~one 1080p frame of pixels with the 1-GPU run's sky /
+      geometry mix.
+An N>1 run also times the other split as a sub-object ("weak" / "strong"; --no-weak / --no-strong
+skip it).  After timing, the strong frame is gathered into rank 0's device film (mcpt/parallel.py:
+point-to-point RCCL sends over xGMI) and rank 0 re-renders every other rank's tiles alone and
+compares them with the gathered pixels bit for bit (--no-gather / --no-verify-gather skip these).
+No collective runs inside a timed region: tiles are independent.
 """
 from __future__ import annotations
 
@@ -64,16 +66,22 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=5, help="timed frames")
     ap.add_argument("--warmup", type=int, default=1, help="untimed frames before the timed ones")
     ap.add_argument("--config", type=int, default=2)
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="N>1: which split `value` reports (the other is timed as a sub-object)")
     ap.add_argument("--spp", type=int, default=None, help="override the config's spp (not the BASELINE workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=12, help="spp of the full-frame CPU-oracle sample")
     ap.add_argument("--no-strong", action="store_true",
-                    help="N>1: skip the strong-scaling split of the config's own frame (run after the weak frames)")
+                    help="N>1 with --scaling weak: skip the strong split of the config's own frame (the sub-object)")
+    ap.add_argument("--no-weak", action="store_true",
+                    help="N>1 with --scaling strong: skip the weak 1920 x 1080N frame (the sub-object)")
     ap.add_argument("--no-gather", action="store_true",
                     help="N>1: skip the frame-end gather of the strong frame into rank 0's device film (RCCL)")
     ap.add_argument("--no-verify-gather", action="store_true",
                     help="N>1: skip checking the gathered frame against rank 0 rendering it alone (bit for bit)")
+    ap.add_argument("--no-work-counters", action="store_true",
+                    help="skip rank 0's extra untimed frame with the counting k_trace build (the roofline's per-ray "
+                         "node / triangle figures are then absent); the rocprofv3 passes use it")
     ap.add_argument("--steady", action="store_true",
                     help="also time 60 steady-state iterations (outside value; off by default so that every "
                          "k_trace launch of the process belongs to a timed or warmup frame, as rocprofv3 sees it)")
@@ -390,51 +398,97 @@ def rank_times(dist, dev, dt, rays, world, torch):
             "max_over_mean": round(max(t) / mean, 4) if mean > 0 else None}
 
 
-def run_strong(pt, rc, rank, world, dist, backend, spp, args, torch):
-    """Strong scaling: the config's own frame split over the ranks by the tile
-    partition, path slots scaled so every rank keeps the one-GPU run's paths in flight
-    (parallel.strong_slots).  Then, outside the timed region, the frame-end gather of the film into
-    rank 0's device film (point-to-point sends over RCCL / xGMI) and its check against rank 0
-    rendering the whole frame alone with the same slots (bit for bit)."""
+def set_layout(pt, rc, rank, world, kind, spp, args):
+    """Film, tile set and path slots of one split.  kind "strong": the config's own frame over the
+    ranks, slots scaled by the rank's pixel share (parallel.strong_slots); "weak": 1920 x 1080N at the
+    base slots.  N > 1: compact path state (the rank's tiles only, mcpt_set_compact_paths), allocated
+    film first (one slot), then the tile set, then the slots -- never slots x the whole frame."""
+    from mcpt import parallel
+
+    W, H = frame_size(rc, world, kind)
+    tile = part_tile(world)
+    base = args.slots or BENCH_SLOTS[args.config]
+    slots = parallel.strong_slots(base, world, W, H, spp, tile) if kind == "strong" else base
+    tiles = tiles_for(rank, world, W, H, tile)
+    if world == 1:
+        pt.set_path_slots(slots)
+        pt.resize(W, H, tile, tile)
+        pt.set_tiles(tiles)
+    else:
+        pt.set_compact_paths(True)
+        pt.set_path_slots(1)
+        pt.resize(W, H, tile, tile)
+        pt.set_tiles(tiles)
+        pt.set_path_slots(slots)
+    return {"frame": [W, H], "tile": tile, "slots": slots, "tiles": tiles,
+            "path_pixels_rank": len(tiles) * tile * tile if world > 1 else W * H}
+
+
+def run_split(pt, rc, rank, world, dist, backend, kind, spp, args, torch):
+    """One split timed (warmup + steps frames): its layout, the rank's own timing, every rank's
+    (seconds, Mray/s) and the job's value (all ranks' rays / the max-over-ranks time)."""
+    lay = set_layout(pt, rc, rank, world, kind, spp, args)
+    dt, st = timed_frames(pt, args.steps, args.warmup, dist, torch)
+    out = {"kind": kind, "layout": lay, "dt": dt, "st": st, "dt_all": dt, "rays_all": float(st.rays), "per_rank": None}
+    if dist:
+        per = rank_times(dist, dev_of(backend), dt, st.rays, world, torch)
+        out["per_rank"] = per
+        out["dt_all"] = max(per["seconds"])
+        out["rays_all"] = sum(b * a * 1e6 for a, b in zip(per["seconds"], per["mray_s"]))
+    return out
+
+
+def split_summary(run, args, world):
+    """The JSON sub-object of a split that is not the headline."""
+    lay = run["layout"]
+    return {"frame": lay["frame"], "slots": lay["slots"], "spp": run["spp"], "steps": args.steps,
+            "ms_per_frame": round(run["dt_all"] * 1e3 / args.steps, 3),
+            "mray_s": round(run["rays_all"] / run["dt_all"] / 1e6, 2), "per_rank": run["per_rank"],
+            "tile": lay["tile"], "path_pixels_per_rank": lay["path_pixels_rank"],
+            "tiles_per_rank": [len(tiles_for(r, world, lay["frame"][0], lay["frame"][1], lay["tile"]))
+                               for r in range(world)]}
+
+
+def gather_and_verify(pt, rc, rank, world, dist, spp, args, torch):
+    """The strong frame's frame-end gather into rank 0's device film (point-to-point sends over
+    RCCL / xGMI), outside any timed region, and its check: rank 0 re-renders every other rank's
+    tiles alone (same path slots, so the same summation order) and compares them with the gathered
+    pixels bit for bit.  The film must hold the strong layout (set_layout)."""
+    import numpy as np
+
     from mcpt import parallel
 
     W, H = rc.width, rc.height
-    slots = parallel.strong_slots(args.slots or BENCH_SLOTS[args.config], world, W, H, spp)
     tile = part_tile(world)
-    # the strong frame first, at the weak run's slot count (frees the weak film), then its slots:
-    # set_path_slots re-allocates at the current film size, and the weak film with the strong
-    # split's slots would not fit (N = 8 on 1080p: 1920 x 8640 px x 131 slots, 274 GB)
-    pt.resize(W, H, tile, tile)
-    pt.set_path_slots(slots)
-    pt.set_tiles(tiles_for(rank, world, W, H, tile))
-    dt, st = timed_frames(pt, args.steps, args.warmup, dist, torch)
-    per = rank_times(dist, dev_of(backend), dt, st.rays, world, torch)
-    tmax = max(per["seconds"])
-    rays = sum(b * a * 1e6 for a, b in zip(per["seconds"], per["mray_s"]))
-    out = {"frame": [W, H], "slots": slots, "spp": spp, "steps": args.steps,
-           "ms_per_frame": round(tmax * 1e3 / args.steps, 3), "mray_s": round(rays / tmax / 1e6, 2),
-           "per_rank": per, "tile": tile, "tiles_per_rank": [len(tiles_for(r, world, W, H, tile)) for r in range(world)]}
-    if not args.no_gather:
-        pt.clear()
-        pt.render()  # the film the gather moves: one whole strong frame
-        torch.cuda.synchronize()
-        dist.barrier()
-        tg = time.perf_counter()
-        parallel.gather_film_to_root(pt, rank, world, tile)
-        torch.cuda.synchronize()
-        out["gather_s"] = round(time.perf_counter() - tg, 4)
-        out["gather_backend"] = dist.get_backend()
-        if not args.no_verify_gather and rank == 0:
-            import numpy as np
-
-            Lg, sg = pt.film()  # the gathered frame
-            pt.set_tiles(None)  # every tile on rank 0 alone: the reference film
-            pt.clear()
-            pt.render()
-            Lr, sr = pt.film()
-            out["gather_equals_one_rank_frame"] = bool(np.array_equal(Lg.view(np.uint32), Lr.view(np.uint32)) and
-                                                       np.array_equal(sg, sr))
-        dist.barrier()
+    out = {}
+    pt.clear()
+    pt.render()  # the film the gather moves: one whole strong frame
+    torch.cuda.synchronize()
+    dist.barrier()
+    tg = time.perf_counter()
+    parallel.gather_film_to_root(pt, rank, world, tile)
+    torch.cuda.synchronize()
+    out["gather_s"] = round(time.perf_counter() - tg, 4)
+    out["gather_backend"] = dist.get_backend()
+    if not args.no_verify_gather and rank == 0:
+        Lg, sg = pt.film()  # the gathered frame
+        ok, covered = True, 0
+        for r in range(world):
+            tr = tiles_for(r, world, W, H, tile)
+            if not tr:
+                continue
+            if r:
+                pt.set_tiles(tr)  # compact: re-allocates for rank r's tiles and clears the film
+                pt.render()
+            Lr, sr = pt.film() if r else (Lg, sg)
+            m = np.zeros((H, W), bool)
+            for tx, ty in tr:
+                m[ty * tile:(ty + 1) * tile, tx * tile:(tx + 1) * tile] = True
+            ok = ok and bool(np.array_equal(Lg[m].view(np.uint32), Lr[m].view(np.uint32)) and np.array_equal(sg[m], sr[m]))
+            covered += int(m.sum())
+        out["gather_equals_one_rank_frame"] = bool(ok and covered == W * H and int(sg.sum()) > 0)
+        out["verify"] = "rank 0 re-rendered every other rank's tiles alone; gathered pixels equal bit for bit"
+    dist.barrier()
     return out
 
 
@@ -469,26 +523,20 @@ def main():
 
     import mcpt
 
-    from mcpt import parallel
-
     rc = mcpt.CONFIGS[args.config]
     spp = args.spp or rc.spp
-    slots = args.slots or BENCH_SLOTS[args.config]
-    if args.scaling == "strong" and world > 1:  # each rank owns 1/N of the pixels: keep its paths in flight
-        slots = parallel.strong_slots(slots, world, rc.width, rc.height, spp)
-    W, H = frame_size(rc, world, args.scaling)
     scene = mcpt.build_config_scene(args.config)
     cam = mcpt.config_camera(rc, rc.width, rc.height)  # the config's view at any N (see docstring)
     pt = mcpt.PathTracer(local, mcpt.default_config(spp=spp, max_depth=rc.max_depth))
     pt.upload_scene(scene)
     pt.set_camera(cam)
-    pt.set_path_slots(slots)
-    tile = part_tile(world)
-    pt.resize(W, H, tile, tile)
-    my_tiles = tiles_for(rank, world, W, H, tile)
-    pt.set_tiles(my_tiles)
 
-    dt, st = timed_frames(pt, args.steps, args.warmup, dist, torch)
+    # the headline split (value); N = 1: the config's frame on one GPU (both splits are that frame)
+    head = run_split(pt, rc, rank, world, dist, backend, args.scaling, spp, args, torch)
+    head["spp"] = spp
+    dt, st = head["dt"], head["st"]
+    dt_all, rays_all = head["dt_all"], head["rays_all"]
+    slots, W, H, tile = head["layout"]["slots"], head["layout"]["frame"][0], head["layout"]["frame"][1], head["layout"]["tile"]
 
     # steady state (outside `value`): iterations with every pixel's paths in flight
     steady = None
@@ -498,39 +546,37 @@ def main():
         t1 = time.perf_counter()
         ss = pt.iterate(60)
         steady = [time.perf_counter() - t1, float(ss.rays), float(ss.ms_extend), float(ss.ms_shade)]
-    if dist:
-        dev = "cuda" if backend == "nccl" else "cpu"
-        v = torch.tensor([dt, float(st.rays)], dtype=torch.float64, device=dev)
-        mx = v.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        dt_all, rays_all = float(mx[0]), float(v[1])
-        if steady:
-            f = torch.tensor(steady, dtype=torch.float64, device=dev)
+        if dist:
+            f = torch.tensor(steady, dtype=torch.float64, device=dev_of(backend))
             fmax = f.clone()
             dist.all_reduce(fmax, op=dist.ReduceOp.MAX)
             dist.all_reduce(f, op=dist.ReduceOp.SUM)
             steady = [float(fmax[0]), float(f[1]), float(steady[2]), float(steady[3])]
-    else:
-        dt_all, rays_all = dt, float(st.rays)
 
     # traversal work counters (node steps, triangle tests, hits) from one more, untimed frame with
-    # the counting k_trace build (mcpt_set_work_counters): they feed the roofline's per-ray figures
+    # the counting k_trace build (mcpt_set_work_counters): they feed the roofline's per-ray figures.
+    # --no-work-counters skips it (rocprofv3 passes: every launch then belongs to a timed or warmup frame)
     work = None
-    if rank == 0:
+    if rank == 0 and not args.no_work_counters:
         pt.set_work_counters(True)
         pt.clear()
         work = Acc()
         work.add(pt.render())
         work.occ = pt.occ_stats()[0]
         pt.set_work_counters(False)
-    # N > 1: every rank's own time and rays of the timed frames (the value's max-over-ranks above)
-    per_rank = None
-    if dist:
-        per_rank = rank_times(dist, dev_of(backend), dt, st.rays, world, torch)
-    strong = None
-    if dist and not args.no_strong and args.scaling == "weak":
-        strong = run_strong(pt, rc, rank, world, dist, backend, spp, args, torch)
+    per_rank = head["per_rank"]
+    gather = None
+    if dist and args.scaling == "strong" and not args.no_gather:
+        gather = gather_and_verify(pt, rc, rank, world, dist, spp, args, torch)
+    other = None
+    other_kind = "weak" if args.scaling == "strong" else "strong"
+    skip_other = args.no_weak if other_kind == "weak" else args.no_strong
+    if dist and not skip_other:
+        orun = run_split(pt, rc, rank, world, dist, backend, other_kind, spp, args, torch)
+        orun["spp"] = spp
+        other = split_summary(orun, args, world)
+        if other_kind == "strong" and not args.no_gather:
+            other.update(gather_and_verify(pt, rc, rank, world, dist, spp, args, torch))
 
     if rank != 0:
         if dist:
@@ -571,6 +617,12 @@ def main():
             "frame": [W, H],
             "spp": spp,
             "tiles": f"{tile}x{tile}, rank = (tx+ty) mod N",
+            "split": ("one GPU: the config's frame" if world == 1 else
+                      f"{args.scaling}: " + ("the config's own frame split over the ranks (the metric's frame)"
+                                             if args.scaling == "strong" else
+                                             f"a {W}x{H} frame (1080p per rank, N-fold vertical supersampling)")),
+            "path_state": ("full frame" if world == 1 else
+                           f"compact: the rank's tiles only, {head['layout']['path_pixels_rank']} pixels x {slots} slots"),
             "step": "one whole frame: film cleared, every pixel the rank owns rendered to spp "
                     "(all wavefront iterations: shade + extend + shadow)",
             "rays_per_step": int(rays_all / K),
@@ -606,8 +658,10 @@ def main():
                                        "(rank 0's kernel times; rays and time over all ranks)"}
     if per_rank:
         out["per_rank"] = per_rank
-    if strong:
-        out["strong"] = strong
+    if gather:
+        out["gather"] = gather
+    if other:
+        out[other_kind] = other
     print(json.dumps(out), flush=True)
     pt.close()
     if dist:

@@ -216,6 +216,17 @@ int mcpt_set_trace_partitions(mcpt_ctx *ctx, uint32_t nparts);
  * per-lane registers, which the 64-VGPR 8-wave traversal cannot afford without spilling. */
 int mcpt_set_work_counters(mcpt_ctx *ctx, int32_t on);
 int mcpt_set_tiles(mcpt_ctx *ctx, const uint32_t *tile_xy, uint32_t ntiles); /* batch tile set; NULL = all */
+/* Path-state layout (default 0, full: one path per pixel of the whole W x H film per slot, path id =
+ * pixel id as in the reference, wavefront_kernels.cu:108,114; Film.cu:254-275 sizes the pool at
+ * W x H).  on = 1, compact: the path state covers only the tile set, slots x (tiles x tile pixels)
+ * paths -- a rank of a multi-GPU split that owns 1/N of the tiles holds 1/N of the state and clears
+ * 1/N of it.  Results do not change (every sample is keyed by its pixel).  In the compact layout
+ * mcpt_set_tiles re-allocates the path state and CLEARS the film (a tile listed twice is rejected),
+ * mcpt_set_path_slots keeps the tile set, mcpt_film_resize resets it to every tile, and
+ * mcpt_wavefront_step accepts only tiles of the set.  The film readers still return the W x H frame:
+ * the tile set's pixels, pixels scattered in by mcpt_film_unpack_tiles / mcpt_gather, zero elsewhere.
+ * A change re-allocates and clears the film. */
+int mcpt_set_compact_paths(mcpt_ctx *ctx, int32_t on);
 int mcpt_wavefront_step(mcpt_ctx *ctx, uint32_t tile_x, uint32_t tile_y, mcpt_stage_stats *st); /* one iteration, one tile */
 int mcpt_iterate(mcpt_ctx *ctx, uint32_t iterations, mcpt_stage_stats *st);  /* batch iterations over the tile set */
 int mcpt_render(mcpt_ctx *ctx, mcpt_stage_stats *st);                       /* iterate until every pixel has spp */
@@ -248,6 +259,10 @@ int mcpt_device_name(mcpt_ctx *ctx, char *buf, int32_t len);
  * device time of the last mcpt_stage_run kernel. */
 int mcpt_debug_queue_rays(mcpt_ctx *ctx, int which, float *ray_o, float *ray_d, uint32_t *n_inout);
 float mcpt_debug_last_stage_ms(const mcpt_ctx *ctx);
+/* Tests: on = 1 runs the traversal with a 2-entry LDS stack per lane (deeper entries in scratch)
+ * instead of the 8 / 10 entries the tree depth selects, so that the scratch path is exercised on
+ * every tree.  Same results, slower. */
+int mcpt_debug_tiny_lds_stack(mcpt_ctx *ctx, int32_t on);
 float mcpt_debug_last_build_ms(const mcpt_ctx *ctx);  /* device time of the last GPU BVH build */
 /* HRDI tables: an upload whose desc has env_tex but no env_marginal_y / env_conds_y / env_pdf builds
  * them on the device (build_environment_light, light_initialization_kernels.cu:3-161; bit-identical to

@@ -41,6 +41,7 @@
 #define MCPT_HPP
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -160,7 +161,9 @@ public:
         name = "Environment Light";
         color = c;
     }
-    explicit EnvironmentLight(const std::string& path) : type_(HRDI), path_(path) { name = "Environment Light"; }
+    explicit EnvironmentLight(const std::string& path) : tex_rev_(next_texture_revision()), type_(HRDI), path_(path) {
+        name = "Environment Light";
+    }
     void set_type(const EnvironmentLightType t) {
         if (t == Atmosphere) throw Error(MCPT_E_INVALID, "EnvironmentLight: Atmosphere is a raster-only type");
         type_ = t;
@@ -168,7 +171,7 @@ public:
     }
     void set_texture_filepath(const std::string& path) {
         path_ = path;
-        ++tex_rev_;  // re-read even for the same path: the file may have changed on disk
+        tex_rev_ = next_texture_revision();  // re-read even for the same path: the file may have changed on disk
         notify();
     }
     std::string get_texture_filepath() const { return path_; }
@@ -178,15 +181,21 @@ public:
     // instead of on the host; bit-identical tables, for large maps.
     void set_device_tables(bool on) {
         device_tables_ = on;
-        ++tex_rev_;
+        tex_rev_ = next_texture_revision();
         notify();
     }
     bool get_device_tables() const { return device_tables_; }
-    // Bumped by the edits that change the texture or its tables (path, table source) and not by
-    // set_ls / set_color / set_type, which Scene::desc applies without re-reading the .hdr.
+    // A new value with every edit that changes the texture or its tables (path, table source) and
+    // not with set_ls / set_color / set_type, which Scene::desc applies without re-reading the .hdr.
+    // Values are drawn from one process-wide counter: a copy of a light keeps its id (Light's id is
+    // copied with it), so per-object counts could make two re-pointed copies look alike.
     uint64_t texture_revision() const { return tex_rev_; }
 
 private:
+    static uint64_t next_texture_revision() {
+        static std::atomic<uint64_t> n{0};
+        return ++n;
+    }
     uint64_t tex_rev_ = 0;
     EnvironmentLightType type_ = Color;
     std::string path_;
@@ -274,7 +283,8 @@ public:
         // set_color, set_type) only change the fields desc() fills in below.  The env arrays
         // live beside the BVH in the builder, so an env reload never rebuilds the geometry
         // (built_ stays tied to geometry and BVH-parameter edits).
-        const std::pair<int, uint64_t> env_key{env.get_id(), env.texture_revision()};  // ids are never reused
+        // (revisions are process-wide unique per texture edit, so copies of one light differ too)
+        const std::pair<int, uint64_t> env_key{env.get_id(), env.texture_revision()};
         if (!proxy_env_ && env.get_light_type() == HRDI && (!env_loaded_ || env_key != env_built_)) {
             if (env.get_texture_filepath().empty()) throw Error(MCPT_E_INVALID, "EnvironmentLight: HRDI without a texture");
             detail::check(mcpt_scene_set_env_hdr_ex(s_, env.get_texture_filepath().c_str(), 1,

@@ -341,25 +341,23 @@ struct MatOut {
     float rrz;       // nee1.w
 };
 
-// Light choice + wf_mat_mix for the continuing path pid (vertex len, sample index
-// `sidx`, throughput `beta_store` after the logic update).
+// Light choice + wf_mat_mix for the continuing path pid of pixel `pix` (vertex len, sample
+// index `sidx`, throughput `beta_store` after the logic update).
 //
 // FIXED (quality mode, mcpt_config.flags & MCPT_FLAG_FIXED) changes, each
 // a reference quirk of Appendix A: light-selection pdf 1/N folded into both light pdfs
 // (A.6), delta lights get MIS weight 1 (pdf_brdf.y = 0 instead of 1, A.7), textbook
 // Gram-Schmidt (A.9), env sampling/pdf on matched, clamped cells (A.11).
 template <bool FIXED>
-__device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t sidx, uint32_t len, V3 beta_store,
-                                 int32_t htri, float4* stage, bool occ_on) {
+__device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix, uint32_t sidx, uint32_t len,
+                                 V3 beta_store, int32_t htri, float4* stage, bool occ_on) {
     const DevScene& sc = a.scene;
     const uint2 none = make_uint2(kOccEmpty, kOccEmpty);
     MatOut mo{};
     mo.el = mo.eb = none;
-    // path slot -> pixel; the sample index comes with the record (k_shade: slot k of a pixel
-    // runs samples k, k + S, k + 2S, ...)
-    const uint32_t npix = (uint32_t)a.W * (uint32_t)a.H;
-    const uint32_t slot = a.slots > 1 ? pid / npix : 0u;
-    const Rng r{rng_key(a.seed, pid - slot * npix, sidx), len};
+    // the pixel and the sample index come with the record (k_shade: slot k of a pixel runs
+    // samples k, k + S, k + 2S, ...)
+    const Rng r{rng_key(a.seed, pix, sidx), len};
     const V3 ro = xyz(a.p.ray_o[pid]), rdir = xyz(a.p.ray_d[pid]);
     V3 pos, n;
     int mat;
@@ -537,7 +535,10 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         y = t.y * a.tile_h + li / a.tile_w;
         valid = x < a.W - 1 && y < a.H - 1;  // last column and row never rendered (wavefront_kernels.cu:110)
         pix = (uint32_t)y * (uint32_t)a.W + (uint32_t)x;
-        pid = (uint32_t)slot * ((uint32_t)a.W * (uint32_t)a.H) + pix;
+        // path index (ShadeArgs::npx): the pixel id, or its place in the compact tile-set layout
+        const uint32_t local = a.compact ? (uint32_t)(a.tile_base ? a.tile_base[tile] : tile) * (uint32_t)tile_px + (uint32_t)li
+                                         : pix;
+        pid = (uint32_t)slot * a.npx + local;
     }
     // ---- phase 1: logic + generate (one thread per pixel)
     bool gen_ext = false, gen_trivial = false, cont = false;
@@ -672,7 +673,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         if (gen_ext) a.ext_q[shard * a.ext_cap + slot[0]] = pid;
         if (cont) {
             const uint32_t qi = shard * a.ext_cap + slot[1];
-            a.mat_rec[qi] = make_uint4(pid, cont_len, cont_sidx, (uint32_t)cont_htri);
+            a.mat_rec[qi] = make_uint4(pid, pix, cont_sidx | (cont_len << kRecLenShift), (uint32_t)cont_htri);
             a.mat_beta[qi] = f4(beta_store, 0.f);
         }
     }
@@ -697,8 +698,28 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
 // pushes meet at the barrier together.  Block b serves shard b mod kShards, chunks
 // b / kShards, + gridDim.x / kShards, ... of it (grid from the occupancy calculator).
 // ---------------------------------------------------------------------------
+// The kernel's by-value argument struct read through an opaque copy of the kernarg segment
+// pointer.  Kernel arguments are invariant loads, so the compiler hoists every field a persistent
+// loop uses into SGPRs at kernel entry; ShadeArgs' ~60 uniform words then exceed the SGPR file and
+// spill into VGPR lanes (k_material: 78 SGPRs, 76 v_writelane / 281 v_readlane).  Behind the empty
+// asm the pointer is a new value wherever this is called, so the fields are loaded (s_load from the
+// scalar cache) where they are used.  The struct stays in the constant address space: the cast to
+// a generic reference is undone by address-space inference after inlining (scalar loads, no flat).
+// k_material: 128 -> 112 VGPRs, no SGPR spill, shade stage 142.9 -> 141.1 ms per config-2 frame
+// (interleaved A/B, two rounds).  The same re-read per k_trace loop trip removed its 12 SGPR spills
+// but cost 2.52 -> 2.59 ms per launch (scalar-load latency on every trip): not used there.
+template <class T>
+__device__ inline const T& kernarg_fresh() {
+    typedef const __attribute__((address_space(4))) T KT;
+    KT* p = (KT*)__builtin_amdgcn_kernarg_segment_ptr();
+    __asm__ volatile("" : "+s"(p));
+    return *(const T*)p;
+}
+
 template <bool FIXED>
-__global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) {
+__global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a_kernarg) {
+    (void)a_kernarg;  // read through kernarg_fresh (the same bytes: it is the kernel's only argument)
+    const ShadeArgs& a = kernarg_fresh<ShadeArgs>();
     if (a.cnt->idle) return;  // the tile set is complete
     const uint32_t shard = blockIdx.x % kShards, w_in = blockIdx.x / kShards, bps = gridDim.x / kShards;
     uint32_t* sc_ctr = a.cnt->shard[shard];
@@ -712,15 +733,17 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a) 
     // wrote and read 32-B pieces of partly used lines).
     __shared__ float4 s_any[4][kBlock];
     for (uint32_t base = w_in * kBlock; base < n; base += bps * kBlock) {  // block-uniform trip count
+        const ShadeArgs& a = kernarg_fresh<ShadeArgs>();  // this trip's loads (see kernarg_fresh)
         const uint32_t i = base + threadIdx.x;
         MatOut mo{};
         uint32_t mpid = 0;
         bool occ_l = false, occ_b = false, try_l = false, try_b = false;  // resolved by / tested against the occluder cache
         if (i < n) {
-            const uint4 q = a.mat_rec[shard * a.ext_cap + i];  // {pid, len, sample index, hit_tri}
+            const uint4 q = a.mat_rec[shard * a.ext_cap + i];  // {pid, pixel, sample index | len << 24, hit_tri}
             const float4 b4 = a.mat_beta[shard * a.ext_cap + i];
             mpid = q.x;
-            mo = material<FIXED>(a, mpid, q.z, q.y, xyz(b4), (int32_t)q.w, &s_any[0][0], occ_on);
+            mo = material<FIXED>(a, mpid, q.y, q.z & ((1u << kRecLenShift) - 1u), q.z >> kRecLenShift, xyz(b4),
+                                 (int32_t)q.w, &s_any[0][0], occ_on);
             // the occluder cache (see occ_hit1), before the BRDF sample's light terms: a ray it
             // resolves gets its wf_shadow result here and is not queued
             if (occ_on) {
@@ -1370,6 +1393,14 @@ __global__ void k_clear(ClearArgs a) {  // g_clear_dfilm (wavefront_kernels.cu:5
 __global__ void k_resolve(ResolveArgs a) {  // film = sum of the path slots' accumulators, in slot order
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
+    uint32_t o = i;  // the pixel
+    if (a.tiles) {   // compact layout: accumulator i is pixel li of tile-set tile ti
+        const uint32_t tpx = (uint32_t)(a.tile_w * a.tile_h), ti = i / tpx, li = i - ti * tpx;
+        const int2 t = a.tiles[ti];
+        const uint32_t x = (uint32_t)t.x * a.tile_w + li % (uint32_t)a.tile_w, y = (uint32_t)t.y * a.tile_h + li / (uint32_t)a.tile_w;
+        if (x >= (uint32_t)a.W || y >= (uint32_t)a.H) return;
+        o = y * (uint32_t)a.W + x;
+    }
     float4 L = a.Ld[i];
     uint32_t n = a.samples[i];
     for (int k = 1; k < a.slots; k++) {
@@ -1377,8 +1408,8 @@ __global__ void k_resolve(ResolveArgs a) {  // film = sum of the path slots' acc
         L = make_float4(L.x + l.x, L.y + l.y, L.z + l.z, 0.f);
         n += a.samples[(size_t)k * a.n + i];
     }
-    a.out_Ld[i] = L;
-    a.out_samples[i] = n;
+    a.out_Ld[o] = L;
+    a.out_samples[o] = n;
 }
 
 __global__ void k_tonemap(TonemapArgs a) {  // draw_to_surface (wavefront_kernels.cu:6-40)
@@ -1597,6 +1628,13 @@ void launch_trace(const TraceArgs& args, const LaunchGeom& g, hipStream_t s) {
     a.refill_min = g.refill_min ? g.refill_min : kRefill[w][k];
     const uint32_t wps = std::max<uint32_t>(1, g.trace_waves[w][k] / nsh);
     const dim3 grid(wps * nsh), block(kTraceBlock);
+    // Test instantiation with a 2-entry LDS stack (mcpt_debug_tiny_lds_stack): every push past the
+    // second takes the scratch entries, so parity tests cover that path on every tree.
+    if (a.tiny_stack) {
+        if (w == 0) hipLaunchKernelGGL((k_trace<2, kLdsStackTiny, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_trace<4, kLdsStackTiny, false>), grid, block, 0, s, a);
+        return;
+    }
     // The counting instantiation (work counters, mcpt_set_work_counters) runs on the same grid;
     // a persistent wave that finds its partitions drained simply exits.
     if (a.set[0].stats || a.set[1].stats) {

@@ -38,6 +38,7 @@ constexpr int kLdsStack = MCPT_LDS_STACK;  // traversal stack entries per lane k
 #define MCPT_LDS_STACK_DEEP 10
 #endif
 constexpr int kLdsStackDeep = MCPT_LDS_STACK_DEEP;  // the same for trees deeper than kDeepTree levels
+constexpr int kLdsStackTiny = 2;  // test instantiation (mcpt_debug_tiny_lds_stack): pushes beyond 2 go to scratch
 #ifndef MCPT_DEEP_TREE
 #define MCPT_DEEP_TREE 20
 #endif
@@ -54,6 +55,8 @@ enum : uint32_t {
     F_SIDX_SHIFT = 13       // bits 13..31: the sample index the path renders (RNG key)
 };
 constexpr uint32_t kMaxSpp = 1u << (32 - F_SIDX_SHIFT);  // sample indices must fit the flags word
+constexpr int kRecLenShift = 24;  // material record word 2: sample index (< kMaxSpp) | len << 24 (len < 256)
+static_assert(kMaxSpp <= (1u << kRecLenShift), "sample index and len share a record word");
 
 // k_shade blocks: kBlock consecutive pixels of one path slot; slot k's blocks follow slot k-1's
 __host__ __device__ constexpr int shade_blocks_per_tile(int tile_px, int slots) {
@@ -151,11 +154,21 @@ struct ShadeArgs {
     int ntiles, tile_w, tile_h, W, H;
     int spp, max_depth, rr_depth;
     int slots;  // path slots per pixel (paths in flight per pixel; slot k runs samples k, k + slots, ...)
+    // Path index of a pixel: slot * npx + its index within the slot.  Full layout (compact 0): npx =
+    // W * H and the index is the pixel id (the reference's path_id = pixel_id, wavefront_kernels.cu:
+    // 108,114).  Compact layout (mcpt_set_compact_paths): the path state covers only the context's tile
+    // set, npx = tile-set tiles * tile pixels and the index is set_tile * tile_w * tile_h + the pixel's
+    // index in its tile, where set_tile = tile_base[t] for launch tile t (nullptr: t itself, the launch
+    // runs the whole set in its order).
+    uint32_t npx;
+    int compact;
+    const int* tile_base;
     uint64_t seed;
     uint32_t *ext_q, *any_q;
     // material queue (continuing paths, k_shade -> k_material, ext_cap per shard): dense records
-    // {pid, len, sample index, hit_tri} + the updated throughput, so k_material reads its per-path
-    // inputs from k_shade's coalesced loads instead of gathering them again at pid
+    // {pid, pixel, sample index | len << kRecLenShift, hit_tri} + the updated throughput, so
+    // k_material reads its per-path inputs from k_shade's coalesced loads instead of gathering them
+    // again at pid (the pixel keys its RNG draws: the path index need not be the pixel id)
     uint4* mat_rec;
     float4* mat_beta;
     uint32_t ext_cap, any_cap;  // per-shard queue capacity
@@ -192,11 +205,18 @@ struct TraceArgs {
     uint32_t ndies;             // XCDs of the device (set by launch_trace)
     uint32_t* grab;             // nparts chunk counters, C_WORDS apart, zero at launch (k_accumulate resets)
     const uint32_t* idle;       // optional: nonzero = the tile set is complete, exit at once (CounterBlock::idle)
+    int tiny_stack;             // host side: launch the kLdsStackTiny instantiation (mcpt_debug_tiny_lds_stack)
 };
 
 struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; int32_t* scene_tri; uint32_t n; };
 struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n; };
-struct ResolveArgs { const float4* Ld; const uint32_t* samples; float4* out_Ld; uint32_t* out_samples; uint32_t n; int slots; };
+// n accumulators per slot.  tiles == nullptr: n = W * H pixels in pixel order (full layout); else the
+// compact layout's order (tile-set tile i's pixels at i * tile_w * tile_h, row by row), scattered to
+// out[y * W + x] for the pixels inside the W x H film
+struct ResolveArgs {
+    const float4* Ld; const uint32_t* samples; float4* out_Ld; uint32_t* out_samples; uint32_t n; int slots;
+    const int2* tiles; int tile_w, tile_h, W, H;
+};
 struct TonemapArgs { const float4* Ld; const uint32_t* samples; uchar4* out; float exposure; uint32_t n; };
 struct PackArgs { const float4* Ld; const uint32_t* samples; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* out; };
 struct UnpackArgs { const float4* in; const int2* tiles; int ntiles, tile_w, tile_h, W, H; float4* Ld; uint32_t* samples; };

@@ -58,8 +58,12 @@ struct mcpt_ctx {
     // film + paths
     uint32_t W = 0, H = 0, tile_w = 256, tile_h = 256;
     size_t P = 0;      // pixels (W * H)
-    uint32_t slots = 1;  // path slots per pixel (mcpt_set_path_slots); path state holds slots * P paths
-    float4* film_Ld = nullptr;     // slots > 1: resolved film (sum of the slot accumulators)
+    uint32_t slots = 1;  // path slots per pixel (mcpt_set_path_slots); path state holds slots * npx paths
+    // Path layout (mcpt_set_compact_paths).  Full: npx = P, path index = slot * P + pixel id.  Compact:
+    // the path state covers the tile set only, npx = tile-set tiles x tile pixels (ShadeArgs::npx).
+    bool compact = false;
+    size_t npx = 0;
+    float4* film_Ld = nullptr;     // slots > 1 or compact: the film, W x H (sum of the slot accumulators)
     uint32_t* film_samples = nullptr;
     std::vector<void*> film_bufs;
     uint8_t* blk_done = nullptr;  // k_shade block done flags (ShadeArgs::blk_done), in film_bufs
@@ -74,8 +78,8 @@ struct mcpt_ctx {
     CounterBlock* cnt_host = nullptr;  // pinned
     CounterBlock totals{};             // host copy of the counters after the last call (valid: totals_ok)
     bool totals_ok = false;
-    int2* step_tile = nullptr;         // mcpt_wavefront_step's one-tile set: device + pinned staging
-    int2* step_tile_h = nullptr;
+    int2* step_tile = nullptr;         // mcpt_wavefront_step's one-tile set: device + pinned staging (16 B:
+    int2* step_tile_h = nullptr;       // the tile, then its index in the tile set, ShadeArgs::tile_base)
     int2* tiles = nullptr;
     std::vector<int2> tiles_h;
     uint32_t tiles_cap = 0;
@@ -88,6 +92,7 @@ struct mcpt_ctx {
     bool env_device_built = false;  // the uploaded scene's HRDI tables were built on the device
     bool env_guides = false;        // env_cell uses the search guides
     int gpu_bvh_builder = MCPT_GPU_BVH_PLOC;  // mcpt_set_gpu_bvh_builder
+    bool tiny_stack = false;  // mcpt_debug_tiny_lds_stack: k_trace with a 2-entry LDS stack (tests)
 };
 
 static int set_err(mcpt_ctx* c, int rc, const std::string& msg) {
@@ -839,9 +844,13 @@ static std::vector<int2> all_tiles(const mcpt_ctx* c) {
 int mcpt_film_clear(mcpt_ctx* c) {
     if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
     HIPCHK(c, hipSetDevice(c->device));
-    ClearArgs a{c->p.flags, c->p.samples, c->p.Ld, (uint32_t)(c->P * c->slots)};
+    ClearArgs a{c->p.flags, c->p.samples, c->p.Ld, (uint32_t)(c->npx * c->slots)};
     launch_clear(a, c->stream);
     HIPCHK(c, hipGetLastError());
+    if (c->compact) {  // the W x H film also holds pixels unpacked from other contexts (mcpt_film_unpack_tiles)
+        HIPCHK(c, hipMemsetAsync(c->film_Ld, 0, c->P * sizeof(float4), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->film_samples, 0, c->P * sizeof(uint32_t), c->stream));
+    }
     if (c->blk_done) HIPCHK(c, hipMemsetAsync(c->blk_done, 0, c->blk_done_n, c->stream));
     // The occluder cache starts empty with every film (and its lookup gate on), so a frame's work
     // never depends on the frames before it.  (It only ever chose which triangle an any-hit ray
@@ -858,18 +867,27 @@ int mcpt_film_clear(mcpt_ctx* c) {
     return MCPT_OK;
 }
 
-int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t th) {
-    if (!c || w == 0 || h == 0 || tw == 0 || th == 0) return set_err(c, MCPT_E_INVALID, "bad film size");
-    if ((uint64_t)w * h >= (1ull << 31)) return set_err(c, MCPT_E_INVALID, "film too large");
-    if ((uint64_t)tw * th > (1ull << 26)) return set_err(c, MCPT_E_INVALID, "tile too large");
-    HIPCHK(c, hipSetDevice(c->device));
+// Film state for the current film size, path slots, layout and tile set: the path streams (slots x
+// npx paths), the k_shade block flags and the W x H film of the slot sums (slots > 1 or compact).
+// Frees the previous film state first; the caller clears the film.
+static int alloc_film_state(mcpt_ctx* c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     free_list(c->film_bufs);
-    c->P = 0;
+    {
+        DevPaths keep{};  // the queue-owned any-hit ray buffers stay
+        keep.sray_o = c->p.sray_o;
+        keep.sray_d = c->p.sray_d;
+        c->p = keep;
+    }
+    c->film_Ld = nullptr;
+    c->film_samples = nullptr;
     c->blk_done = nullptr;
     c->blk_done_n = 0;
-    c->W = w; c->H = h; c->tile_w = tw; c->tile_h = th;
-    const size_t npix = (size_t)w * h, P = npix * c->slots;  // P: paths
+    const uint32_t w = c->W, h = c->H, tw = c->tile_w, th = c->tile_h;
+    const size_t npix = (size_t)w * h;
+    const size_t npx = c->compact ? c->tiles_h.size() * (size_t)tw * th : npix;
+    const size_t P = npx * c->slots;  // P: paths
+    c->npx = 0;
     if (P >= (1ull << 31)) return set_err(c, MCPT_E_INVALID, "film too large for the path slots");
     DevPaths p{};
     int rc;
@@ -880,16 +898,36 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
         (rc = dalloc(c, c->film_bufs, &p.flags, P)) || (rc = dalloc(c, c->film_bufs, &p.samples, P)) ||
         (rc = dalloc(c, c->film_bufs, &p.vis, 2 * P)))
         return rc;
-    c->film_Ld = nullptr;
-    c->film_samples = nullptr;
     {  // k_shade block done flags: slots x film tiles x blocks per tile
         const size_t ntiles = (size_t)((w + tw - 1) / tw) * ((h + th - 1) / th);
         c->blk_done_n = c->slots * ntiles * (size_t)shade_blocks_per_tile((int)(tw * th), 1);
         if ((rc = dalloc(c, c->film_bufs, &c->blk_done, c->blk_done_n))) return rc;
     }
-    if (c->slots > 1 && ((rc = dalloc(c, c->film_bufs, &c->film_Ld, npix)) ||
-                         (rc = dalloc(c, c->film_bufs, &c->film_samples, npix))))
+    if ((c->slots > 1 || c->compact) && ((rc = dalloc(c, c->film_bufs, &c->film_Ld, npix)) ||
+                                         (rc = dalloc(c, c->film_bufs, &c->film_samples, npix))))
         return rc;
+    HIPCHK(c, hipMemset(p.hit_tri, 0xff, P * sizeof(int32_t)));
+    HIPCHK(c, hipMemset(p.vis, 0, 2 * P));
+    p.sray_o = c->p.sray_o;  // the any-hit rays live with the queues (set_tiles_internal)
+    p.sray_d = c->p.sray_d;
+    c->p = p;
+    c->npx = npx;
+    return MCPT_OK;
+}
+
+int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t th) {
+    if (!c || w == 0 || h == 0 || tw == 0 || th == 0) return set_err(c, MCPT_E_INVALID, "bad film size");
+    if ((uint64_t)w * h >= (1ull << 31)) return set_err(c, MCPT_E_INVALID, "film too large");
+    if ((uint64_t)tw * th > (1ull << 26)) return set_err(c, MCPT_E_INVALID, "tile too large");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    free_list(c->film_bufs);
+    c->P = 0;
+    c->npx = 0;
+    c->p = DevPaths{};  // (set_tiles_internal below re-points the any-hit ray buffers)
+    c->blk_done = nullptr;
+    c->blk_done_n = 0;
+    c->W = w; c->H = h; c->tile_w = tw; c->tile_h = th;
     for (uint32_t** q : {&c->ext_q, &c->any_q, &c->mat_q}) {  // re-sized for the new tile set below
         if (*q) (void)hipFree(*q);
         *q = nullptr;
@@ -897,26 +935,64 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
     if (c->any_ray) (void)hipFree(c->any_ray);
     c->any_ray = nullptr;
     c->queue_alloc = 0;
-    HIPCHK(c, hipMemset(p.hit_tri, 0xff, P * sizeof(int32_t)));
-    HIPCHK(c, hipMemset(p.vis, 0, 2 * P));
-    c->p = p;
-    c->P = npix;
-    int rc2 = set_tiles_internal(c, all_tiles(c));
-    if (rc2) return rc2;
+    int rc = set_tiles_internal(c, all_tiles(c));
+    if (rc) return rc;
+    if ((rc = alloc_film_state(c))) return rc;
+    c->P = (size_t)w * h;
+    return mcpt_film_clear(c);
+}
+
+// A new tile set.  In the compact layout the path state follows the tile set: it is re-allocated and
+// the film cleared (a tile listed twice would share its paths: rejected).
+static int set_tiles_checked(mcpt_ctx* c, const std::vector<int2>& t) {
+    if (!c->compact) return set_tiles_internal(c, t);
+    for (size_t i = 0; i < t.size(); i++)
+        for (size_t j = 0; j < i; j++)
+            if (t[i].x == t[j].x && t[i].y == t[j].y)
+                return set_err(c, MCPT_E_INVALID, "compact paths: a tile is listed twice");
+    int rc = set_tiles_internal(c, t);
+    if (rc) return rc;
+    const size_t P = c->P;
+    c->P = 0;  // the film is not allocated until the new path state is
+    if ((rc = alloc_film_state(c))) return rc;
+    c->P = P;
     return mcpt_film_clear(c);
 }
 
 int mcpt_set_tiles(mcpt_ctx* c, const uint32_t* xy, uint32_t n) {
     if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
     HIPCHK(c, hipSetDevice(c->device));
-    if (!xy) return set_tiles_internal(c, all_tiles(c));
+    if (!xy) return set_tiles_checked(c, all_tiles(c));
     std::vector<int2> t;
     uint32_t nx = (c->W + c->tile_w - 1) / c->tile_w, ny = (c->H + c->tile_h - 1) / c->tile_h;
     for (uint32_t i = 0; i < n; i++) {
         if (xy[2 * i] >= nx || xy[2 * i + 1] >= ny) return set_err(c, MCPT_E_INVALID, "tile out of range");
         t.push_back(make_int2((int)xy[2 * i], (int)xy[2 * i + 1]));
     }
-    return set_tiles_internal(c, t);
+    return set_tiles_checked(c, t);
+}
+
+int mcpt_set_compact_paths(mcpt_ctx* c, int32_t on) {
+    if (!c) return MCPT_E_INVALID;
+    const bool v = on != 0;
+    if (v == c->compact) return MCPT_OK;
+    c->compact = v;
+    if (!c->P) return MCPT_OK;  // takes effect with the film's allocation
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t P = c->P;
+    c->P = 0;
+    int rc = alloc_film_state(c);
+    if (rc) {  // e.g. out of memory: back to the previous layout
+        const std::string err = c->err;
+        c->compact = !v;
+        if (alloc_film_state(c) == MCPT_OK) {
+            c->P = P;
+            (void)mcpt_film_clear(c);
+        }
+        return set_err(c, rc, err);
+    }
+    c->P = P;
+    return mcpt_film_clear(c);
 }
 
 static hipEvent_t ev(mcpt_ctx* c, size_t i) {
@@ -939,7 +1015,7 @@ static int check_ready(mcpt_ctx* c) {
 }
 
 // One wavefront iteration over the current tile set: shade -> extend -> any-hit.
-static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2* tiles, int ntiles) {
+static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2* tiles, int ntiles, const int* tile_base) {
     ShadeArgs sa;
     sa.scene = c->scene;
     sa.cam = c->cam;
@@ -955,6 +1031,9 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     sa.rr_depth = c->cfg.rr_depth;
     sa.seed = c->cfg.seed;
     sa.slots = (int)c->slots;
+    sa.npx = (uint32_t)c->npx;
+    sa.compact = c->compact ? 1 : 0;
+    sa.tile_base = tile_base;
     sa.ext_q = c->ext_q;
     sa.any_q = c->any_q;
     sa.mat_rec = reinterpret_cast<uint4*>(c->mat_q);
@@ -993,6 +1072,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     ta.vis = c->p.vis;
     ta.grab = &c->cnt->grab[0][0];  // reset by k_accumulate below
     ta.idle = &c->cnt->idle;
+    ta.tiny_stack = c->tiny_stack ? 1 : 0;
     launch_trace(ta, c->geom, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
     launch_accumulate(c->cnt, c->geom.trace_parts, c->scene.occ ? c->scene.occ_gate : nullptr, c->stream);
@@ -1003,7 +1083,8 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
 // n iterations over a tile set (the context's, or one tile for mcpt_wavefront_step).  One
 // host synchronisation per call: the counter totals before the call are the host copy the
 // previous call (or the film clear) left.
-static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st, const int2* tiles = nullptr, int ntiles = -1) {
+static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st, const int2* tiles = nullptr, int ntiles = -1,
+                          const int* tile_base = nullptr) {
     int rc = check_ready(c);
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1025,7 +1106,7 @@ static int run_iterations(mcpt_ctx* c, uint32_t n, mcpt_stage_stats* st, const i
     for (uint32_t i = 0; i < n; i++) {
         // events for at most the first 4096 iterations of a call
         bool timing = i < 4096;
-        if ((rc = enqueue_iteration(c, (size_t)3 * i, timing, tiles, ntiles))) {
+        if ((rc = enqueue_iteration(c, (size_t)3 * i, timing, tiles, ntiles, tile_base))) {
             c->totals_ok = false;
             return rc;
         }
@@ -1072,6 +1153,14 @@ int mcpt_wavefront_step(mcpt_ctx* c, uint32_t tx, uint32_t ty, mcpt_stage_stats*
     if (rc) return rc;
     uint32_t nx = (c->W + c->tile_w - 1) / c->tile_w, ny = (c->H + c->tile_h - 1) / c->tile_h;
     if (tx >= nx || ty >= ny) return set_err(c, MCPT_E_INVALID, "tile out of range");
+    // compact layout: the tile's paths are those of its place in the tile set
+    int base = 0;
+    if (c->compact) {
+        base = -1;
+        for (size_t i = 0; i < c->tiles_h.size() && base < 0; i++)
+            if (c->tiles_h[i].x == (int)tx && c->tiles_h[i].y == (int)ty) base = (int)i;
+        if (base < 0) return set_err(c, MCPT_E_INVALID, "compact paths: the tile is not in the tile set");
+    }
     // The one-tile set goes through its own small buffer (pinned staging, stream-ordered
     // copy): the context's tile set and queues stay as they are when their per-shard queue
     // capacity covers one tile, which it does unless the tile set is empty.
@@ -1080,12 +1169,13 @@ int mcpt_wavefront_step(mcpt_ctx* c, uint32_t tx, uint32_t ty, mcpt_stage_stats*
     if (c->ext_cap >= need) {
         if (!c->step_tile) {
             HIPCHK(c, hipSetDevice(c->device));
-            HIPCHK(c, hipMalloc(&c->step_tile, sizeof(int2)));
-            HIPCHK(c, hipHostMalloc(&c->step_tile_h, sizeof(int2)));
+            HIPCHK(c, hipMalloc(&c->step_tile, 2 * sizeof(int2)));
+            HIPCHK(c, hipHostMalloc(&c->step_tile_h, 2 * sizeof(int2)));
         }
-        *c->step_tile_h = make_int2((int)tx, (int)ty);  // the previous call's copy has completed
-        HIPCHK(c, hipMemcpyAsync(c->step_tile, c->step_tile_h, sizeof(int2), hipMemcpyHostToDevice, c->stream));
-        return run_iterations(c, 1, st, c->step_tile, 1);
+        c->step_tile_h[0] = make_int2((int)tx, (int)ty);  // the previous call's copy has completed
+        c->step_tile_h[1] = make_int2(base, 0);
+        HIPCHK(c, hipMemcpyAsync(c->step_tile, c->step_tile_h, 2 * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+        return run_iterations(c, 1, st, c->step_tile, 1, reinterpret_cast<const int*>(c->step_tile + 1));
     }
     std::vector<int2> saved = c->tiles_h;
     if ((rc = set_tiles_internal(c, {make_int2((int)tx, (int)ty)}))) return rc;
@@ -1200,7 +1290,8 @@ static int stage_run_paths(mcpt_ctx* c, int stage, const mcpt_path_view* in, mcp
         rbeta.assign(qn, make_float4(0.f, 0.f, 0.f, 0.f));
         for (uint32_t i = 0; i < n; i++) {
             const uint32_t sh = i % kShards, k = i / kShards;
-            rec[(size_t)sh * ext_cap + k] = make_uint4(i, (fl[i] >> F_LEN_SHIFT) & 0xffu, fl[i] >> F_SIDX_SHIFT, (uint32_t)in->hit_tri[i]);
+            rec[(size_t)sh * ext_cap + k] = make_uint4(i, i, (fl[i] >> F_SIDX_SHIFT) | (((fl[i] >> F_LEN_SHIFT) & 0xffu) << kRecLenShift),
+                                                       (uint32_t)in->hit_tri[i]);
             rbeta[(size_t)sh * ext_cap + k] = make_float4(be[i].x, be[i].y, be[i].z, 0.f);
             hc->shard[sh][C_MAT]++;
         }
@@ -1238,6 +1329,7 @@ static int stage_run_paths(mcpt_ctx* c, int stage, const mcpt_path_view* in, mcp
     sa.rr_depth = c->cfg.rr_depth;
     sa.seed = c->cfg.seed;
     sa.slots = 1;
+    sa.npx = n;  // path i is pixel i of the W x H stage film
     sa.ext_q = ext_q;
     sa.any_q = any_q;
     sa.mat_rec = mrec;
@@ -1373,6 +1465,7 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
     }
     ta.grab = &c->cnt->grab[0][0];
     HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
+    ta.tiny_stack = c->tiny_stack ? 1 : 0;
     launch_trace(ta, c->geom, c->stream);
     HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
     uint32_t grab0 = 0;  // drain check: the one shard is partition 0's
@@ -1413,17 +1506,25 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
 // The film (dFilm.Ld / samples): the path state's accumulators with one slot per pixel,
 // else their per-pixel sum in slot order (k_resolve) -- enqueued on the context stream.
 static int film_view(mcpt_ctx* c, const float4** Ld, const uint32_t** samples) {
-    if (c->slots <= 1) {
+    if (c->slots <= 1 && !c->compact) {
         *Ld = c->p.Ld;
         *samples = c->p.samples;
         return MCPT_OK;
     }
-    ResolveArgs a{c->p.Ld, c->p.samples, c->film_Ld, c->film_samples, (uint32_t)c->P, (int)c->slots};
+    ResolveArgs a{c->p.Ld, c->p.samples, c->film_Ld, c->film_samples, (uint32_t)c->npx, (int)c->slots,
+                  c->compact ? c->tiles : nullptr, (int)c->tile_w, (int)c->tile_h, (int)c->W, (int)c->H};
     launch_resolve(a, c->stream);
     HIPCHK(c, hipGetLastError());
     *Ld = c->film_Ld;
     *samples = c->film_samples;
     return MCPT_OK;
+}
+
+// Where another context's tile pixels are scattered (mcpt_film_unpack_tiles, mcpt_gather): the
+// pixel-indexed accumulators the film view reads beside the context's own tiles
+static void unpack_target(mcpt_ctx* c, float4** Ld, uint32_t** samples) {
+    *Ld = c->compact ? c->film_Ld : c->p.Ld;
+    *samples = c->compact ? c->film_samples : c->p.samples;
 }
 
 int mcpt_set_path_slots(mcpt_ctx* c, uint32_t slots) {
@@ -1434,9 +1535,28 @@ int mcpt_set_path_slots(mcpt_ctx* c, uint32_t slots) {
         return MCPT_OK;
     }
     // check the new size before touching anything: a rejected count leaves the film as it was
-    if ((uint64_t)c->P * slots >= (1ull << 31)) return set_err(c, MCPT_E_INVALID, "film too large for the path slots");
+    if ((uint64_t)c->npx * slots >= (1ull << 31)) return set_err(c, MCPT_E_INVALID, "film too large for the path slots");
     const uint32_t old = c->slots;
     c->slots = slots;
+    if (c->compact) {  // the path state of the current tile set (its queues too: their capacity follows the slots)
+        HIPCHK(c, hipSetDevice(c->device));
+        const std::vector<int2> t = c->tiles_h;
+        const size_t P = c->P;
+        c->P = 0;
+        int rc = set_tiles_internal(c, t);
+        if (!rc) rc = alloc_film_state(c);
+        if (rc != MCPT_OK) {
+            const std::string err = c->err;
+            c->slots = old;
+            if (set_tiles_internal(c, t) == MCPT_OK && alloc_film_state(c) == MCPT_OK) {
+                c->P = P;
+                (void)mcpt_film_clear(c);
+            }
+            return set_err(c, rc, err);
+        }
+        c->P = P;
+        return mcpt_film_clear(c);
+    }
     int rc = mcpt_film_resize(c, c->W, c->H, c->tile_w, c->tile_h);  // clears the film
     if (rc != MCPT_OK) {  // e.g. out of memory: back to the old slot count and its (cleared) film
         const std::string err = c->err;
@@ -1525,8 +1645,12 @@ int mcpt_film_unpack_tiles(mcpt_ctx* c, const void* d_in, const uint32_t* xy, ui
     hipError_t e = hipMemcpyAsync(dt, t.data(), n * sizeof(int2), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) {
         // scattered into slot 0 of the path state (its other slots of a pixel the context never
-        // renders stay zero, so the film view's slot sum returns these values)
-        UnpackArgs ua{(const float4*)d_in, dt, (int)n, (int)c->tile_w, (int)c->tile_h, (int)c->W, (int)c->H, c->p.Ld, c->p.samples};
+        // renders stay zero, so the film view's slot sum returns these values); compact layout: into
+        // the W x H film, where the film view's resolve writes only the context's own tiles
+        float4* tL;
+        uint32_t* ts;
+        unpack_target(c, &tL, &ts);
+        UnpackArgs ua{(const float4*)d_in, dt, (int)n, (int)c->tile_w, (int)c->tile_h, (int)c->W, (int)c->H, tL, ts};
         launch_unpack(ua, c->stream);
         e = hipGetLastError();
     }
@@ -1590,7 +1714,10 @@ int mcpt_gather(mcpt_ctx* const* ctxs, int32_t n, int32_t root) {
         if (e == hipSuccess)
             e = hipMemcpyAsync(dt, c->tiles_h.data(), c->tiles_h.size() * sizeof(int2), hipMemcpyHostToDevice, R->stream);
         if (e == hipSuccess) {
-            UnpackArgs ua{dst, dt, (int)c->tiles_h.size(), (int)R->tile_w, (int)R->tile_h, (int)R->W, (int)R->H, R->p.Ld, R->p.samples};
+            float4* tL;
+            uint32_t* ts;
+            unpack_target(R, &tL, &ts);
+            UnpackArgs ua{dst, dt, (int)c->tiles_h.size(), (int)R->tile_w, (int)R->tile_h, (int)R->W, (int)R->H, tL, ts};
             launch_unpack(ua, R->stream);
             e = hipGetLastError();
         }
@@ -1651,7 +1778,7 @@ int mcpt_debug_queue_rays(mcpt_ctx* c, int which, float* ro, float* rd, uint32_t
     for (int sh = 0; sh < kShards; sh++)
         for (uint32_t k = 0; k < cb.last_ext_shard[sh] && q.size() < n; k++) q.push_back(all[(size_t)sh * c->ext_cap + k]);
     n = (uint32_t)q.size();
-    const size_t np = c->P * c->slots;
+    const size_t np = c->npx * c->slots;
     std::vector<float4> o(np), d(np);
     HIPCHK(c, hipMemcpy(o.data(), c->p.ray_o, np * sizeof(float4), hipMemcpyDeviceToHost));
     HIPCHK(c, hipMemcpy(d.data(), c->p.ray_d, np * sizeof(float4), hipMemcpyDeviceToHost));
@@ -1664,6 +1791,11 @@ int mcpt_debug_queue_rays(mcpt_ctx* c, int which, float* ro, float* rd, uint32_t
     return MCPT_OK;
 }
 float mcpt_debug_last_stage_ms(const mcpt_ctx* c) { return c ? c->last_stage_ms : -1.f; }
+int mcpt_debug_tiny_lds_stack(mcpt_ctx* c, int32_t on) {
+    if (!c) return MCPT_E_INVALID;
+    c->tiny_stack = on != 0;
+    return MCPT_OK;
+}
 
 int mcpt_debug_quot(mcpt_ctx* c, const float* a, const float* b, uint32_t n, float* out) {
     if (!c || (n && (!a || !b || !out))) return set_err(c, MCPT_E_INVALID, "null argument");

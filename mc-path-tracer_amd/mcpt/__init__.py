@@ -118,6 +118,8 @@ ABI = {
     "mcpt_film_resize": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "mcpt_film_clear": (C.c_int, [C.c_void_p]),
     "mcpt_set_tiles": (C.c_int, [C.c_void_p, _u, C.c_uint32]),
+    "mcpt_set_compact_paths": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mcpt_debug_tiny_lds_stack": (C.c_int, [C.c_void_p, C.c_int32]),
     "mcpt_set_path_slots": (C.c_int, [C.c_void_p, C.c_uint32]),
     "mcpt_set_trace_partitions": (C.c_int, [C.c_void_p, C.c_uint32]),
     "mcpt_gather": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_int32]),
@@ -469,6 +471,15 @@ class PathTracer:
     def set_trace_partitions(self, nparts=0):
         """k_trace work partitions (mcpt_set_trace_partitions); 0 = the device default, two per XCD."""
         self._ck(lib().mcpt_set_trace_partitions(self.h, nparts))
+
+    def set_compact_paths(self, on=True):
+        """Path state over the tile set only (mcpt_set_compact_paths); re-allocates and clears the film.
+        In this layout set_tiles re-allocates and clears too."""
+        self._ck(lib().mcpt_set_compact_paths(self.h, int(bool(on))))
+
+    def set_tiny_lds_stack(self, on=True):
+        """Tests: the traversal's 2-entry LDS stack instantiation (mcpt_debug_tiny_lds_stack)."""
+        self._ck(lib().mcpt_debug_tiny_lds_stack(self.h, int(bool(on))))
 
     def set_tiles(self, tiles=None):
         if tiles is None:

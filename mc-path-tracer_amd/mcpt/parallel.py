@@ -31,15 +31,22 @@ PATH_BYTES = 126
 SLOT_BUDGET_BYTES = 32 << 30
 
 
-def strong_slots(base_slots, world, W, H, spp, budget=SLOT_BUDGET_BYTES):
+def rank_path_pixels(world, W, H, tile):
+    """Pixels of path state the largest rank allocates in the compact layout (mcpt_set_compact_paths):
+    its tiles x tile pixels, the overhang of edge tiles included."""
+    return max(len(tiles_for_rank(r, world, W, H, tile)) for r in range(world)) * tile * tile
+
+
+def strong_slots(base_slots, world, W, H, spp, tile=64, budget=SLOT_BUDGET_BYTES):
     """Path slots for a frame split over `world` ranks: every rank keeps the paths in flight of the
     one-GPU run (base_slots x W x H) over its 1/world of the pixels, so slots scale with world --
-    bounded by spp (a slot renders >= 1 sample) and by the state budget (the film's path state is
-    allocated for the whole W x H frame on every rank).  One value for every rank: the slot count
-    sets the film's summation order, so the gathered frame then equals a one-rank frame rendered
-    with the same slots bit for bit."""
-    cap = max(1, budget // (PATH_BYTES * W * H))
-    return int(max(base_slots, min(base_slots * world, spp, cap, 256)))  # mcpt_set_path_slots: 1..256
+    bounded by spp (a slot renders >= 1 sample), by the ABI's 256, and by the per-GPU state budget
+    over the rank's own path state (compact layout: its tiles only) with fewer than 2^31 paths.  One
+    value for every rank: the slot count sets the film's summation order, so the gathered frame then
+    equals a one-rank frame rendered with the same slots bit for bit."""
+    px = rank_path_pixels(world, W, H, tile) if world > 1 else W * H
+    cap = max(1, min(budget // (PATH_BYTES * px), ((1 << 31) - 1) // px))
+    return int(max(1, min(max(base_slots, min(base_slots * world, spp, 256)), cap)))  # mcpt_set_path_slots: 1..256
 
 
 def pack(Ld: np.ndarray, samples: np.ndarray, tiles, W, H, tile=256) -> np.ndarray:

@@ -166,7 +166,19 @@ def render(arrays: dict, cam, W, H, spp, max_depth=5, rr_depth=3, seed=0x5EED202
     return Ld.reshape(H, W, 3), samples.reshape(H, W), dict(zip(keys, list(cnt)))
 
 
-def trace_closest(arrays, ro, rd, traversal=0):
+def _chunks(n, nthreads, fn):
+    """fn(i0, i1) over [0, n) in nthreads contiguous chunks on a thread pool (ctypes releases the GIL
+    during the C call; the ray functions keep no global state).  Results do not depend on nthreads."""
+    if nthreads <= 1 or n < 8192:
+        return [fn(0, n)]
+    from concurrent.futures import ThreadPoolExecutor
+
+    step = (n + nthreads - 1) // nthreads
+    with ThreadPoolExecutor(nthreads) as ex:
+        return list(ex.map(lambda i: fn(i, min(n, i + step)), range(0, n, step)))
+
+
+def trace_closest(arrays, ro, rd, traversal=0, nthreads=1):
     s = scene_struct(arrays)
     ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
     rd = np.ascontiguousarray(rd, np.float32).reshape(-1, 3)
@@ -174,17 +186,27 @@ def trace_closest(arrays, ro, rd, traversal=0):
     pos_t = np.zeros((n, 4), np.float32)
     nrm = np.zeros((n, 4), np.float32)
     tri = np.zeros(n, np.int32)
-    lib().or_trace_closest(C.byref(s), n, fptr(ro), fptr(rd), traversal, fptr(pos_t), fptr(nrm), tri.ctypes.data_as(_i))
+
+    def run(i0, i1):
+        lib().or_trace_closest(C.byref(s), i1 - i0, fptr(ro[i0:i1]), fptr(rd[i0:i1]), traversal, fptr(pos_t[i0:i1]),
+                               fptr(nrm[i0:i1]), tri[i0:i1].ctypes.data_as(_i))
+
+    _chunks(n, nthreads, run)
     return pos_t, nrm, tri
 
 
-def trace_any(arrays, ro, rd, traversal=0):
+def trace_any(arrays, ro, rd, traversal=0, nthreads=1):
     s = scene_struct(arrays)
     ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
     rd = np.ascontiguousarray(rd, np.float32).reshape(-1, 3)
     n = len(ro)
     vis = np.zeros(n, np.uint8)
-    lib().or_trace_any(C.byref(s), n, fptr(ro), fptr(rd), traversal, vis.ctypes.data_as(C.POINTER(C.c_uint8)))
+
+    def run(i0, i1):
+        lib().or_trace_any(C.byref(s), i1 - i0, fptr(ro[i0:i1]), fptr(rd[i0:i1]), traversal,
+                           vis[i0:i1].ctypes.data_as(C.POINTER(C.c_uint8)))
+
+    _chunks(n, nthreads, run)
     return vis
 
 
@@ -202,10 +224,11 @@ def model_margins(arrays, safe_c=0.0):
     return {"node_w": nw, "tri_w": tw, "p": float(p[0]), "contained": bool(ok)}
 
 
-def model_trace(arrays, ro, rd, mode, margins=None):
+def model_trace(arrays, ro, rd, mode, margins=None, nthreads=1):
     """trav_model.c: closest (triangle id, t) and any-hit visibility under culling rule `mode`
     (0 none, 1 round 3, 2 round 4, 6 round-5 candidate with safe-ray margins) and the number of
-    boxes tested."""
+    boxes tested.  nthreads > 1 splits the rays over threads (not for mode 6: its safe-ray switch is
+    module state)."""
     s = scene_struct(arrays)
     m = margins or model_margins(arrays)
     ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
@@ -214,10 +237,16 @@ def model_trace(arrays, ro, rd, mode, margins=None):
     tri = np.zeros(n, np.int32)
     t = np.zeros(n, np.float32)
     vis = np.zeros(n, np.uint8)
-    nodes = C.c_uint64(0)
-    lib().or_model_trace(C.byref(s), n, fptr(ro), fptr(rd), mode, fptr(m["node_w"]), fptr(m["tri_w"]), m["p"],
-                         tri.ctypes.data_as(_i), fptr(t), vis.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(nodes))
-    return tri, t, vis, int(nodes.value)
+
+    def run(i0, i1):
+        nodes = C.c_uint64(0)
+        lib().or_model_trace(C.byref(s), i1 - i0, fptr(ro[i0:i1]), fptr(rd[i0:i1]), mode, fptr(m["node_w"]),
+                             fptr(m["tri_w"]), m["p"], tri[i0:i1].ctypes.data_as(_i), fptr(t[i0:i1]),
+                             vis[i0:i1].ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(nodes))
+        return int(nodes.value)
+
+    boxes = sum(_chunks(n, 1 if mode == 6 else nthreads, run))
+    return tri, t, vis, boxes
 
 
 def env_build(tex: np.ndarray):

@@ -126,6 +126,33 @@ static int run_cpu(const std::string& assets) {
         scene->set_environment_light(std::make_shared<EnvironmentLight>(tmp));  // another object, same path
         d = scene->desc(dp);
         CHECK(d.env_w == 2 && d.env_h == 1);
+        // copies keep the original's light id: two copies re-pointed the same number of times at
+        // different files must still reload when swapped
+        {
+            const std::string tmp2 = tmp + ".b.hdr";
+            auto base = std::make_shared<EnvironmentLight>(tmp);
+            auto ca = std::make_shared<EnvironmentLight>(*base), cb = std::make_shared<EnvironmentLight>(*base);
+            CHECK(ca->get_id() == cb->get_id());
+            write_hdr(4, 2);
+            ca->set_texture_filepath(tmp);
+            {
+                FILE* f = std::fopen(tmp2.c_str(), "wb");
+                std::fprintf(f, "#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y %d +X %d\n", 5, 7);
+                for (int i = 0; i < 35; i++) std::fputc(128, f), std::fputc(64, f), std::fputc(32, f), std::fputc(129, f);
+                std::fclose(f);
+            }
+            cb->set_texture_filepath(tmp2);
+            scene->set_environment_light(ca);
+            d = scene->desc(dp);
+            CHECK(d.env_w == 4 && d.env_h == 2);
+            scene->set_environment_light(cb);
+            d = scene->desc(dp);
+            CHECK(d.env_w == 7 && d.env_h == 5);
+            scene->set_environment_light(ca);
+            d = scene->desc(dp);
+            CHECK(d.env_w == 4 && d.env_h == 2);
+            std::remove(tmp2.c_str());
+        }
         std::remove(tmp.c_str());
         scene->set_environment_light(grey);
     }

@@ -173,19 +173,35 @@ def test_gather_with_an_empty_rank_gloo_world3():
 
 
 def test_strong_split_slots():
-    """--scaling strong / the strong section of an N>1 run: path slots grow with the ranks so every
-    GPU keeps the one-GPU run's paths in flight, bounded by spp and by the per-GPU state budget
-    (the film is allocated for the whole frame on every rank); one value for all ranks."""
+    """The strong split (bench.py's N > 1 headline): path slots grow with the ranks so every GPU keeps
+    the one-GPU run's paths in flight, bounded by spp, by 256 and by the per-GPU state budget over
+    the rank's own (compact) path state; one value for all ranks."""
     import bench
 
+    T = bench.MULTI_TILE
     assert parallel.strong_slots(24, 1, 1920, 1080, 256) == 24
-    assert parallel.strong_slots(24, 2, 1920, 1080, 256) == 48
-    s8 = parallel.strong_slots(24, 8, 1920, 1080, 256)
-    assert 24 < s8 <= 192 and s8 * 1920 * 1080 * parallel.PATH_BYTES <= parallel.SLOT_BUDGET_BYTES
-    assert parallel.strong_slots(16, 8, 3840, 2160, 1024) * 3840 * 2160 * parallel.PATH_BYTES <= parallel.SLOT_BUDGET_BYTES
-    assert parallel.strong_slots(16, 8, 256, 256, 16) == 16  # spp bound: a slot renders at least one sample
+    assert parallel.strong_slots(24, 2, 1920, 1080, 256, T) == 48
+    assert parallel.strong_slots(24, 8, 1920, 1080, 256, T) == 192  # no longer capped by a whole-frame budget
+    for W, H, base, spp in ((1920, 1080, 24, 256), (3840, 2160, 16, 1024), (4096, 4096, 16, 4096)):
+        for world in (2, 4, 8):
+            s = parallel.strong_slots(base, world, W, H, spp, T)
+            px = parallel.rank_path_pixels(world, W, H, T)
+            assert base <= s <= min(base * world, 256) and s * px < 2 ** 31
+            assert s * px * parallel.PATH_BYTES <= parallel.SLOT_BUDGET_BYTES
+    assert parallel.strong_slots(16, 8, 256, 256, 16, T) == 16  # spp bound: a slot renders at least one sample
     a = bench.parse(["--gpus", "8", "--no-gather"])
-    assert a.no_gather and not a.no_strong and not a.no_verify_gather and a.scaling == "weak"
+    assert a.no_gather and not a.no_strong and not a.no_weak and not a.no_verify_gather and a.scaling == "strong"
+
+
+def test_rank_path_pixels_cover_the_partition():
+    """The compact layout's per-rank path state: tiles x tile pixels of the rank's own tiles, edge
+    overhang included; the ranks together hold every tile once (1/N of the full layout's state)."""
+    for W, H, T in ((1920, 1080, 64), (3840, 2160, 64), (300, 70, 64)):
+        nx, ny = parallel.tile_grid(W, H, T)
+        for world in (1, 2, 3, 8):
+            per = [len(parallel.tiles_for_rank(r, world, W, H, T)) * T * T for r in range(world)]
+            assert sum(per) == nx * ny * T * T
+            assert parallel.rank_path_pixels(world, W, H, T) == max(per)
 
 
 def test_multi_gpu_tile_balances_pixels():
@@ -211,37 +227,57 @@ class _FakeStats:
             setattr(self, k, 0)
         self.extend_rays = px
 
+    @property
+    def rays(self):
+        return self.extend_rays
+
 
 class _FakeTracer:
-    """The allocation rules of mcpt_film_resize / mcpt_set_path_slots (runtime.cpp): path state for
-    W x H x slots paths, refused at >= 2^31 paths, re-allocated at the current film size by
-    set_path_slots; plus a per-GPU memory cap (one MI355X: 288 GB) at ~234 B per path (state +
-    queues)."""
+    """The allocation rules of runtime.cpp: path state of slots x npx paths, npx = W x H (full
+    layout) or the tile set's tiles x tile pixels (compact, mcpt_set_compact_paths); refused at >= 2^31
+    paths; resize resets the tile set to every tile; set_path_slots keeps the tile set in the compact
+    layout (re-sizes at the film size in the full one); set_tiles re-allocates in the compact layout.
+    Plus a per-GPU memory cap (one MI355X: 288 GB) at ~234 B per path (state + queues)."""
     CAP = 288e9
 
     def __init__(self):
-        self.W = self.H = 0
+        self.W = self.H = self.T = 0
         self.slots = 1
+        self.compact = False
         self.peak = 0.0
+        self.ntiles = 0
         self.tiles = None
 
-    def _alloc(self, W, H, slots):
-        P = W * H * slots
-        assert P < 2 ** 31, f"film too large for the path slots: {W}x{H}x{slots}"
-        assert P * 234 <= self.CAP, f"out of memory: {W}x{H}x{slots}"
+    def _alloc(self):
+        if not self.W:
+            return
+        npx = self.ntiles * self.T * self.T if self.compact else self.W * self.H
+        P = npx * self.slots
+        assert P < 2 ** 31, f"film too large for the path slots: {npx} px x {self.slots}"
+        assert P * 234 <= self.CAP, f"out of memory: {npx} px x {self.slots}"
         self.peak = max(self.peak, P * 234)
 
+    def set_compact_paths(self, on=True):
+        self.compact = bool(on)
+        self._alloc()
+
     def set_path_slots(self, s):
-        if self.W:
-            self._alloc(self.W, self.H, s)
         self.slots = s
+        self._alloc()
 
     def resize(self, W, H, tw, th):
-        self._alloc(W, H, self.slots)
-        self.W, self.H = W, H
+        self.W, self.H, self.T = W, H, tw
+        nx, ny = parallel.tile_grid(W, H, tw)
+        self.ntiles = nx * ny
+        self.tiles = None
+        self._alloc()
 
     def set_tiles(self, t):
         self.tiles = t
+        nx, ny = parallel.tile_grid(self.W, self.H, self.T)
+        self.ntiles = nx * ny if t is None else len(t)
+        if self.compact:
+            self._alloc()
 
     def clear(self):
         pass
@@ -273,12 +309,13 @@ class _FakeDist:
         return "gloo"
 
 
-def test_strong_split_fits_after_the_weak_frame():
-    """bench.py main renders the weak frame (1920 x 1080 N at the base slots), then run_strong
-    switches to the config's own frame with the strong split's slots.  The switch must shrink the
-    film before raising the slots: set_path_slots at the weak film's size would ask for
-    1920 x 8640 x 131 paths at N = 8 (2^31 and 274 GB: the round-4 rehearsal at N = 4 ran out of
-    memory this way).  Checked for N = 2 / 4 / 8 on configs 2 and 4 with the allocator's rules."""
+def test_split_layouts_fit_one_gpu():
+    """bench.py N > 1: the headline split and the other one run back to back on every rank
+    (strong then weak by default, and the reverse under --scaling weak).  Each layout allocates the
+    film at one slot, then the rank's tiles (compact path state), then the slots, so no step asks for
+    slots x the whole frame: the round-4 N = 4 rehearsal ran out of memory on a weak film with the
+    strong split's slots.  Checked for N = 2 / 4 / 8 on configs 2, 4 and 5 with the allocator's rules;
+    each rank's path state is its own tiles' (about 1/N of the frame)."""
     import argparse
     import types
 
@@ -289,14 +326,18 @@ def test_strong_split_fits_after_the_weak_frame():
 
     fake_torch = types.SimpleNamespace(cuda=types.SimpleNamespace(synchronize=lambda: None), tensor=torch.tensor,
                                        zeros_like=torch.zeros_like, float64=torch.float64)
-    for cid in (2, 4):
+    for cid in (2, 4, 5):
         rc = mcpt.CONFIGS[cid]
         for world in (2, 4, 8):
-            pt = _FakeTracer()
-            base = bench.BENCH_SLOTS[cid]
-            pt.set_path_slots(base)
-            pt.resize(rc.width, rc.height * world, bench.part_tile(world), bench.part_tile(world))  # the weak frame
-            args = argparse.Namespace(slots=None, config=cid, steps=1, warmup=0, no_gather=True, no_verify_gather=True)
-            out = bench.run_strong(pt, rc, 0, world, _FakeDist(world), "gloo", rc.spp, args, fake_torch)
-            assert (pt.W, pt.H) == (rc.width, rc.height) and out["slots"] == pt.slots
-            assert pt.peak <= _FakeTracer.CAP
+            for order in (("strong", "weak"), ("weak", "strong")):
+                pt = _FakeTracer()
+                for rank in (0, world - 1):
+                    for kind in order:
+                        args = argparse.Namespace(slots=None, config=cid, steps=1, warmup=0)
+                        run = bench.run_split(pt, rc, rank, world, _FakeDist(world), "gloo", kind, rc.spp, args,
+                                              fake_torch)
+                        lay = run["layout"]
+                        assert pt.compact and pt.slots == lay["slots"] and [pt.W, pt.H] == lay["frame"]
+                        assert lay["path_pixels_rank"] == len(pt.tiles) * pt.T * pt.T
+                        assert lay["path_pixels_rank"] <= 1.1 * lay["frame"][0] * lay["frame"][1] / world + 4 * 64 * 64
+                assert pt.peak <= _FakeTracer.CAP

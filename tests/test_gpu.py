@@ -827,11 +827,13 @@ def test_ploc_small_and_degenerate_inputs(mcpt_mod, oracle):
         pt.close()
 
 
+@pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("slots", [1, 2])
-def test_native_gather_equals_one_pass(mcpt_mod, scene_c2, slots):
+def test_native_gather_equals_one_pass(mcpt_mod, scene_c2, slots, compact):
     """mcpt_gather (C ABI): three contexts render the interleaved tile partition of a frame
     ((tx + ty) mod 3, as three GPUs would) and the root gathers the others' tiles; the root's film
-    then equals the single-context frame bit for bit (path slots resolved before the copy)."""
+    then equals the single-context frame bit for bit (path slots resolved before the copy).
+    compact: every context holds path state for its own tiles only (mcpt_set_compact_paths)."""
     from mcpt import parallel
 
     rc = mcpt_mod.CONFIGS[2]
@@ -844,6 +846,8 @@ def test_native_gather_equals_one_pass(mcpt_mod, scene_c2, slots):
     parts = []
     for r in range(3):
         pt = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)
+        if compact:
+            pt.set_compact_paths(True)
         pt.set_path_slots(slots)
         pt.set_tiles(parallel.tiles_for_rank(r, 3, W, H, T))
         pt.render()
@@ -858,6 +862,88 @@ def test_native_gather_equals_one_pass(mcpt_mod, scene_c2, slots):
         mcpt_mod.gather([parts[0], parts[0]], root=0)  # a context listed twice
     for pt in parts + [full]:
         pt.close()
+
+
+def test_compact_paths_layout(mcpt_mod, scene_c2):
+    """mcpt_set_compact_paths: path state over the tile set only (a multi-GPU rank's 1/N).  Films are
+    the full layout's bit for bit: the whole tile set in a scrambled order, a partition's tiles with 3
+    path slots, the reference's one-tile-per-call loop over the set's tiles, and a partition packed
+    and unpacked into a compact root (the RCCL gather's two halves).  Tiles outside the set are
+    rejected by mcpt_wavefront_step, duplicates by mcpt_set_tiles; path slots keep the set."""
+    from mcpt import parallel
+
+    rc = mcpt_mod.CONFIGS[2]
+    W, H, T = 200, 120, 64  # ragged: the last tile row and column overhang the film
+    cam = mcpt_mod.config_camera(rc, W, H)
+    full = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)
+    full.set_path_slots(3)
+    full.render()
+    L0, s0 = full.film()
+    nx, ny = parallel.tile_grid(W, H, T)
+    every = [(tx, ty) for ty in range(ny) for tx in range(nx)]
+    rng = np.random.default_rng(5)
+    scrambled = [every[i] for i in rng.permutation(len(every))]
+    pt = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)
+    pt.set_compact_paths(True)
+    pt.set_path_slots(3)
+    pt.set_tiles(scrambled)
+    pt.render()
+    L1, s1 = pt.film()
+    assert np.array_equal(L0.view(np.uint32), L1.view(np.uint32)) and np.array_equal(s0, s1)
+    # one rank of three: its own tiles equal the full frame's, the rest of the film is zero
+    mine = parallel.tiles_for_rank(1, 3, W, H, T)
+    pt.set_tiles(mine)
+    pt.set_path_slots(2)  # keeps the tile set (compact layout)
+    pt.set_path_slots(3)
+    pt.render()
+    L2, s2 = pt.film()
+    own = np.zeros((H, W), bool)
+    for tx, ty in mine:
+        own[ty * T:(ty + 1) * T, tx * T:(tx + 1) * T] = True
+    assert np.array_equal(s2[own], s0[own]) and not s2[~own].any()
+    assert np.array_equal(L2[own].view(np.uint32), L0[own].view(np.uint32)) and not L2[~own].any()
+    # the reference orchestration (one tile per call) over the set's tiles, one slot
+    ref = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)
+    ref.set_compact_paths(True)
+    ref.set_tiles(mine)
+    for it in range(40 * len(mine)):
+        ref.step(*mine[it % len(mine)])
+    L3, s3 = ref.film()
+    full.set_path_slots(1)
+    full.render()
+    Lf1, sf1 = full.film()
+    assert np.array_equal(s3[own], sf1[own]) and np.array_equal(L3[own].view(np.uint32), Lf1[own].view(np.uint32))
+    other = next(t for t in every if t not in mine)
+    with pytest.raises(mcpt_mod.McptError):
+        ref.step(*other)
+    with pytest.raises(mcpt_mod.McptError):
+        ref.set_tiles([mine[0], mine[0]])
+    # pack on this rank, unpack into a compact root that owns the other tiles (mcpt/parallel.py's
+    # gather without the transport): the root's film is then the whole frame
+    import ctypes as C
+
+    import torch
+
+    root = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)
+    root.set_compact_paths(True)
+    root.set_path_slots(3)
+    root.set_tiles([t for t in every if t not in mine])
+    root.render()
+    n = C.c_uint32()
+    lib = mcpt_mod.lib()
+    assert lib.mcpt_film_pack_tiles(pt.h, None, C.byref(n)) == 0 and n.value == len(mine) * T * T
+    buf = torch.empty((n.value, 4), dtype=torch.float32, device="cuda")
+    assert lib.mcpt_film_pack_tiles(pt.h, C.c_void_p(buf.data_ptr()), C.byref(n)) == 0
+    xy = np.ascontiguousarray(mine, np.uint32).reshape(-1, 2)
+    assert lib.mcpt_film_unpack_tiles(root.h, C.c_void_p(buf.data_ptr()), xy.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                      len(mine)) == 0
+    L4, s4 = root.film()
+    assert np.array_equal(L0.view(np.uint32), L4.view(np.uint32)) and np.array_equal(s0, s4)
+    root.clear()  # a film clear empties the unpacked pixels too
+    _, s5 = root.film()
+    assert not s5.any()
+    for p in (full, pt, ref, root):
+        p.close()
 
 
 @pytest.mark.parametrize("gpu_bvh", [False, "ploc"])

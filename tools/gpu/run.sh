@@ -7,7 +7,8 @@
 #   test       python -m pytest tests -m gpu (TEST_ARGS adds pytest arguments)
 #   smoke      __graft_entry__.smoke()
 #   bench      bench.py $BENCH_ARGS                      -> gpurun_out/bench_$TAG.json
-#   kstats     rocprofv3 --kernel-trace --stats of bench  -> gpurun_out/kt_$TAG/
+#   kstats     rocprofv3 --kernel-trace --stats of bench  -> gpurun_out/kt_$TAG/ (profiled runs pass
+#              --no-work-counters: no extra counting frame, every launch is a timed or warmup frame's)
 #   pmc        FETCH_SIZE and WRITE_SIZE passes (separate runs, gpurun_out/pmcraw_<sfx>/) + four SQ /
 #              TCC counter passes of the same bench command (gpurun_out/pmct_<sfx>/), summarised by
 #              tools/pmc.py / tools/pmc_detail.py into profiles/ (kernel_stats_*, pmc_*, pmcdetail_*
@@ -23,7 +24,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 CONFIG=${CONFIG:-2}
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 STEPS=${STEPS:-3}
 O=gpurun_out
 BARGS="--no-cpu-baseline --config $CONFIG --steps $STEPS --warmup 1 ${BENCH_ARGS}"
@@ -45,7 +46,7 @@ for step in "$@"; do
     cut -c1-600 $O/bench_$sfx.json ;;
   kstats)
     rm -rf $O/kt_$sfx
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt_$sfx -o kt --output-format csv -- python3 bench.py $BARGS \
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt_$sfx -o kt --output-format csv -- python3 bench.py $BARGS --no-work-counters \
       > $O/kt_$sfx.log 2>&1 || fail kstats 20 $O/kt_$sfx.log
     f=$(find $O/kt_$sfx -name "*kernel_stats.csv" | head -1)
     cp "$f" $O/kernel_stats_$sfx.csv
@@ -62,7 +63,7 @@ PY
     rm -rf $R && mkdir -p $R
     for c in FETCH_SIZE WRITE_SIZE; do
       d=$R/prof_$([[ $c == FETCH_SIZE ]] && echo fetch || echo write)
-      timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace -d $d -o p --output-format csv -- python3 bench.py $BARGS \
+      timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace -d $d -o p --output-format csv -- python3 bench.py $BARGS --no-work-counters \
         > $d.log 2>&1 || fail "pmc $c" 20 $d.log
     done
     if [[ "$FETCH_ONLY" == 1 ]]; then echo "fetch/write passes only"; continue; fi
@@ -74,7 +75,7 @@ PY
                "SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_FLAT SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR" \
                "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum"; do
       i=$((i+1))
-      timeout -k 10 600 rocprofv3 --pmc $set --kernel-trace -d $O/pmct_$sfx/p$i -o p$i --output-format csv -- python3 bench.py $BARGS \
+      timeout -k 10 600 rocprofv3 --pmc $set --kernel-trace -d $O/pmct_$sfx/p$i -o p$i --output-format csv -- python3 bench.py $BARGS --no-work-counters \
         > $O/pmct_$sfx/p$i.log 2>&1 || fail "pmc pass $i" 10 $O/pmct_$sfx/p$i.log
     done
     PMC_CONFIG=$CONFIG PMC_ARGS="$BARGS" STATS_NAME=kernel_stats_$sfx python3 tools/pmc.py $sfx $R > /dev/null &&

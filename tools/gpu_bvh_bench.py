@@ -17,16 +17,17 @@ for c in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "2,3,5").split(
     for b in ("sah", "ploc", "lbvh"):
         gpu = False if b == "sah" else b
         pt.upload_scene(s, gpu_bvh=gpu)
-        pt.set_work_counters(True)  # StageStats node / test counts
         if gpu:
-            pt.upload_scene(s, gpu_bvh=gpu)
-            pt.set_work_counters(True)  # StageStats node / test counts  # second build: warm
+            pt.upload_scene(s, gpu_bvh=gpu)  # second build: warm
             r[f"gpu_{b}_build_ms"] = round(pt.last_build_ms, 2)
         pt.set_camera(mcpt.config_camera(rc)); pt.resize(rc.width, rc.height)
         pt.iterate(20)
-        st = pt.iterate(20)
+        st = pt.iterate(20)  # timed with the lean k_trace
         r[f"trace_ms_{b}"] = round(st.ms_extend / 20, 4)
-        r[f"nodes_per_ray_{b}"] = round((st.ext_nodes + st.any_nodes) / max(1, st.rays), 2)
+        pt.set_work_counters(True)  # node counts from 20 more, untimed iterations (counting build)
+        wk = pt.iterate(20)
+        pt.set_work_counters(False)
+        r[f"nodes_per_ray_{b}"] = round((wk.ext_nodes + wk.any_nodes) / max(1, wk.rays), 2)
     print(json.dumps(r), flush=True)
     out.append(r)
     pt.close()
