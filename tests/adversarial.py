@@ -14,6 +14,13 @@ can stray for a ray that grazes a triangle.  These generators aim at exactly tha
   grazing  rays that graze a triangle from 0.01..3 scene units away.
 
 Triangles are drawn from the largest ones (walls, ground quads) and from all of them.
+
+far_cut_rays (round 5) aims the corner construction at the *finite-margin*
+far cut: the grazed triangle T comes from the bounded triangles (finite W'_T: C2's spheres, C3/C5's
+icosphere, C4's head), with the crossing at t_S (1 +- 2^-6) and within (1 +- 2^-12).  Half the rays
+take S anywhere; the other half take S and T from adjacent bounded triangles (sharing a vertex) with
+the hit point near the shared vertex, so that the line meets T itself near t_S -- the case where the
+cull of T's leaf box decides the result.
 """
 from __future__ import annotations
 
@@ -61,25 +68,41 @@ def triangle_pools(a, n_big=16, seed=0):
     return big, np.arange(len(area))
 
 
-def corner_rays(a, m, seed, pool_s, pool_t, scale=1.0):
+def corner_rays(a, m, seed, pool_s, pool_t, scale=1.0, dmax=2.0 ** -6, pairs=None):
+    """Rays that hit S front-facing at t_S and cross T's plane at t_S (1 + delta), |delta| <= dmax,
+    grazing T (|cos| in [1e-6, 1e-3]).  S and T come from the pools, or (pairs = (S, T, shared
+    vertex) arrays) from given pairs with the hit point near the shared vertex."""
     rng = np.random.default_rng(seed)
     out_o, out_d = [], []
     have = 0
     for _ in range(50):
         k = 4 * (m - have) + 64
-        S = pool_s[rng.integers(0, len(pool_s), k)]
-        T = pool_t[rng.integers(0, len(pool_t), k)]
+        if pairs is None:
+            S = pool_s[rng.integers(0, len(pool_s), k)]
+            T = pool_t[rng.integers(0, len(pool_t), k)]
+        else:
+            pi = rng.integers(0, len(pairs[0]), k)
+            S, T, vs = pairs[0][pi], pairs[1][pi], pairs[2][pi]
         s0, s1, s2, ns = _tri_frames(a, S)
         t0, _, _, nt = _tri_frames(a, T)
         u, v = _bary(rng, k)
-        p = s0 + u[:, None] * (s1 - s0) + v[:, None] * (s2 - s0)
+        if pairs is None:
+            p = s0 + u[:, None] * (s1 - s0) + v[:, None] * (s2 - s0)
+        else:  # near the shared vertex: barycentric weights of S's other two corners up to eps
+            eps = 10.0 ** rng.uniform(-4, np.log10(0.3), k)
+            corners = np.stack([s0, s1, s2], 1)
+            j = np.argmin(np.linalg.norm(corners - vs[:, None, :], axis=2), axis=1)  # the shared corner
+            c0 = corners[np.arange(k), j]
+            c1 = corners[np.arange(k), (j + 1) % 3]
+            c2 = corners[np.arange(k), (j + 2) % 3]
+            p = c0 + (eps * u)[:, None] * (c1 - c0) + (eps * v)[:, None] * (c2 - c0)
         tS = scale * rng.uniform(0.05, 2.0, k)
         d, c = _grazing_dir(rng, nt)
         # S must be hit front-facing too: flip the tangential part when it is not
         bad = np.sum(d * ns, axis=1) >= 0
         d[bad] = d[bad] - 2 * (d[bad] - np.sum(d[bad] * nt[bad], axis=1, keepdims=True) * nt[bad])
         ok = np.sum(d * ns, axis=1) < 0
-        delta = rng.uniform(-2.0 ** -6, 2.0 ** -6, k)
+        delta = rng.uniform(-dmax, dmax, k)
         h = delta * tS * c  # height of p above T's plane: the line crosses it at tS (1 + delta)
         w = nt - np.sum(nt * ns, axis=1, keepdims=True) * ns  # in-plane direction of steepest height change
         wn = np.sum(nt * w, axis=1)
@@ -131,6 +154,139 @@ def grazing_rays(a, m, seed, pool, scale=1.0, band=(1e-6, 1e-3)):
     t = scale * rng.uniform(0.01, 3.0, m)
     o = q - t[:, None] * d + scale * 1e-5 * rng.normal(size=(m, 3))
     return o.astype(np.float32), d.astype(np.float32)
+
+
+U24 = 2.0 ** -24
+
+
+def bounded_pool(a):
+    """Triangles whose general culling bound is finite (mcpt_core.hpp "conservative box culling":
+    beta_T = 28.3u |e1||e2| / 1e-6 (1 + 2^-9) + 1.01u, unbounded when sqrt(3) beta_T >= 1/2), with
+    a 10 % margin below the switch."""
+    v0, v1, v2 = (np.asarray(a[k], np.float64) for k in ("v0", "v1", "v2"))
+    n1 = np.linalg.norm(v1 - v0, axis=1)
+    n2 = np.linalg.norm(v2 - v0, axis=1)
+    beta = 28.3 * U24 * n1 * n2 / 1e-6 * (1 + 2.0 ** -9) + 1.01 * U24
+    return np.nonzero(np.sqrt(3.0) * beta < 0.45)[0]
+
+
+def adjacent_pairs(a, pool):
+    """(S, T, shared vertex) for triangles of the pool that share a vertex (exact float equality,
+    as baked meshes share them): each triangle corner paired with the next two triangles around
+    the same vertex."""
+    pool = np.asarray(pool)
+    V = np.stack([np.asarray(a[k], np.float32)[pool] for k in ("v0", "v1", "v2")], 1)  # [n, 3, 3]
+    keys = np.ascontiguousarray(V.reshape(-1, 3)).view(np.dtype((np.void, 12))).ravel()
+    _, vid = np.unique(keys, return_inverse=True)
+    tri = np.repeat(pool, 3)
+    pos = V.reshape(-1, 3)
+    order = np.argsort(vid, kind="stable")
+    vs, ts, ps = vid[order], tri[order], pos[order]
+    start = np.searchsorted(vs, vs, side="left")
+    size = np.searchsorted(vs, vs, side="right") - start
+    S, T, P = [], [], []
+    for off in (1, 2):
+        sel = size > off
+        partner = start[sel] + (np.arange(len(vs))[sel] - start[sel] + off) % size[sel]
+        S.append(ts[sel])
+        T.append(ts[partner])
+        P.append(ps[sel])
+    S, T, P = np.concatenate(S), np.concatenate(T), np.concatenate(P)
+    keep = S != T
+    return S[keep], T[keep], P[keep].astype(np.float64)
+
+
+def level_corner_rays(a, m, seed, S_all, T_all, scale=1.0, dmax=2.0 ** -6):
+    """The corner construction placed directly: for a pair (S, T) whose planes cross inside S, the
+    hit point p is drawn on the segment of S at height h = delta t_S c above T's plane (the level set
+    of S's linear height function), so the ray that grazes T (|cos| = c in [1e-6, 1e-3]) and hits S
+    at p crosses T's plane at t_S (1 + delta), |delta| <= dmax.  Pairs (S_all[i], T_all[i]) are drawn
+    at random; those whose planes do not cross inside S are redrawn."""
+    rng = np.random.default_rng(seed)
+    out_o, out_d = [], []
+    have = 0
+    for _ in range(200):
+        k = 2 * (m - have) + 64
+        pi = rng.integers(0, len(S_all), k)
+        S, T = S_all[pi], T_all[pi]
+        s0, s1, s2, ns = _tri_frames(a, S)
+        t0, _, _, nt = _tri_frames(a, T)
+        tS = scale * rng.uniform(0.05, 2.0, k)
+        d, c = _grazing_dir(rng, nt)
+        bad = np.sum(d * ns, axis=1) >= 0  # S front-facing too: flip the part tangent to T's plane
+        d[bad] = d[bad] - 2 * (d[bad] - np.sum(d[bad] * nt[bad], axis=1, keepdims=True) * nt[bad])
+        ok = (np.sum(d * ns, axis=1) < 0) & (S != T)
+        h = rng.uniform(-dmax, dmax, k) * tS * c
+        V = np.stack([s0, s1, s2], 1)
+        g = np.einsum("kij,kj->ki", V - t0[:, None, :], nt) - h[:, None]  # heights above the level
+        pts, val = [], []
+        for i, j in ((0, 1), (1, 2), (2, 0)):
+            gi, gj = g[:, i], g[:, j]
+            cross = gi * gj < 0
+            w = np.where(cross, gi / np.where(cross, gi - gj, 1.0), 0.0)
+            pts.append(V[:, i] + w[:, None] * (V[:, j] - V[:, i]))
+            val.append(cross)
+        pts, val = np.stack(pts, 1), np.stack(val, 1)
+        two = val.sum(1) == 2
+        order = np.argsort(~val, axis=1, kind="stable")[:, :2]  # the two crossed edges
+        A = pts[np.arange(k), order[:, 0]]
+        B = pts[np.arange(k), order[:, 1]]
+        r = rng.random(k)
+        p = A + r[:, None] * (B - A)
+        keep = ok & two & np.isfinite(p).all(1)
+        out_o.append((p - tS[:, None] * d)[keep])
+        out_d.append(d[keep])
+        have += int(keep.sum())
+        if have >= m:
+            break
+    o, d = np.concatenate(out_o)[:m], np.concatenate(out_d)[:m]
+    return o.astype(np.float32), d.astype(np.float32)
+
+
+def crossing_pairs(a, pool_s, pool_t, n, seed):
+    """Up to n (S, T) pairs, S from pool_s and T from pool_t, whose planes cross inside S."""
+    rng = np.random.default_rng(seed)
+    S_out, T_out = [], []
+    got = 0
+    for _ in range(30):  # scenes of small triangles only (C4) find few such pairs: a pool of them is enough
+        k = 4 * n
+        S = pool_s[rng.integers(0, len(pool_s), k)]
+        T = pool_t[rng.integers(0, len(pool_t), k)]
+        s0, s1, s2, _ = _tri_frames(a, S)
+        t0, _, _, nt = _tri_frames(a, T)
+        g = np.stack([np.sum((v - t0) * nt, 1) for v in (s0, s1, s2)], 1)
+        sel = (g.min(1) < 0) & (g.max(1) > 0) & (S != T)
+        S_out.append(S[sel])
+        T_out.append(T[sel])
+        got += int(sel.sum())
+        if got >= n:
+            break
+    return np.concatenate(S_out)[:n], np.concatenate(T_out)[:n]
+
+
+def far_cut_rays(a, m, seed=0, scale=1.0, pool=None):
+    """m rays for the finite-margin far cut: T bounded; S anywhere (a quarter) or adjacent to T
+    (sharing a vertex: three quarters, the case where the line meets T itself near t_S); crossings
+    within t_S (1 +- 2^-6) and (1 +- 2^-12) in equal parts."""
+    bounded = bounded_pool(a) if pool is None else np.asarray(pool)
+    anyt = np.arange(len(a["v0"]))
+    Sa, Ta = crossing_pairs(a, anyt, bounded, 20000, seed)
+    Sp, Tp, _ = adjacent_pairs(a, bounded)
+    k = m // 8
+    j = (m - 2 * k) // 2
+    parts = [level_corner_rays(a, k, seed + 1, Sa, Ta, scale, 2.0 ** -6),
+             level_corner_rays(a, k, seed + 2, Sa, Ta, scale, 2.0 ** -12),
+             level_corner_rays(a, j, seed + 3, Sp, Tp, scale, 2.0 ** -6),
+             level_corner_rays(a, m - 2 * k - j, seed + 4, Sp, Tp, scale, 2.0 ** -12)]
+    return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+
+
+def engaged(a, ro, rd, T_hit):
+    """Fraction of rays whose closest hit T_hit (>= 0) is a bounded triangle: there the far cut of
+    a bounded leaf decided between candidates at nearly one t."""
+    b = np.zeros(len(a["v0"]), bool)
+    b[bounded_pool(a)] = True
+    return float(np.mean((T_hit >= 0) & b[np.maximum(T_hit, 0)]))
 
 
 def adversarial_rays(a, m, seed=0, scale=1.0):

@@ -264,6 +264,48 @@ def test_cull_margins_monotone_and_scale_free(oracle, adv_scenes):
     assert np.isfinite(m["tri_w"]).mean() > 0.99
 
 
+# ---- the finite-margin far cut ------------------------------------------
+# adversarial_rays' corner rays graze the 16 largest triangles, whose margins are infinite on C2:
+# they never exercise a finite far cut.  far_cut_rays grazes the bounded triangles (finite W'_T)
+# with S anywhere or adjacent to T.  At x1e3 no C2 triangle is bounded (|e1||e2| grows against the
+# fixed det threshold 1e-6), at x1e-3 every one is (the walls included).
+FAR_SCENES = [("c2", 1.0), ("c2", 1e-3), ("c3", 1.0), ("c4", 1.0)]
+FAR_RAYS = 1000000
+
+
+@pytest.fixture(scope="module")
+def far_scenes(mcpt_mod, adv_scenes):
+    out = dict(adv_scenes)
+    out[("c4", 1.0)] = mcpt_mod.build_config_scene(4).arrays()
+    return out
+
+
+@pytest.mark.parametrize("name,scale", FAR_SCENES)
+def test_far_cut_model_equals_reference(oracle, far_scenes, name, scale):
+    """1 M far-cut rays per scene through the model of the product's traversal (trav_model.c mode
+    2: the round-4 bound, finite margins on the grazed triangles) against the oracle's cull-free
+    reference traversal: closest triangle, t and visibility bit for bit.  Most closest hits are on
+    a bounded triangle (the far cut of its leaf decided between candidates at nearly one t)."""
+    from adversarial import bounded_pool, engaged, far_cut_rays
+
+    a = far_scenes[(name, scale)]
+    assert len(bounded_pool(a)) > 0
+    ro, rd = far_cut_rays(a, FAR_RAYS, seed=41, scale=scale)
+    assert len(ro) == FAR_RAYS
+    th = max(1, min(8, os.cpu_count() or 1))
+    pos_t, _, otri = oracle.trace_closest(a, ro, rd, nthreads=th)
+    ovis = oracle.trace_any(a, ro, rd, nthreads=th)
+    m = oracle.model_margins(a)
+    assert m["contained"]
+    tri, t, vis, _ = oracle.model_trace(a, ro, rd, 2, m, nthreads=th)
+    assert np.array_equal(tri, otri), f"{(tri != otri).sum()} closest hits differ"
+    assert np.array_equal(t.view(np.uint32), pos_t[:, 3].view(np.uint32))
+    assert np.array_equal(vis, ovis), f"{(vis != ovis).sum()} visibilities differ"
+    e = engaged(a, ro, rd, otri)
+    assert e > 0.5, e
+    print(f"{name} x{scale}: {FAR_RAYS} far-cut rays, {e:.3f} with a bounded closest hit, 0 differ")
+
+
 # ---- a round-5 candidate, modelled on the CPU (DESIGN.md section 9, item 1) ---------------
 SAFE_C = 1e-3
 
@@ -345,7 +387,41 @@ def test_safe_ray_margins_model_equals_reference(oracle, adv_scenes, name, scale
 
 # ---- the product on the GPU -----------------------------------------------------------------
 GPU_SCENES = [("c2", 1.0, 1000000), ("c2", 1e3, 1000000), ("c2", 1e-3, 1000000), ("c3", 1.0, 1000000),
-              ("floor", 1.0, 1000000), ("c5", 1.0, 500000)]
+              ("floor", 1.0, 1000000), ("c5", 1.0, 500000), ("c4", 1.0, 1000000)]
+# far-cut rays (finite margins) on every scene with bounded triangles; tiny: the 2-entry LDS stack
+# instantiation (mcpt_debug_tiny_lds_stack), so that scratch stack entries carry adversarial rays
+GPU_FAR = [("c2", 1.0, False), ("c2", 1e-3, False), ("c3", 1.0, False), ("c4", 1.0, False), ("c5", 1.0, False),
+           ("c2", 1.0, True), ("c4", 1.0, True), ("c5", 1.0, True)]
+
+
+def _gpu_scene(mcpt_mod, request, name, scale):
+    if name == "c3":
+        return request.getfixturevalue("scene_c3")
+    if name == "floor":
+        s = floor_scene(mcpt_mod)
+    elif name in ("c4", "c5"):
+        s = mcpt_mod.build_config_scene(int(name[1]))
+    else:
+        s = scaled_scene(mcpt_mod, 2, scale)
+    return s, s.arrays()
+
+
+def _gpu_vs_oracle(mcpt_mod, oracle, s, a, ro, rd, tiny=False):
+    pt = mcpt_mod.PathTracer(0)
+    pt.upload_scene(s)
+    if tiny:
+        pt.set_tiny_lds_stack(True)
+    gp, gn, gt = pt.trace_closest(ro, rd)
+    gv = pt.trace_any(ro, rd)
+    pt.close()
+    th = max(1, min(8, os.cpu_count() or 1))
+    op_, on, ot = oracle.trace_closest(a, ro, rd, nthreads=th)
+    ov = oracle.trace_any(a, ro, rd, nthreads=th)
+    bad = np.nonzero((gt != ot) | (gv != ov))[0]
+    assert len(bad) == 0, f"{len(bad)} of {len(ro)} rays differ, first {bad[:5]}"
+    assert np.array_equal(gp.view(np.uint32), op_.view(np.uint32))
+    assert np.array_equal(gn.view(np.uint32), on.view(np.uint32))
+    return ot, ov
 
 
 @pytest.mark.gpu
@@ -354,27 +430,23 @@ def test_gpu_cull_adversarial(mcpt_mod, oracle, request, name, scale, n):
     """k_trace (persistent traversal, pair or 4-wide nodes, conservative culls) against the
     oracle's cull-free reference traversal on adversarial rays: closest-hit triangle, t, position,
     normal and any-hit visibility bit for bit.  C5 (2 M triangles) runs the 4-wide nodes."""
-    if name == "c3":
-        s, a = request.getfixturevalue("scene_c3")
-    elif name == "floor":
-        s = floor_scene(mcpt_mod)
-        a = s.arrays()
-    elif name == "c5":
-        s = mcpt_mod.build_config_scene(5)
-        a = s.arrays()
-    else:
-        s = scaled_scene(mcpt_mod, 2, scale)
-        a = s.arrays()
+    s, a = _gpu_scene(mcpt_mod, request, name, scale)
     ro, rd = adversarial_rays(a, n, seed=23, scale=scale)
-    pt = mcpt_mod.PathTracer(0)
-    pt.upload_scene(s)
-    gp, gn, gt = pt.trace_closest(ro, rd)
-    gv = pt.trace_any(ro, rd)
-    pt.close()
-    op_, on, ot = oracle.trace_closest(a, ro, rd)
-    ov = oracle.trace_any(a, ro, rd)
-    bad = np.nonzero((gt != ot) | (gv != ov))[0]
-    assert len(bad) == 0, f"{len(bad)} of {n} rays differ, first {bad[:5]}"
-    assert np.array_equal(gp.view(np.uint32), op_.view(np.uint32))
-    assert np.array_equal(gn.view(np.uint32), on.view(np.uint32))
+    ot, ov = _gpu_vs_oracle(mcpt_mod, oracle, s, a, ro, rd)
     print(f"{name} x{scale}: {n} rays, {(ot >= 0).mean():.3f} hit, {(ov == 0).mean():.3f} occluded, 0 differ")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,scale,tiny", GPU_FAR)
+def test_gpu_far_cut_adversarial(mcpt_mod, oracle, request, name, scale, tiny):
+    """k_trace on 1 M far-cut rays (tests/adversarial.py far_cut_rays: the grazed triangle bounded,
+    S anywhere or adjacent, crossings within t_S (1 +- 2^-6) and (1 +- 2^-12)) against the oracle's
+    cull-free traversal, bit for bit: C2 (pairs, 8-entry stack), C3 and C5 (4-wide), C4 (pairs,
+    deep 10-entry stack: k_trace<2,10>); tiny = the 2-entry LDS stack with scratch entries."""
+    from adversarial import engaged, far_cut_rays
+
+    s, a = _gpu_scene(mcpt_mod, request, name, scale)
+    ro, rd = far_cut_rays(a, FAR_RAYS, seed=43, scale=scale)
+    ot, ov = _gpu_vs_oracle(mcpt_mod, oracle, s, a, ro, rd, tiny)
+    print(f"{name} x{scale} tiny={tiny}: {len(ro)} far-cut rays, {engaged(a, ro, rd, ot):.3f} bounded closest hits, "
+          f"{(ov == 0).mean():.3f} occluded, 0 differ")
