@@ -331,6 +331,30 @@ def roofline(st, ms_trace, ms_shade, config, slots, work=None):
     return roof
 
 
+def trace_phases(work):
+    """k_trace's lane utilisation split by loop phase, from the counting frame's phase counts
+    (mcpt_debug_trace_profile): node phase = node steps / (64 x node-phase wave iterations),
+    triangle phase = triangle tests / (64 x triangle phases), and the lanes idle / parked at a
+    trip's start (after the refill)."""
+    ph = getattr(work, "phases", None) if work is not None else None
+    if not ph or not ph.get("trips"):
+        return None
+    trips = ph["trips"]
+    node_steps = work.ext_nodes + work.any_nodes
+    return {"node_phase_lane_util": round(node_steps / max(1, 64 * ph["node_iters"]), 4),
+            "tri_phase_lane_util": round(ph["tri_lanes"] / max(1, 64 * ph["tri_phases"]), 4),
+            "node_iters_per_trip": round(ph["node_iters"] / trips, 3),
+            "tri_phases_per_trip": round(ph["tri_phases"] / trips, 4),
+            "refills_per_trip": round(ph["refills"] / trips, 4),
+            "lanes_refilled_per_refill": round(ph["refill_lanes"] / max(1, ph["refills"]), 2),
+            "trip_start_lanes": {"node_work": round(ph["trip_node_lanes"] / (64 * trips), 4),
+                                 "parked_leaf": round(ph["trip_leaf_lanes"] / (64 * trips), 4),
+                                 "idle": round(ph["trip_idle_lanes"] / (64 * trips), 4)},
+            "counts": ph,
+            "what": "counting k_trace build, one untimed frame: wave iterations of the node-phase loop (per trip "
+                    "the busiest lane's steps) and triangle phases, with the lanes doing work in each"}
+
+
 def extend_shade(st, frame_s, steps, config, slots):
     """The metric's own roofline fraction: the whole wavefront step (extend + shade: k_shade,
     k_material, k_trace) against 8 TB/s, per frame.  state: SURVEY.md 8(d)'s algorithmic bytes
@@ -528,7 +552,8 @@ def main():
     scene = mcpt.build_config_scene(args.config)
     cam = mcpt.config_camera(rc, rc.width, rc.height)  # the config's view at any N (see docstring)
     pt = mcpt.PathTracer(local, mcpt.default_config(spp=spp, max_depth=rc.max_depth))
-    pt.upload_scene(scene)
+    # MCPT_GPU_BVH=ploc|lbvh: the device-built tree (A/B of tree quality; films do not depend on the tree)
+    pt.upload_scene(scene, gpu_bvh=os.environ.get("MCPT_GPU_BVH") or False)
     pt.set_camera(cam)
 
     # the headline split (value); N = 1: the config's frame on one GPU (both splits are that frame)
@@ -563,6 +588,7 @@ def main():
         work = Acc()
         work.add(pt.render())
         work.occ = pt.occ_stats()[0]
+        work.phases = pt.trace_profile()
         pt.set_work_counters(False)
     per_rank = head["per_rank"]
     gather = None
@@ -587,6 +613,9 @@ def main():
     K = args.steps
     roof = roofline(st, st.ms_extend, st.ms_shade, args.config, slots, work)
     roof["extend_shade"] = extend_shade(st, dt_all / K, K, args.config, slots)
+    tp = trace_phases(work)
+    if tp:
+        roof["k_trace_phases"] = tp
     roof["measured_copy_GBps"] = round(pt.hbm_copy_gbps(1 << 30, 20), 1)  # one-pass dwordx4 copy ceiling
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

@@ -282,8 +282,12 @@ int mcpt_debug_occ_stats(const mcpt_ctx *ctx, uint64_t *resolved, int32_t *enabl
  * (the rest: NaN / zero directions and root-box misses resolved where the ray was made), any-hit
  * (shadow + BRDF visibility) rays, of them traversed, and of them resolved by the occluder cache. */
 int mcpt_debug_ray_counts(const mcpt_ctx *ctx, uint64_t *out);
-/* k_trace loop profile of the round-2/3 diagnostics builds, which are gone since round 4 (rocprofv3
- * counter passes replace them): returns 0, out12 untouched.  Kept so that existing callers link. */
+/* The traversal's loop-phase counts, recorded by the counting build (mcpt_set_work_counters on)
+ * since the last film clear or reset (reset = 1 starts a new count after reading): out12[0] loop
+ * trips, [1] refills, [2] lanes refilled, [3] node-phase wave iterations, [4] triangle phases,
+ * [5] lanes testing a triangle in them, [6] / [7] / [8] lanes with node work / a parked leaf / no
+ * ray at a trip's start; [9..11] 0.  With the node steps of mcpt_stage_stats they split the lane
+ * utilisation by phase.  Returns the number of words filled (9), 0 when none were recorded. */
 int mcpt_debug_trace_profile(mcpt_ctx *ctx, uint64_t *out12, int reset);
 /* diagnostics: the kernels' shared-denominator division (mcpt::quot3, mcpt_core.hpp) on the
  * device for n host pairs: out[i] = a[i] / b[i] as the kernels compute it (must equal IEEE fp32). */

@@ -62,6 +62,50 @@ __device__ inline void block_push(const bool (&want)[NQ], uint32_t* const (&coun
 }
 
 __device__ inline V3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
+
+// Path-state streams of the shading kernels (k_shade, k_material): every word is touched once per
+// kernel and iteration, over a state many times the L2 and MALL, so MCPT_NT marks these loads (bit
+// 1) and stores (bit 2) non-temporal -- streaming, not retained -- for the env tables, BVH and
+// occluder records to keep the caches (A/B knob; 0 = ordinary accesses).
+#ifndef MCPT_NT
+#define MCPT_NT 0
+#endif
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
+template <class T>
+__device__ inline T ld_s(const T* p) {
+    if constexpr (MCPT_NT & 1) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+__device__ inline float4 ld_s(const float4* p) {
+    if constexpr (MCPT_NT & 1) {
+        const f4v_t v = __builtin_nontemporal_load(reinterpret_cast<const f4v_t*>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
+__device__ inline uint4 ld_s(const uint4* p) {
+    if constexpr (MCPT_NT & 1) {
+        const u4v_t v = __builtin_nontemporal_load(reinterpret_cast<const u4v_t*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
+template <class T>
+__device__ inline void st_s(T* p, T v) {
+    if constexpr (MCPT_NT & 2) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ inline void st_s(float4* p, float4 v) {
+    if constexpr (MCPT_NT & 2) __builtin_nontemporal_store(f4v_t{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v_t*>(p));
+    else *p = v;
+}
+__device__ inline void st_s(uint4* p, uint4 v) {
+    if constexpr (MCPT_NT & 2) __builtin_nontemporal_store(u4v_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u4v_t*>(p));
+    else *p = v;
+}
 // the xyz of a float4 element with one dwordx3 load (one VGPR fewer than the float4)
 __device__ inline V3 ld3f4(const float4* p) {
     const float* f = reinterpret_cast<const float*>(p);
@@ -358,7 +402,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
     // the pixel and the sample index come with the record (k_shade: slot k of a pixel runs
     // samples k, k + S, k + 2S, ...)
     const Rng r{rng_key(a.seed, pix, sidx), len};
-    const V3 ro = xyz(a.p.ray_o[pid]), rdir = xyz(a.p.ray_d[pid]);
+    const V3 ro = xyz(ld_s(a.p.ray_o + pid)), rdir = xyz(ld_s(a.p.ray_d + pid));
     V3 pos, n;
     int mat;
     float t_hit;
@@ -381,9 +425,9 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
         if ((f_s.x == 0.f && f_s.y == 0.f && f_s.z == 0.f) || pdf_s == 0.f) nf |= F_FZERO;
         rr = f_s / pdf_s;
         const V3 new_o = pos + n * 0.001f;  // :358
-        a.p.beta[pid] = f4(beta_store, rr.x);
-        a.p.ray_o[pid] = f4(new_o, 0.f);
-        a.p.ray_d[pid] = f4(wi_s, 0.f);
+        st_s(a.p.beta + pid, f4(beta_store, rr.x));
+        st_s(a.p.ray_o + pid, f4(new_o, 0.f));
+        st_s(a.p.ray_d + pid, f4(wi_s, 0.f));
         mo.want_ext = true;
         if (ray_misses_scene(sc, new_o, wi_s)) {  // resolved here: isect stays "not found"
             a.p.hit_tri[pid] = -1;
@@ -425,7 +469,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
         float wL = power_heuristic(pdfl_x, pdfb_y);
         V3 cL = ((f_l * Li_l) * wL) / pdfl_x;
         if (wL > 0.f && pdfl_x > 0.f) nf |= F_CONDL;
-        a.p.nee0[pid] = f4(cL, rr.y);
+        st_s(a.p.nee0 + pid, f4(cL, rr.y));
         const V3 so_l = pos + n * 0.01f;
         if (ray_misses_scene(sc, so_l, ldir)) {
             a.p.vis[2 * pid] = 1;
@@ -487,8 +531,8 @@ __device__ inline void material_brdf_terms(const ShadeArgs& a, uint32_t pid, con
         cB = ((f_b * Li_b) * wB) / pdfb_x;
         if (wB > 0.f && pdfb_x > 0.f) nf |= F_CONDB;
     }
-    a.p.nee1[pid] = f4(cB, mo.rrz);
-    a.p.flags[pid] = nf;
+    st_s(a.p.nee1 + pid, f4(cB, mo.rrz));
+    st_s(a.p.flags + pid, nf);
 }
 
 #ifdef MCPT_SHADE_WPE
@@ -558,10 +602,10 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         // per-path state unconditionally, the len-dependent streams (ray_d for a
         // primary miss, the MIS terms and visibility for len > 1) at pid when needed
         // and at a shared dummy index 0 otherwise (no extra bandwidth).
-        const uint32_t fl = a.p.flags[pid];
-        uint32_t samples = a.p.samples[pid];
-        const int32_t htri = a.p.hit_tri[pid];
-        const float4 b4 = a.p.beta[(((fl >> F_LEN_SHIFT) & 0xffu) > 1u) ? pid : 0u];  // len 1: beta is (1,1,1), not loaded
+        const uint32_t fl = ld_s(a.p.flags + pid);
+        uint32_t samples = ld_s(a.p.samples + pid);
+        const int32_t htri = ld_s(a.p.hit_tri + pid);
+        const float4 b4 = ld_s(a.p.beta + ((((fl >> F_LEN_SHIFT) & 0xffu) > 1u) ? pid : 0u));  // len 1: beta is (1,1,1), not loaded
         const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
         const bool need_rd = len == 1 && htri < 0;
         const bool need_nee = len <= (uint32_t)a.max_depth && len > 1;
@@ -572,7 +616,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         const bool need_ld = !(fl & F_DEAD) && (need_rd || need_nee);
         const V3 ld4 = ld3f4(a.p.Ld + (need_ld ? pid : 0u));  // .w is always 0 (k_clear, k_resolve): xyz only
         const V3 rd = ld3f4(a.p.ray_d + (need_rd ? pid : 0u));
-        const float4 n0 = a.p.nee0[need_nee ? pid : 0u], n1 = a.p.nee1[need_nee ? pid : 0u];
+        const float4 n0 = ld_s(a.p.nee0 + (need_nee ? pid : 0u)), n1 = ld_s(a.p.nee1 + (need_nee ? pid : 0u));
         const uchar2 vv = reinterpret_cast<const uchar2*>(a.p.vis)[need_nee ? pid : 0u];
         bool dead = (fl & F_DEAD) != 0;
         const uint32_t spp = (uint32_t)a.spp;
@@ -627,12 +671,12 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             if (need_ld && (__float_as_uint(film.x) != __float_as_uint(ld4.x) ||
                             __float_as_uint(film.y) != __float_as_uint(ld4.y) ||
                             __float_as_uint(film.z) != __float_as_uint(ld4.z)))
-                a.p.Ld[pid] = f4(film, 0.f);
+                st_s(a.p.Ld + pid, f4(film, 0.f));
             if (terminate) {  // :199-204
                 dead = true;
                 samples++;
                 sidx += (uint32_t)a.slots;
-                a.p.samples[pid] = samples;
+                st_s(a.p.samples + pid, samples);
             } else {
                 cont = true;
                 cont_len = len;
@@ -648,8 +692,8 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             gen_ray(a.cam, a.W, a.H, x, y, r0, new_o, new_d);
             // beta = (1,1,1) (:245) is implied by len 1: k_shade does not load it for len-1 paths
             nflags = (1u << F_LEN_SHIFT) | (sidx << F_SIDX_SHIFT);
-            a.p.ray_o[pid] = f4(new_o, 0.f);
-            a.p.ray_d[pid] = f4(new_d, 0.f);
+            st_s(a.p.ray_o + pid, f4(new_o, 0.f));
+            st_s(a.p.ray_d + pid, f4(new_d, 0.f));
             gen_ext = true;
             if (ray_misses_scene(sc, new_o, new_d)) {  // resolved here: isect stays "not found"
                 a.p.hit_tri[pid] = -1;
@@ -657,7 +701,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
                 gen_trivial = true;
             }
         }
-        if (!cont && nflags != fl) a.p.flags[pid] = nflags;  // continuing paths: written by material()
+        if (!cont && nflags != fl) st_s(a.p.flags + pid, nflags);  // continuing paths: written by material()
         finished = dead && !(sidx < spp);
     }
     // ---- pushes: generated extension rays and continuing paths (material queue); one
@@ -673,8 +717,8 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         if (gen_ext) a.ext_q[shard * a.ext_cap + slot[0]] = pid;
         if (cont) {
             const uint32_t qi = shard * a.ext_cap + slot[1];
-            a.mat_rec[qi] = make_uint4(pid, pix, cont_sidx | (cont_len << kRecLenShift), (uint32_t)cont_htri);
-            a.mat_beta[qi] = f4(beta_store, 0.f);
+            st_s(a.mat_rec + qi, make_uint4(pid, pix, cont_sidx | (cont_len << kRecLenShift), (uint32_t)cont_htri));
+            st_s(a.mat_beta + qi, f4(beta_store, 0.f));
         }
     }
     uint32_t n_ext = (gen_ext || gen_trivial) ? 1u : 0u;  // queued + resolved-in-place rays
@@ -739,8 +783,8 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a_k
         uint32_t mpid = 0;
         bool occ_l = false, occ_b = false, try_l = false, try_b = false;  // resolved by / tested against the occluder cache
         if (i < n) {
-            const uint4 q = a.mat_rec[shard * a.ext_cap + i];  // {pid, pixel, sample index | len << 24, hit_tri}
-            const float4 b4 = a.mat_beta[shard * a.ext_cap + i];
+            const uint4 q = ld_s(a.mat_rec + shard * a.ext_cap + i);  // {pid, pixel, sample index | len << 24, hit_tri}
+            const float4 b4 = ld_s(a.mat_beta + shard * a.ext_cap + i);
             mpid = q.x;
             mo = material<FIXED>(a, mpid, q.y, q.z & ((1u << kRecLenShift) - 1u), q.z >> kRecLenShift, xyz(b4),
                                  (int32_t)q.w, &s_any[0][0], occ_on);
@@ -990,6 +1034,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     // test and hit; the any-hit set's share is attributed per ray (tot_n1 -= tot_n when an
     // any-hit ray starts, += when it finishes), so a step costs one add.
     uint32_t tot_n = 0, tot_t = 0, tot_h = 0, tot_n1 = 0, tot_t1 = 0, tot_h1 = 0;
+    uint32_t ph[kPhaseWords] = {};  // loop-phase counts (kCount only; wave-uniform)
     uint64_t drained = 0;  // partitions this wave saw run dry (by an atomic: never stale)
     for (;;) {  // one trip per partition joined
     // Per-lane ray state is declared per partition trip: when the trip ends no lane holds a
@@ -1073,6 +1118,10 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             const uint32_t p0 = buf_lo;
             const uint32_t take = min(nidle, buf_hi - buf_lo);
             buf_lo += take;
+            if constexpr (kCount) {
+                ph[PH_REFILLS]++;
+                ph[PH_REFILL_LANES] += take;
+            }
             const uint32_t q = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             const uint32_t pos = p0 + q;  // meaningful on idle lanes
@@ -1139,11 +1188,19 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             if (!more && buf_lo >= buf_hi) break;  // partition drained, every lane idle
             continue;
         }
+        uint32_t itc = 0;  // node steps this lane took in this trip (kCount)
+        if constexpr (kCount) {
+            ph[PH_TRIPS]++;
+            ph[PH_TRIP_NODE] += (uint32_t)__popcll(__ballot(act && ref >= 0));
+            ph[PH_TRIP_LEAF] += (uint32_t)__popcll(__ballot(act && leaf != kEnd));
+            ph[PH_TRIP_IDLE] += (uint32_t)__popcll(__ballot(!act));
+        }
         // ---- node phase: up to kNodeSteps child-pair tests per lane holding an
         // interior node (amortises the per-trip bookkeeping over several steps)
         if (act) {
 #pragma unroll 1
           for (int it = 0; it < kNodeSteps; it++) {
+            if constexpr (kCount) itc++;
             bool need_pop = false;
             if (ref >= 0) {
               if constexpr (kCount) tot_n++;
@@ -1251,11 +1308,20 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             if (ref < 0) break;  // parked-leaf slot full or traversal done: wait for the triangle phase
           }
         }
+        if constexpr (kCount) {  // the node phase ran as many wave iterations as its busiest lane
+            uint32_t m = itc;
+            for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+            ph[PH_NODE_ITERS] += m;
+        }
         // ---- triangle phase (wave-uniform): when enough lanes have a parked
         // leaf, or no lane has node work left, each parked leaf tests one triangle
         const uint32_t n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
         const uint32_t n_node = (uint32_t)__popcll(__ballot(act && ref >= 0));
         if (n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node)) {
+            if constexpr (kCount) {
+                ph[PH_TRI_PHASES]++;
+                ph[PH_TRI_LANES] += n_tri;
+            }
             if (leaf != kEnd) {
                 if constexpr (kCount) tot_t++;
                 const int id = leaf & 0xffffff;
@@ -1317,6 +1383,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     if constexpr (kCount) {
         wave_stats(a.set[0].stats, lane, tot_n - tot_n1, tot_t - tot_t1, tot_h - tot_h1);
         wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);
+        if (a.phase && lane == 0) {
+            uint32_t* pw = a.phase + (blockIdx.x % kShards) * C_WORDS;
+#pragma unroll
+            for (int k = 0; k < kPhaseWords; k++)
+                if (ph[k]) atomicAdd(pw + k, ph[k]);
+        }
     }
 }
 
@@ -1456,6 +1528,13 @@ __global__ void k_accumulate(CounterBlock* c, uint32_t nparts, uint32_t* occ_gat
         for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
     if (__ballot(short_part) != 0 && t == 0) c->trace_short += 1;
     if (t < kMaxParts) c->grab[t][0] = 0;  // k_trace chunk hand-out counters
+    uint32_t phw[kPhaseWords];  // k_trace loop-phase counts (counting build; zero otherwise)
+#pragma unroll
+    for (int k = 0; k < kPhaseWords; k++) {
+        phw[k] = c->shard[t][C_PH + k];
+        c->shard[t][C_PH + k] = 0;
+        for (int off = 32; off > 0; off >>= 1) phw[k] += __shfl_xor(phw[k], off);
+    }
     uint32_t er = c->shard[t][C_EXT_RAYS], ar = c->shard[t][C_ANY_RAYS], oc = c->shard[t][C_OCC],
              ot = c->shard[t][C_OCC_TRY];
     c->shard[t][C_EXT_RAYS] = 0;
@@ -1493,6 +1572,7 @@ __global__ void k_accumulate(CounterBlock* c, uint32_t nparts, uint32_t* occ_gat
         c->last_live = er;
         if (er == 0) c->idle = 1;  // no path alive and none generated: every later iteration is a no-op
         for (int k = 0; k < 6; k++) c->tot_stats[k] += v[C_STATS + k];
+        for (int k = 0; k < kPhaseWords; k++) c->tot_phase[k] += phw[k];
     }
 }
 
@@ -1681,7 +1761,7 @@ int wave_times(unsigned long long* out, int n) {
     (void)n;
     return 0;
 }
-int trace_profile(unsigned long long* out, int reset) {
+int trace_profile(unsigned long long* out, int reset) {  // (replaced by the counting build's phase counts)
     (void)out;
     (void)reset;
     return 0;

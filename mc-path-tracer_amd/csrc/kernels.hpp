@@ -130,8 +130,22 @@ struct DevPaths {
 constexpr int kShards = 64;
 constexpr int kMaxParts = kShards;  // k_trace work partitions (at most one per queue shard)
 enum : int { C_EXT = 0, C_ANY = 1, C_VIS = 2, C_STATS = 3, C_EXT_RAYS = 9, C_ANY_RAYS = 10, C_MAT = 11, C_OCC = 12,
-              C_OCC_TRY = 13, C_WORDS = 32 };  // C_STATS..+5; C_OCC / C_OCC_TRY: any-hit rays resolved by /
-                                               // tested against the occluder cache
+              C_OCC_TRY = 13, C_PH = 14, C_WORDS = 32 };  // C_STATS..+5; C_OCC / C_OCC_TRY: any-hit rays resolved by /
+                                                          // tested against the occluder cache; C_PH..+kPhaseWords-1:
+                                                          // k_trace's loop-phase counts (counting build, PH_*)
+// k_trace loop-phase counts of the counting instantiation (mcpt_debug_trace_profile), per wave summed:
+enum : int {
+    PH_TRIPS = 0,          // loop trips with a ray in the wave
+    PH_REFILLS = 1,        // refill events
+    PH_REFILL_LANES = 2,   // lanes handed a ray by them
+    PH_NODE_ITERS = 3,     // node-phase wave iterations (per trip: the most steps any lane took, <= kNodeSteps)
+    PH_TRI_PHASES = 4,     // triangle phases run
+    PH_TRI_LANES = 5,      // lanes that tested a triangle in them
+    PH_TRIP_NODE = 6,      // lanes with node work at a trip's start
+    PH_TRIP_LEAF = 7,      // lanes holding a parked leaf at a trip's start
+    PH_TRIP_IDLE = 8,      // lanes without a ray at a trip's start (after the refill)
+    kPhaseWords = 9
+};
 struct CounterBlock {
     uint32_t shard[kShards][C_WORDS];  // [0] ext pushes [1] any-hit pushes [2] vis rays [3..8] traversal stats [9,10] rays [11] material pushes
     uint32_t last_ext, last_live;
@@ -144,6 +158,7 @@ struct CounterBlock {
     unsigned long long tot_ext, tot_any, tot_vis, tot_occ;
     unsigned long long tot_stats[6];
     unsigned long long tot_ext_q, tot_any_q;  // rays queued to k_trace (the rest were resolved in place)
+    unsigned long long tot_phase[kPhaseWords];  // k_trace loop-phase counts (PH_*; counting build only)
 };
 
 struct ShadeArgs {
@@ -206,6 +221,7 @@ struct TraceArgs {
     uint32_t* grab;             // nparts chunk counters, C_WORDS apart, zero at launch (k_accumulate resets)
     const uint32_t* idle;       // optional: nonzero = the tile set is complete, exit at once (CounterBlock::idle)
     int tiny_stack;             // host side: launch the kLdsStackTiny instantiation (mcpt_debug_tiny_lds_stack)
+    uint32_t* phase;            // counting build: loop-phase counts of shard s at phase[s * C_WORDS + PH_*] (or nullptr)
 };
 
 struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; int32_t* scene_tri; uint32_t n; };

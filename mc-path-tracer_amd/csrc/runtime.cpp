@@ -93,6 +93,7 @@ struct mcpt_ctx {
     bool env_guides = false;        // env_cell uses the search guides
     int gpu_bvh_builder = MCPT_GPU_BVH_PLOC;  // mcpt_set_gpu_bvh_builder
     bool tiny_stack = false;  // mcpt_debug_tiny_lds_stack: k_trace with a 2-entry LDS stack (tests)
+    unsigned long long phase_base[kPhaseWords] = {};  // mcpt_debug_trace_profile's reset point
 };
 
 static int set_err(mcpt_ctx* c, int rc, const std::string& msg) {
@@ -863,6 +864,7 @@ int mcpt_film_clear(mcpt_ctx* c) {
     HIPCHK(c, hipMemsetAsync(c->cnt, 0, sizeof(CounterBlock), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     memset(&c->totals, 0, sizeof(c->totals));  // the counters are now zero on the device too
+    memset(c->phase_base, 0, sizeof(c->phase_base));
     c->totals_ok = true;
     return MCPT_OK;
 }
@@ -1068,6 +1070,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     v.stats = c->count_work ? &c->cnt->shard[0][C_STATS + 3] : nullptr;
     v.prefiltered = 1;
     v.ray_at_slot = 1;  // k_material stores the any-hit rays at their queue positions
+    ta.phase = c->count_work ? &c->cnt->shard[0][C_PH] : nullptr;  // loop-phase counts (mcpt_debug_trace_profile)
     ta.hit_tri = c->p.hit_tri;
     ta.vis = c->p.vis;
     ta.grab = &c->cnt->grab[0][0];  // reset by k_accumulate below
@@ -1847,13 +1850,16 @@ int mcpt_debug_hbm_copy(mcpt_ctx* c, uint64_t bytes, uint32_t iters, double* gbp
     return rc;
 }
 
-int mcpt_debug_trace_profile(mcpt_ctx* c, uint64_t* out8, int reset) {  // out8: 12 words
-    if (!c || !out8) return MCPT_E_INVALID;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    unsigned long long v[12] = {};
-    int n = trace_profile(v, reset);
-    for (int i = 0; i < 12; i++) out8[i] = v[i];
-    return n;
+// k_trace's loop-phase counts (PH_*, counting build: mcpt_set_work_counters on) since the last film
+// clear or reset, from the host copy of the counters the last call left: returns kPhaseWords
+int mcpt_debug_trace_profile(mcpt_ctx* c, uint64_t* out12, int reset) {
+    if (!c || !out12) return MCPT_E_INVALID;
+    for (int i = 0; i < 12; i++) out12[i] = 0;
+    if (!c->totals_ok) return 0;
+    for (int i = 0; i < kPhaseWords; i++) out12[i] = c->totals.tot_phase[i] - c->phase_base[i];
+    if (reset)
+        for (int i = 0; i < kPhaseWords; i++) c->phase_base[i] = c->totals.tot_phase[i];
+    return kPhaseWords;
 }
 // Diagnostics builds (-DMCPT_WAVE_TIMES) only, not part of mcpt.h: entry / exit s_memrealtime (100 MHz)
 // stamps of the last k_trace launch's first n waves (out: 4n words: entry, exit, partition,

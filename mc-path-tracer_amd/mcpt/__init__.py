@@ -570,11 +570,12 @@ class PathTracer:
         self._ck(lib().mcpt_film_write_pfm(self.h, os.fsencode(path)))
 
     def trace_profile(self, reset=True):
-        """k_trace loop profile (diagnostics build only): dict of summed wave-level counts."""
+        """k_trace loop-phase counts of the counting build (mcpt_debug_trace_profile; work counters on)
+        since the last film clear or reset, as a dict of wave-summed counts (None: none recorded)."""
         v = (C.c_uint64 * 12)()
         n = lib().mcpt_debug_trace_profile(self.h, v, int(reset))
-        names = ("trips", "refills", "node_lanes", "tri_phases", "tri_lanes", "finish_trips", "idle_lanes",
-                 "pop_trips", "pop_lanes", "slow_slab_trips", "finish_lanes", "_11")
+        names = ("trips", "refills", "refill_lanes", "node_iters", "tri_phases", "tri_lanes", "trip_node_lanes",
+                 "trip_leaf_lanes", "trip_idle_lanes")
         return {k: int(x) for k, x in zip(names, v)} if n > 0 else None
 
     def hbm_copy_gbps(self, nbytes=1 << 30, iters=20) -> float:
@@ -653,7 +654,9 @@ def write_pfm(path, rgb):
 # traces ~14% faster than BVHAccel's single-axis 12-bucket SAH; films are identical for any tree.
 DEFAULT_BVH = dict(builder="sah3", buckets=128, trav_cost=0.5, isect_cost=1.0, max_prims=8)
 # A/B knobs for the builder's cost model (films do not depend on the tree)
-for _k, _env, _t in (("trav_cost", "MCPT_BVH_TRAV_COST", float), ("max_prims", "MCPT_BVH_MAX_PRIMS", int)):
+for _k, _env, _t in (("trav_cost", "MCPT_BVH_TRAV_COST", float), ("max_prims", "MCPT_BVH_MAX_PRIMS", int),
+                     ("builder", "MCPT_BVH_BUILDER", str), ("buckets", "MCPT_BVH_BUCKETS", int),
+                     ("isect_cost", "MCPT_BVH_ISECT_COST", float)):
     if os.environ.get(_env):
         DEFAULT_BVH[_k] = _t(os.environ[_env])
 
@@ -662,8 +665,8 @@ def build_config_scene(cid: int, asset_dir=ASSET_DIR, **build_kw) -> Scene:
     """BASELINE config cid's proxy scene, built with DEFAULT_BVH (or ``builder="reference"``, ...)."""
     s = Scene()
     s.make_proxy(cid, asset_dir)
-    if build_kw.get("builder") == "reference":
-        s.build(max_prims=build_kw.get("max_prims", 8))
+    if (DEFAULT_BVH | build_kw).get("builder") == "reference":
+        s.build(max_prims=(DEFAULT_BVH | build_kw).get("max_prims", 8))
     else:
         s.build(**(DEFAULT_BVH | build_kw))
     return s
