@@ -66,10 +66,18 @@ __device__ inline V3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
 // Path-state streams of the shading kernels (k_shade, k_material): every word is touched once per
 // kernel and iteration, over a state many times the L2 and MALL, so MCPT_NT marks these loads (bit
 // 1) and stores (bit 2) non-temporal -- streaming, not retained -- for the env tables, BVH and
-// occluder records to keep the caches (A/B knob; 0 = ordinary accesses).
+// occluder records to keep the caches.  Bit 4: k_trace's ray loads and result stores too; bit 8:
+// the queue entries and staged any-hit rays the shading kernels store.  Measured (config 2 / 3,
+// interleaved, two rounds): loads and stores (3) shade stage 144.6 -> 138.4 ms / 107.5 -> 101.4 ms
+// per frame, stores alone (2) nearly as good, loads alone (1) 0.5-3 % slower.
 #ifndef MCPT_NT
-#define MCPT_NT 0
+#define MCPT_NT 3
 #endif
+template <class T>
+__device__ inline void st_q(T* p, T v) {  // queue entries (MCPT_NT bit 8)
+    if constexpr (MCPT_NT & 8) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 typedef float f4v_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
 template <class T>
@@ -158,6 +166,9 @@ __device__ inline bool slab(float mnx, float mny, float mnz, float mxx, float mx
     return !miss;
 }
 constexpr float K_INF_F = __builtin_huge_valf();
+#ifndef MCPT_OCC_LAYOUT
+#define MCPT_OCC_LAYOUT 0  // occluder-table key order (occ_index): 0 origin-cell major, 1 direction-bin major
+#endif
 constexpr int kEnd = -1;  // not a valid leaf: offset + count <= ntri < 2^24
 
 // Culling scale of a ray (mcpt_core.hpp "conservative box culling"): iota = max_a |1/d_a| (1 + 2^-18)
@@ -314,7 +325,13 @@ __device__ inline uint32_t occ_index(const DevScene& sc, V3 o, V3 d) {
     const uint32_t G = (uint32_t)sc.occ_g, B = (uint32_t)sc.occ_b;
     // one table cell per key (hashing the keys into a 2^21- or 2^23-cell table measured 43 % / 60 %
     // of config 2's any-hit rays resolved against 72 % direct: the keys that occur collide heavily)
+#if MCPT_OCC_LAYOUT == 1
+    // direction major: lanes whose rays share a direction bin and lie in neighbouring origin cells
+    // (along x) read one 128-B line (A/B knob)
+    return (((face * B + ub) * B + vb) * G + cz) * G * G + cy * G + cx;
+#else
     return ((((cz * G + cy) * G + cx) * 6u + face) * B + ub) * B + vb;
+#endif
 }
 
 // true: (o, d) (reciprocal inv, all finite; signed culling scale io) is occluded by the triangle of
@@ -335,9 +352,18 @@ __device__ inline bool occ_test(V3 o, V3 d, V3 inv, float io, float4 bmn, float4
     return tri_test_t(o, d, v3(bmx.w, r2.x, r2.y), v3(r2.z, r2.w, r3.x), v3(r3.y, r3.z, r3.w), th) && !(th < 0.f) &&
            th < K_HUGE;
 }
-// The cell's entries of (o, d): kOccWays triangle records (k_trace writes way tri mod kOccWays)
+// The cell's entries of (o, d): kOccWays triangle records (k_trace writes way tri mod kOccWays).
+// MCPT_NT bit 16: the table's random 8-B reads and the occluder stores are non-temporal (the 96 MB
+// table cannot stay in L2; its lines would evict the env tables' and occluder records').
 __device__ inline uint2 occ_entry(const DevScene& sc, V3 o, V3 d) {
-    return reinterpret_cast<const uint2*>(sc.occ)[occ_index(sc, o, d)];
+    const uint2* e = reinterpret_cast<const uint2*>(sc.occ) + occ_index(sc, o, d);
+    if constexpr (MCPT_NT & 16) {
+        typedef uint32_t u2v_t __attribute__((ext_vector_type(2)));
+        const u2v_t v = __builtin_nontemporal_load(reinterpret_cast<const u2v_t*>(e));
+        return make_uint2(v.x, v.y);
+    } else {
+        return *e;
+    }
 }
 // An any-hit ray against its cell's entries: both candidates' occluder records (leaf box, margin
 // and triangle in one aligned 64-B record: one half line each, where the leaf box and the 48-B
@@ -714,7 +740,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         uint32_t* ctr[2] = {sc_ctr + C_EXT, sc_ctr + C_MAT};
         uint32_t slot[2], total[2];
         block_push<2>(want, ctr, slot, total);
-        if (gen_ext) a.ext_q[shard * a.ext_cap + slot[0]] = pid;
+        if (gen_ext) st_q(a.ext_q + shard * a.ext_cap + slot[0], pid);
         if (cont) {
             const uint32_t qi = shard * a.ext_cap + slot[1];
             st_s(a.mat_rec + qi, make_uint4(pid, pix, cont_sidx | (cont_len << kRecLenShift), (uint32_t)cont_htri));
@@ -815,18 +841,28 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a_k
         uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
         uint32_t slot[3], total[3];
         block_push<3>(want, ctr, slot, total);
-        if (mo.want_ext) a.ext_q[shard * a.ext_cap + slot[0]] = mpid;
+        if (mo.want_ext) st_q(a.ext_q + shard * a.ext_cap + slot[0], mpid);
         if (mo.want_l) {
             const uint32_t k = shard * a.any_cap + slot[1];
-            a.any_q[k] = 2 * mpid;
-            a.p.sray_o[k] = s_any[0][threadIdx.x];
-            a.p.sray_d[k] = s_any[1][threadIdx.x];
+            st_q(a.any_q + k, 2 * mpid);
+            if constexpr (MCPT_NT & 8) {
+                st_s(a.p.sray_o + k, s_any[0][threadIdx.x]);
+                st_s(a.p.sray_d + k, s_any[1][threadIdx.x]);
+            } else {
+                a.p.sray_o[k] = s_any[0][threadIdx.x];
+                a.p.sray_d[k] = s_any[1][threadIdx.x];
+            }
         }
         if (mo.want_b) {
             const uint32_t k = shard * a.any_cap + slot[2];
-            a.any_q[k] = 2 * mpid + 1;
-            a.p.sray_o[k] = s_any[2][threadIdx.x];
-            a.p.sray_d[k] = s_any[3][threadIdx.x];
+            st_q(a.any_q + k, 2 * mpid + 1);
+            if constexpr (MCPT_NT & 8) {
+                st_s(a.p.sray_o + k, s_any[2][threadIdx.x]);
+                st_s(a.p.sray_d + k, s_any[3][threadIdx.x]);
+            } else {
+                a.p.sray_o[k] = s_any[2][threadIdx.x];
+                a.p.sray_d[k] = s_any[3][threadIdx.x];
+            }
         }
         // per-wave ray counts from lane masks (wave-uniform scalars: no registers held across the
         // next trip's material())
@@ -916,6 +952,20 @@ constexpr int kGrabMax = MCPT_GRAB_MAX;  // rays one hand-out atomic may reserve
 #define MCPT_ANY_FIRST 0
 #endif
 constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
+// Leaves a lane may hold before it must wait for the triangle phase: the parked-leaf register plus
+// MCPT_LEAF_BUF - 1 entries in LDS ([entry][lane]; their count rides in bits 27-28 of the parked
+// leaf's encoding, which references never use).  1 = the register only.
+#ifndef MCPT_LEAF_BUF
+#define MCPT_LEAF_BUF 1
+#endif
+constexpr int kLeafBuf = MCPT_LEAF_BUF;
+static_assert(kLeafBuf >= 1 && kLeafBuf <= 4, "leaf buffer: 1..4");
+// Triangle phase repeated (one more triangle per lane) while at least this many lanes still hold
+// a leaf (0: once per trip).
+#ifndef MCPT_TRI_REPEAT
+#define MCPT_TRI_REPEAT 0
+#endif
+constexpr int kTriRepeat = MCPT_TRI_REPEAT;
 
 // Waves per SIMD: 7 (<= 72 VGPRs) for child pairs with either LDS stack, 6 (80) for 4-wide nodes
 // (8 float4 of node data per step).  The attribute lets the register allocator park the
@@ -942,6 +992,7 @@ template <int kW, int kLdsStack, bool kCount>
 __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs a) {
     if (a.idle && *a.idle) return;  // the tile set is complete
     __shared__ int2 stk[kLdsStack][kTraceBlock];
+    __shared__ int s_leaf[kLeafBuf > 1 ? kLeafBuf - 1 : 1][kTraceBlock];
     const int lane = threadIdx.x;
     // ---- work distribution.  The queue shards are split into nparts partitions
     // (shard s -> partition s mod nparts; by default one per XCD) and each partition's
@@ -1077,11 +1128,16 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             }
         }
         if (kind) {
-            a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
-            if (tri >= 0 && occ_rec)  // the cell's occluder (occ_hit1)
-                sc.occ[(size_t)occ_index(sc, o, d) * kOccWays + (uint32_t)tri % kOccWays] = (uint32_t)tri;
+            if constexpr (MCPT_NT & 4) __builtin_nontemporal_store((uint8_t)(tri < 0), a.vis + rid);
+            else a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
+            if (tri >= 0 && occ_rec) {  // the cell's occluder (occ_hit1)
+                uint32_t* w = sc.occ + (size_t)occ_index(sc, o, d) * kOccWays + (uint32_t)tri % kOccWays;
+                if constexpr (MCPT_NT & 16) __builtin_nontemporal_store((uint32_t)tri, w);
+                else *w = (uint32_t)tri;
+            }
         } else {
-            a.hit_tri[rid] = tri;  // hit record rebuilt by the consumer (hit_record())
+            if constexpr (MCPT_NT & 4) __builtin_nontemporal_store(tri, a.hit_tri + rid);
+            else a.hit_tri[rid] = tri;  // hit record rebuilt by the consumer (hit_record())
         }
         act = false;
     };
@@ -1145,9 +1201,18 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     // a dense set (ray_at_slot: the any-hit rays k_material stores at their queue
                     // positions) issues its ray loads with the queue-entry load, not after it
                     const bool at_slot = kind ? a.set[1].ray_at_slot : a.set[0].ray_at_slot;
-                    rid = at_slot ? qslot : (qp ? qp[qslot] : qslot);
-                    const float4 o4 = rop[rid], d4 = rdp[rid];
-                    if (at_slot && qp) rid = qp[qslot];  // the result index, needed only when the ray finishes
+                    float4 o4, d4;
+                    if constexpr (MCPT_NT & 4) {
+                        rid = at_slot ? qslot : (qp ? __builtin_nontemporal_load(qp + qslot) : qslot);
+                        o4 = ld_s(rop + rid);
+                        d4 = ld_s(rdp + rid);
+                        if (at_slot && qp) rid = __builtin_nontemporal_load(qp + qslot);  // the result index
+                    } else {
+                        rid = at_slot ? qslot : (qp ? qp[qslot] : qslot);
+                        o4 = rop[rid];
+                        d4 = rdp[rid];
+                        if (at_slot && qp) rid = qp[qslot];  // the result index, needed only when the ray finishes
+                    }
                     o = xyz(o4);
                     d = xyz(d4);
                     tri = -1;
@@ -1300,9 +1365,18 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             }
             // a reached leaf is parked in the lane's leaf slot and traversal
             // continues speculatively with the next stack entry
-            if (!need_pop && ref < 0 && ref != kEnd && leaf == kEnd) {
-                leaf = ref;
-                need_pop = true;
+            if (!need_pop && ref < 0 && ref != kEnd) {
+                if (leaf == kEnd) {
+                    leaf = ref;
+                    need_pop = true;
+                } else if constexpr (kLeafBuf > 1) {  // the slot is taken: the lane's LDS entries
+                    const int nb = (leaf >> 27) & 3;
+                    if (nb < kLeafBuf - 1) {
+                        s_leaf[nb][lane] = ref;
+                        leaf += 1 << 27;
+                        need_pop = true;
+                    }
+                }
             }
             if (need_pop) ref = pop();
             if (ref < 0) break;  // parked-leaf slot full or traversal done: wait for the triangle phase
@@ -1315,9 +1389,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         }
         // ---- triangle phase (wave-uniform): when enough lanes have a parked
         // leaf, or no lane has node work left, each parked leaf tests one triangle
-        const uint32_t n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
+        uint32_t n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
         const uint32_t n_node = (uint32_t)__popcll(__ballot(act && ref >= 0));
-        if (n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node)) {
+        for (bool run = n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node); run;) {
             if constexpr (kCount) {
                 ph[PH_TRI_PHASES]++;
                 ph[PH_TRI_LANES] += n_tri;
@@ -1350,12 +1424,22 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                         cut = best * __builtin_fmaf(__builtin_fabsf(io), sc.cull_p, kCullSlackF);
                     }
                 }
-                if (done) {  // any hit: drop the rest of the traversal
+                if (done) {  // any hit: drop the rest of the traversal (and the buffered leaves)
                     leaf = kEnd;
                     ref = kEnd;
+                } else if ((leaf & 0x07000000) != 0) {
+                    leaf = leaf + 1 - (1 << 24);  // offset + 1, count - 1
+                } else if constexpr (kLeafBuf > 1) {  // the next buffered leaf, if any
+                    const int nb = (leaf >> 27) & 3;
+                    leaf = nb ? (s_leaf[nb - 1][lane] | ((nb - 1) << 27)) : kEnd;
                 } else {
-                    leaf = (leaf & 0x07000000) == 0 ? kEnd : leaf + 1 - (1 << 24);  // offset + 1, count - 1
+                    leaf = kEnd;
                 }
+            }
+            run = false;
+            if constexpr (kTriRepeat > 0) {
+                n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
+                run = n_tri >= (uint32_t)kTriRepeat;
             }
         }
         if (act && ref == kEnd && leaf == kEnd) finish();

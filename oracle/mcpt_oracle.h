@@ -140,7 +140,8 @@ const char *or_version(void);
  * culls nothing, 1 the round-3 rule, 2 the round-4 rule; tri = closest triangle id or -1,
  * t = its t, visible = any-hit result; *nodes = boxes tested. */
 int32_t or_model_margins(const or_scene *sc, float *node_w, float *tri_w, float *p);
-void or_model_set_safe(double c); /* mode 6 margins (0: the product's) */
+void or_model_set_safe(double c); /* modes 6 / 7: margins and planes (0: the product's) */
+uint64_t or_model_tri_tests(void); /* triangle tests of the last or_model_trace call */
 void or_model_trace(const or_scene *sc, int32_t n, const float *ro, const float *rd, int32_t mode,
                     const float *node_w, const float *tri_w, float p, int32_t *tri, float *t, uint8_t *visible,
                     uint64_t *nodes);

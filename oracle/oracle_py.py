@@ -76,6 +76,7 @@ def lib():
             "or_version": (C.c_char_p, []),
             "or_model_margins": (C.c_int32, [C.POINTER(OrScene), _f, _f, _f]),
             "or_model_set_safe": (None, [C.c_double]),
+            "or_model_tri_tests": (C.c_uint64, []),
             "or_model_trace": (None, [C.POINTER(OrScene), C.c_int32, _f, _f, C.c_int32, _f, _f, C.c_float, _i, _f,
                                       C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)]),
         }
@@ -224,11 +225,13 @@ def model_margins(arrays, safe_c=0.0):
     return {"node_w": nw, "tri_w": tw, "p": float(p[0]), "contained": bool(ok)}
 
 
-def model_trace(arrays, ro, rd, mode, margins=None, nthreads=1):
+def model_trace(arrays, ro, rd, mode, margins=None, nthreads=1, safe_c=0.0):
     """trav_model.c: closest (triangle id, t) and any-hit visibility under culling rule `mode`
-    (0 none, 1 round 3, 2 round 4, 6 round-5 candidate with safe-ray margins) and the number of
-    boxes tested.  nthreads > 1 splits the rays over threads (not for mode 6: its safe-ray switch is
-    module state)."""
+    (0 none, 1 round 3, 2 round 4, 6 safe-ray margins with unsafe rays unculled, 7 the product's
+    dual tree: safe rays on safe-ray margins, unsafe rays on the general ones -- margins["node_w"] /
+    ["tri_w"] then hold the general then the safe values, model_margins_dual) and the number of
+    boxes tested.  Modes 6 / 7 classify rays by the planes at safe_c.  nthreads > 1 splits the rays
+    over threads (not for modes 6 / 7: the safe-ray switch is module state)."""
     s = scene_struct(arrays)
     m = margins or model_margins(arrays)
     ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
@@ -245,8 +248,28 @@ def model_trace(arrays, ro, rd, mode, margins=None, nthreads=1):
                              vis[i0:i1].ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(nodes))
         return int(nodes.value)
 
-    boxes = sum(_chunks(n, 1 if mode == 6 else nthreads, run))
+    if mode in (6, 7):
+        lib().or_model_set_safe(float(safe_c))
+    try:
+        boxes = sum(_chunks(n, 1 if mode in (6, 7) else nthreads, run))
+    finally:
+        lib().or_model_set_safe(0.0)
     return tri, t, vis, boxes
+
+
+def model_tri_tests():
+    """Triangle tests of the last single-threaded model_trace call (both kinds of its rays)."""
+    return int(lib().or_model_tri_tests())
+
+
+def model_margins_dual(arrays, safe_c):
+    """Mode 7's margins: the general ones followed by the safe-ray ones (P of the latter, which is
+    the larger)."""
+    g = model_margins(arrays)
+    s = model_margins(arrays, safe_c=safe_c)
+    return {"node_w": np.concatenate([g["node_w"], s["node_w"]]), "tri_w": np.concatenate([g["tri_w"], s["tri_w"]]),
+            "p": max(g["p"], s["p"]), "contained": g["contained"] and s["contained"], "p_general": g["p"],
+            "p_safe": s["p"]}
 
 
 def env_build(tex: np.ndarray):

@@ -225,6 +225,11 @@ static int m_keep(int mode, float t0, float t1, float w, const mray *r, float cu
 
 static int tri_key(const or_scene *sc, int id) { return sc->tri_id ? sc->tri_id[id] : id; }
 
+/* triangle tests of the last or_model_trace call (its rays, both kinds): work counts for the
+ * culling variants (single-threaded callers only) */
+static uint64_t g_tri_tests = 0;
+uint64_t or_model_tri_tests(void) { return g_tri_tests; }
+
 /* kind 0: closest hit (index, t), kind 1: any hit (1 = occluded) */
 static int m_trace(const or_scene *sc, int mode, const float *node_w, const float *tri_w, float pg, mv3 o, mv3 d,
                    int kind, float *tout, uint64_t *nodes) {
@@ -272,6 +277,7 @@ static int m_trace(const or_scene *sc, int mode, const float *node_w, const floa
                     if (!(m_box(mn, mx, &r, &t0, &t1) && m_keep(mode, t0, t1, tri_w[id], &r, cut, &key))) continue;
                 }
                 float t;
+                g_tri_tests++;
                 if (m_tri(sc, id, o, d, &t) && !(t < 0.f)) {
                     if (kind) {
                         if (t < M_HUGE) { *tout = t; return 1; }
@@ -318,10 +324,11 @@ void or_model_trace(const or_scene *sc, int32_t n, const float *ro, const float 
                     const float *node_w, const float *tri_w, float p, int32_t *tri, float *t, uint8_t *visible,
                     uint64_t *nodes) {
     uint64_t nn = 0;
-    /* mode 6: the planes of the triangles the general bound leaves unbounded (n as float, thr) */
+    g_tri_tests = 0;
+    /* modes 6 / 7: the planes of the triangles the general bound leaves unbounded (n as float, thr) */
     int np = 0;
     float *pl = NULL;
-    if (mode == 6) {
+    if (mode == 6 || mode == 7) {
         pl = malloc(sizeof(float) * 4 * (size_t)(sc->ntri > 0 ? sc->ntri : 1));
         for (int t = 0; t < sc->ntri; t++) {
             mv3 p0 = mld(sc->v0, t), e1 = msub(mld(sc->v1, t), p0), e2 = msub(mld(sc->v2, t), p0);
@@ -351,17 +358,26 @@ void or_model_trace(const or_scene *sc, int32_t n, const float *ro, const float 
         mv3 o = mld(ro, i), d = mld(rd, i);
         float tb;
         int rmode = mode;
-        if (mode == 6) {
-            rmode = 2;
-            for (int k = 0; k < np; k++) {
+        const float *nw = node_w, *tw = tri_w;
+        if (mode == 6 || mode == 7) {
+            /* mode 6: unsafe rays (within the threshold of an unbounded triangle's plane) are not
+             * culled at all; mode 7 (the product's dual tree): they take the general margins
+             * (node_w / tri_w first halves), safe rays the safe-ray margins (second halves) */
+            int unsafe = 0;
+            for (int k = 0; k < np && !unsafe; k++) {
                 const float g = (d.x * pl[4 * k] + d.y * pl[4 * k + 1]) + d.z * pl[4 * k + 2];
-                if (!(fabsf(g) >= pl[4 * k + 3])) { rmode = 0; break; }
+                if (!(fabsf(g) >= pl[4 * k + 3])) unsafe = 1;
+            }
+            rmode = mode == 6 && unsafe ? 0 : 2;
+            if (mode == 7 && !unsafe) {
+                nw = node_w + (sc->nnodes > 0 ? sc->nnodes : 1);
+                tw = tri_w + (sc->ntri > 0 ? sc->ntri : 1);
             }
         }
-        const int id = m_trace(sc, rmode, node_w, tri_w, p, o, d, 0, &tb, &nn);
+        const int id = m_trace(sc, rmode, nw, tw, p, o, d, 0, &tb, &nn);
         tri[i] = id >= 0 ? tri_key(sc, id) : -1;
         t[i] = tb;
-        visible[i] = (uint8_t)!m_trace(sc, rmode, node_w, tri_w, p, o, d, 1, &tb, &nn);
+        visible[i] = (uint8_t)!m_trace(sc, rmode, nw, tw, p, o, d, 1, &tb, &nn);
     }
     free(pl);
     *nodes = nn;

@@ -377,7 +377,7 @@ def test_safe_ray_margins_model_equals_reference(oracle, adv_scenes, name, scale
     pos_t, _, _ = oracle.trace_closest(a, ro, rd)
     m6 = oracle.model_margins(a, safe_c=SAFE_C)
     assert np.isfinite(m6["tri_w"][big[:10]]).all()  # the walls are bounded for safe rays
-    tri, t, vis, boxes6 = oracle.model_trace(a, ro, rd, 6, m6)
+    tri, t, vis, boxes6 = oracle.model_trace(a, ro, rd, 6, m6, safe_c=SAFE_C)
     assert np.array_equal(tri, otri), f"{(tri != otri).sum()} closest hits differ"
     assert np.array_equal(t.view(np.uint32), pos_t[:, 3].view(np.uint32))
     assert np.array_equal(vis, ovis), f"{(vis != ovis).sum()} visibilities differ"

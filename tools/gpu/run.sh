@@ -4,7 +4,7 @@
 #
 #   bash tools/gpu/run.sh test smoke bench kstats pmc partition
 #
-#   test       python -m pytest tests -m gpu (TEST_ARGS adds pytest arguments)
+#   test       python -m pytest tests -m gpu (TEST_ARGS adds pytest arguments, TEST_K a -k expression)
 #   smoke      __graft_entry__.smoke()
 #   bench      bench.py $BENCH_ARGS                      -> gpurun_out/bench_$TAG.json
 #   kstats     rocprofv3 --kernel-trace --stats of bench  -> gpurun_out/kt_$TAG/ (profiled runs pass
@@ -35,7 +35,7 @@ fail() { echo "step $1 failed"; tail -${2:-30} "$3"; exit 1; }
 for step in "$@"; do
   case $step in
   test)
-    timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread ${TEST_ARGS} \
+    timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread ${TEST_ARGS} ${TEST_K:+-k "$TEST_K"} \
       > $O/test.log 2>&1 || { grep -E "FAILED|Error|differ" $O/test.log | head -20; fail test 5 $O/test.log; }
     grep -E "passed|failed" $O/test.log | tail -1 ;;
   smoke)
@@ -89,8 +89,10 @@ PY
       for e in "${envs[@]}"; do
         env $e timeout -k 10 300 python -u bench.py $BARGS > $O/abenv.json 2> $O/abenv.err || fail abenv 20 $O/abenv.err
         python3 -c "
-import json; d = json.load(open('$O/abenv.json')); r = d['roofline']
-print('$e'.ljust(30), round(d['value'], 1), 'Mray/s', d['ms_per_step'], 'ms/frame trace', r['avg_launch_ms'], 'shade', d['stage_ms_per_step']['k_shade+k_material'])"
+import json; d = json.load(open('$O/abenv.json')); r = d['roofline']; p = r['per_ray']
+print('$e'.ljust(30), round(d['value'], 1), 'Mray/s', d['ms_per_step'], 'ms/frame trace', r['avg_launch_ms'], 'shade',
+      d['stage_ms_per_step']['k_shade+k_material'], 'ext nodes/tests', p['ext_pair_nodes'], p['ext_tri_tests'],
+      'any', p['any_pair_nodes'], p['any_tri_tests'])"
       done
     done ;;
   partition)
