@@ -274,10 +274,6 @@ int mcpt_debug_env_tables(mcpt_ctx *ctx, float *marginal_y, float *conds_y, floa
  * 2 breadth-first (default 2 for trees of <= 2 MiB of nodes, else 0; MCPT_SIBLING_LAYOUT=0/1/2
  * at upload forces one; inputs that are not a tree -- a shared child -- always get 0). */
 int mcpt_debug_node_layout(const mcpt_ctx *ctx);
-/* Walls the traversal tests ahead of the tree at each ray's start (the root child holding only
- * triangles without a culling margin, e.g. config 2's walls; MCPT_WALLS=0 at upload: none):
- * their count, 0 when the uploaded scene has no such set. */
-int mcpt_debug_wall_set(const mcpt_ctx *ctx);
 /* any-hit occluder cache: any-hit rays resolved by it since the film was
  * last cleared (counted in shadow_rays / vis_rays as traced rays; they skip the traversal), and
  * whether the uploaded scene has the cache (MCPT_OCC_G=0 at upload turns it off). */

@@ -882,37 +882,6 @@ MCPT_HD double cull_tri_margin(V3 e1, V3 e2, double* far, bool plane = true) {
     *far = (b > 0.0 ? beta + b : beta) * (1.0 + 1.0 / 512.0) / den * kCullSlackD * (1.0 + 1.0 / 1048576.0);
     return (omega + beta * diam * (1.0 + 1e-12)) * kCullSlackD / den;
 }
-// Back-facing skip for one triangle (k_trace's wall pre-pass, kernels.hip wall_prepass).  The
-// reference accepts a triangle only if its fp32 det D = dot(e1, cross(d, e2)) is >= 1e-6f
-// (Triangle.cu:17-21), and |D - D*| <= 5.0001 u sum_a |e1_a| (|d_b e2_c| + |d_c e2_b|) <=
-// 7.0712 u |e1| |e2| |d| (the dot-of-cross bound of the culling section), with D* = d . m,
-// m = e2 x e1.  So an accepted ray has d . m^ >= (1e-6f - 7.0712 u |e1| |e2| |d|) / |m|.  The
-// kernel evaluates g = fl(d . n) with n = m^ rounded to float: |g - d . m^| <= 3.0001 u |d| |n| +
-// |d| |n - m^|.  With |d| <= 1 + 2^-10, the triangle is provably rejected when g < tau,
-//   tau = (1e-6f - 7.0712 u |e1| |e2| (1 + 2^-10)) / |m| - (1 + 2^-10) (|n - m^| + 3.0002 u |n|),
-// rounded down; -inf for a degenerate triangle.  n (float) in nf, tau returned.
-MCPT_HD float cull_back_tau(V3 e1, V3 e2, float nf[3]) {
-    const double a[3] = {e1.x, e1.y, e1.z}, b[3] = {e2.x, e2.y, e2.z};
-    const double m[3] = {b[1] * a[2] - b[2] * a[1], b[2] * a[0] - b[0] * a[2], b[0] * a[1] - b[1] * a[0]};
-    const double mm = __builtin_sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
-    nf[0] = nf[1] = nf[2] = 0.f;
-    if (!(mm > 0.0) || !(mm < 1e300)) return -__builtin_huge_valf();
-    double dn = 0.0, nn = 0.0;
-    for (int k = 0; k < 3; k++) {
-        nf[k] = (float)(m[k] / mm);
-        const double e = (double)nf[k] - m[k] / mm;
-        dn += e * e;
-        nn += (double)nf[k] * nf[k];
-    }
-    const double n1 = cull_norm(e1), n2 = cull_norm(e2);
-    const double fd = 1.0 + 1.0 / 1024.0;
-    double tau = ((double)K_EPSILON - 7.0712 * kCullU * n1 * n2 * fd) / mm -
-                 fd * (__builtin_sqrt(dn) * (1.0 + 1e-6) + 1e-30 + 3.0002 * kCullU * __builtin_sqrt(nn));
-    tau -= __builtin_fabs(tau) * 1e-9 + 1e-30;  // the double evaluation's own rounding
-    float t = (float)tau;
-    if ((double)t > tau) t = __builtin_nextafterf(t, -__builtin_huge_valf());
-    return t;
-}
 MCPT_HD bool cull_tri_unbounded(V3 e1, V3 e2, bool plane = true) {
     double far;
     return !(cull_tri_margin(e1, e2, &far, plane) < __builtin_huge_val());

@@ -952,20 +952,6 @@ constexpr int kGrabMax = MCPT_GRAB_MAX;  // rays one hand-out atomic may reserve
 #define MCPT_ANY_FIRST 0
 #endif
 constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
-// Leaves a lane may hold before it must wait for the triangle phase: the parked-leaf register plus
-// MCPT_LEAF_BUF - 1 entries in LDS ([entry][lane]; their count rides in bits 27-28 of the parked
-// leaf's encoding, which references never use).  1 = the register only.
-#ifndef MCPT_LEAF_BUF
-#define MCPT_LEAF_BUF 1
-#endif
-constexpr int kLeafBuf = MCPT_LEAF_BUF;
-static_assert(kLeafBuf >= 1 && kLeafBuf <= 4, "leaf buffer: 1..4");
-// Triangle phase repeated (one more triangle per lane) while at least this many lanes still hold
-// a leaf (0: once per trip).
-#ifndef MCPT_TRI_REPEAT
-#define MCPT_TRI_REPEAT 0
-#endif
-constexpr int kTriRepeat = MCPT_TRI_REPEAT;
 
 // Waves per SIMD: 7 (<= 72 VGPRs) for child pairs with either LDS stack, 6 (80) for 4-wide nodes
 // (8 float4 of node data per step).  The attribute lets the register allocator park the
@@ -992,7 +978,6 @@ template <int kW, int kLdsStack, bool kCount>
 __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs a) {
     if (a.idle && *a.idle) return;  // the tile set is complete
     __shared__ int2 stk[kLdsStack][kTraceBlock];
-    __shared__ int s_leaf[kLeafBuf > 1 ? kLeafBuf - 1 : 1][kTraceBlock];
     const int lane = threadIdx.x;
     // ---- work distribution.  The queue shards are split into nparts partitions
     // (shard s -> partition s mod nparts; by default one per XCD) and each partition's
@@ -1009,7 +994,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     // of a launch finishing anywhere between 52 % and 100 % of its duration
     // (tools/wave_times.py).
     const uint32_t nsh = (uint32_t)a.nshards, nparts = a.nparts;
-    const uint32_t nw = kW == 2 ? a.nwalls : 0u;  // the wall set (TraceArgs::walls), tested ahead of the traversal
     uint32_t home = 0;
     if (nparts > 1) {
         uint32_t xcc;
@@ -1093,7 +1077,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     // ray, so none of it is live across the partition scan below (VGPR budget).
     uint32_t buf_lo = 0, buf_hi = 0, last_p = 0;  // wave-uniform reservation of the partition (refill)
     bool act = false;
-    bool fresh = false;  // the lane's ray started this trip (the wall pre-pass runs for it)
     uint32_t rid = 0;
     V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
     int ref = kEnd, leaf = kEnd, sp = 0, tri = -1;
@@ -1142,58 +1125,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             else a.hit_tri[rid] = tri;  // hit record rebuilt by the consumer (hit_record())
         }
         act = false;
-    };
-    // The wall set ahead of the traversal (TraceArgs::walls).  A starting ray is tested against
-    // every wall whose own box its line crosses: the leaf test the walls' isolated subtree would
-    // make (an own box passing implies its ancestors', by containment), with no cull (their margins
-    // are +inf) -- except the walls the ray provably meets from behind (fl(d . n) < tau:
-    // cull_back_tau), which the reference's det test would reject.  best / tri / cut as the triangle
-    // phase updates them; true: an any-hit ray found its occluder.  The wall data are uniform and
-    // come with the kernel arguments, so the loop issues scalar loads only (the round-4 pre-pass
-    // loaded them per lane, ten dependent round trips per refill, and was slower than the subtree).
-    auto wall_prepass = [&]() -> bool {
-        const bool fin = __builtin_fabsf(io) < K_INF_F;
-        const bool bf = sc.cull_ok && (d.x * d.x + d.y * d.y + d.z * d.z) <= kCullNormMax;
-        const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;
-        bool done = false;
-#pragma unroll 1
-        for (uint32_t k = 0; k < nw; k++) {
-            const float4* W = kernarg_fresh<TraceArgs>().walls + kWallF4 * k;
-            const float4 A = W[0], B = W[1], N = W[2];
-            if (done || (bf && (d.x * N.x + d.y * N.y) + d.z * N.z < A.w)) continue;
-            bool hit;
-            if (fin) {  // pair_slab's arithmetic for one box
-                const float ax = (A.x - o.x) * inv.x, bx = (B.x - o.x) * inv.x;
-                const float ay = (A.y - o.y) * inv.y, by = (B.y - o.y) * inv.y;
-                const float az = (A.z - o.z) * inv.z, bz = (B.z - o.z) * inv.z;
-                const float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax, bx), __builtin_fminf(ay, by)),
-                                                 __builtin_fminf(az, bz));
-                const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by)),
-                                                 __builtin_fmaxf(az, bz));
-                hit = t0 <= t1;
-            } else {
-                float t0, t1;
-                hit = slab(A.x, A.y, A.z, B.x, B.y, B.z, o, inv, nx, ny, nz, t0, t1);
-            }
-            if (!hit) continue;
-            if constexpr (kCount) tot_t++;
-            const float4 P = W[3], Q = W[4], R = W[5];
-            float t;
-            if (!tri_test_t(o, d, v3(P.x, P.y, P.z), v3(P.w, Q.x, Q.y), v3(Q.z, Q.w, R.x), t) || t < 0.f) continue;
-            const int id = __float_as_int(B.w);
-            if (best < 0.f) {
-                if (t < K_HUGE) {
-                    tri = id;  // occluded (tmax 1e32)
-                    done = true;
-                }
-            } else if (t < best ||
-                       (t == best && tri >= 0 && __float_as_int(N.w) < __float_as_int(sc.tri[kTriF4 * tri + 2].y))) {
-                best = t;
-                tri = id;
-                cut = best * __builtin_fmaf(__builtin_fabsf(io), sc.cull_p, kCullSlackF);
-            }
-        }
-        return done;
     };
     for (;;) {
         // ---- refill idle lanes with the partition's next rays
@@ -1297,20 +1228,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                                            t0, t1) ||
                                      !keep_box(t0, t1, sc.root_w * io, cut, key)))
                             finish();
-                        else {
-                            ref = sc.root_ref;  // (the wall set's other child when nw > 0)
-                            fresh = true;
-                        }
+                        else
+                            ref = sc.root_ref;
                     }
                 }
             }
         }
-        if constexpr (kW == 2) {  // the rays that started this trip meet the wall set first
-            if (nw && __ballot(fresh) != 0) {
-                if (fresh && wall_prepass()) finish();
-            }
-        }
-        fresh = false;
         if (__ballot(act) == 0) {
             if (!more && buf_lo >= buf_hi) break;  // partition drained, every lane idle
             continue;
@@ -1431,13 +1354,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 if (leaf == kEnd) {
                     leaf = ref;
                     need_pop = true;
-                } else if constexpr (kLeafBuf > 1) {  // the slot is taken: the lane's LDS entries
-                    const int nb = (leaf >> 27) & 3;
-                    if (nb < kLeafBuf - 1) {
-                        s_leaf[nb][lane] = ref;
-                        leaf += 1 << 27;
-                        need_pop = true;
-                    }
                 }
             }
             if (need_pop) ref = pop();
@@ -1451,9 +1367,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         }
         // ---- triangle phase (wave-uniform): when enough lanes have a parked
         // leaf, or no lane has node work left, each parked leaf tests one triangle
-        uint32_t n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
+        const uint32_t n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
         const uint32_t n_node = (uint32_t)__popcll(__ballot(act && ref >= 0));
-        for (bool run = n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node); run;) {
+        if (n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node)) {
             if constexpr (kCount) {
                 ph[PH_TRI_PHASES]++;
                 ph[PH_TRI_LANES] += n_tri;
@@ -1486,22 +1402,14 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                         cut = best * __builtin_fmaf(__builtin_fabsf(io), sc.cull_p, kCullSlackF);
                     }
                 }
-                if (done) {  // any hit: drop the rest of the traversal (and the buffered leaves)
+                if (done) {  // any hit: drop the rest of the traversal
                     leaf = kEnd;
                     ref = kEnd;
                 } else if ((leaf & 0x07000000) != 0) {
                     leaf = leaf + 1 - (1 << 24);  // offset + 1, count - 1
-                } else if constexpr (kLeafBuf > 1) {  // the next buffered leaf, if any
-                    const int nb = (leaf >> 27) & 3;
-                    leaf = nb ? (s_leaf[nb - 1][lane] | ((nb - 1) << 27)) : kEnd;
                 } else {
                     leaf = kEnd;
                 }
-            }
-            run = false;
-            if constexpr (kTriRepeat > 0) {
-                n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
-                run = n_tri >= (uint32_t)kTriRepeat;
             }
         }
         if (act && ref == kEnd && leaf == kEnd) finish();

@@ -208,19 +208,8 @@ struct TraceSet {
     int ray_at_slot;            // 1: the ray of queue position k is ro/rd[k] (dense); queue[k] is only the
                                 //    result index.  0: the ray is ro/rd[queue[k]]
 };
-// The wall set (k_trace's pre-pass, kernels.hip wall_prepass): when one child of the root holds
-// only unbounded triangles (no culling margin: config 2's walls, isolated there by the host SAH
-// builder) and at most kMaxWalls of them, k_trace tests them at each ray's start -- skipping the
-// ones the ray provably meets from behind -- and starts the traversal at the root's other child
-// (DevScene::root_ref).  Per wall, kWallF4 float4 in the kernel arguments (scalar loads):
-// {own box mn, back-face tau} {own box mx, record index bits} {n, scene id bits} {v0, e1.x}
-// {e1.yz, e2.xy} {e2.z, 0, 0, 0}.
-constexpr int kMaxWalls = 16;
-constexpr int kWallF4 = 6;
 struct TraceArgs {
     DevScene scene;
-    uint32_t nwalls;            // 0: no wall pre-pass (the traversal starts at the whole tree's root)
-    float4 walls[kMaxWalls * kWallF4];
     TraceSet set[2];            // [0] closest hit -> hit_tri, [1] any hit -> vis
     int nshards;
     int32_t* hit_tri;           // closest-hit output: triangle index or -1

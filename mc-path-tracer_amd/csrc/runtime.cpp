@@ -93,10 +93,6 @@ struct mcpt_ctx {
     bool env_guides = false;        // env_cell uses the search guides
     int gpu_bvh_builder = MCPT_GPU_BVH_PLOC;  // mcpt_set_gpu_bvh_builder
     bool tiny_stack = false;  // mcpt_debug_tiny_lds_stack: k_trace with a 2-entry LDS stack (tests)
-    // the wall set of the uploaded scene (TraceArgs::walls, kernels.hip wall_prepass): nwalls walls,
-    // kWallF4 float4 each; 0: none (the traversal starts at the whole tree's root)
-    uint32_t nwalls = 0;
-    std::vector<float4> walls;
     unsigned long long phase_base[kPhaseWords] = {};  // mcpt_debug_trace_profile's reset point
 };
 
@@ -599,81 +595,6 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         for (int k = 0; k < 3; k++) { s.root_mn[k] = 1.f; s.root_mx[k] = -1.f; }
         s.root_ref = 0;
     }
-    // The wall set (TraceArgs::walls): when one child of the root holds only triangles no box bound
-    // covers (unbounded margins: config 2's walls, which the host SAH builder isolates there) and at
-    // most kMaxWalls of them, k_trace tests them at each ray's start with a back-facing skip
-    // (wall_prepass) and the traversal starts at the root's other child, an interior node.  Needs
-    // child-pair nodes, a host BVH and nested boxes (an own box passing implies its ancestors').
-    // MCPT_WALLS=0 turns it off (A/B; same results).
-    c->nwalls = 0;
-    c->walls.clear();
-    {
-        const char* we = std::getenv("MCPT_WALLS");
-        const char* pl = std::getenv("MCPT_CULL_PLANE");
-        const bool plane = !(pl && pl[0] == '0' && pl[1] == 0);
-        if (!(we && we[0] == '0' && we[1] == 0) && !gpu_bvh && N > 0 && width == 2 && d->nprims[0] == 0 && nest_ok) {
-            std::vector<int> tlo(N), thi(N), tcnt(N);
-            for (int i = N - 1; i >= 0; i--) {  // triangle range and count of every subtree
-                if (d->nprims[i] > 0) {
-                    tlo[i] = d->offset[i];
-                    thi[i] = d->offset[i] + d->nprims[i];
-                    tcnt[i] = d->nprims[i];
-                } else {
-                    const int c0 = i + 1, c1 = d->offset[i];
-                    tlo[i] = std::min(tlo[c0], tlo[c1]);
-                    thi[i] = std::max(thi[c0], thi[c1]);
-                    tcnt[i] = tcnt[c0] + tcnt[c1];
-                }
-            }
-            auto rec = [&](int t, mcpt::V3& v0, mcpt::V3& e1, mcpt::V3& e2) {
-                const float *a0 = d->v0 + 3 * (size_t)t, *a1 = d->v1 + 3 * (size_t)t, *a2 = d->v2 + 3 * (size_t)t;
-                v0 = mcpt::v3(a0[0], a0[1], a0[2]);
-                e1 = mcpt::v3(a1[0] - a0[0], a1[1] - a0[1], a1[2] - a0[2]);  // as the triangle record stores them
-                e2 = mcpt::v3(a2[0] - a0[0], a2[1] - a0[1], a2[2] - a0[2]);
-            };
-            const int ch[2] = {1, d->offset[0]};
-            for (int k = 0; k < 2 && !c->nwalls; k++) {
-                const int cu = ch[k], co = ch[1 - k];
-                // contiguous triangle ranges, few walls, and the traversal's start an interior node
-                if (thi[cu] - tlo[cu] != tcnt[cu] || thi[co] - tlo[co] != tcnt[co] || tcnt[cu] > kMaxWalls ||
-                    tcnt[co] == 0 || d->nprims[co] != 0)
-                    continue;
-                bool all = true;
-                for (int t = tlo[cu]; t < thi[cu] && all; t++) {
-                    mcpt::V3 v0, e1, e2;
-                    rec(t, v0, e1, e2);
-                    all = mcpt::cull_tri_unbounded(e1, e2, plane);
-                }
-                if (!all) continue;
-                std::vector<float4> w;
-                for (int t = tlo[cu]; t < thi[cu]; t++) {
-                    const float* v[3] = {d->v0 + 3 * (size_t)t, d->v1 + 3 * (size_t)t, d->v2 + 3 * (size_t)t};
-                    float mn[3], mx[3];
-                    for (int a = 0; a < 3; a++) {
-                        mn[a] = std::fmin(std::fmin(v[0][a], v[1][a]), v[2][a]);
-                        mx[a] = std::fmax(std::fmax(v[0][a], v[1][a]), v[2][a]);
-                    }
-                    mcpt::V3 v0, e1, e2;
-                    rec(t, v0, e1, e2);
-                    float nf[3];
-                    const float tau = mcpt::cull_back_tau(e1, e2, nf);
-                    const int32_t sid = d->tri_id ? d->tri_id[t] : t;
-                    float ft, fs;
-                    memcpy(&ft, &t, 4);
-                    memcpy(&fs, &sid, 4);
-                    w.push_back(make_float4(mn[0], mn[1], mn[2], tau));
-                    w.push_back(make_float4(mx[0], mx[1], mx[2], ft));
-                    w.push_back(make_float4(nf[0], nf[1], nf[2], fs));
-                    w.push_back(make_float4(v0.x, v0.y, v0.z, e1.x));
-                    w.push_back(make_float4(e1.y, e1.z, e2.x, e2.y));
-                    w.push_back(make_float4(e2.z, 0.f, 0.f, 0.f));
-                }
-                c->walls = w;
-                c->nwalls = (uint32_t)tcnt[cu];
-                s.root_ref = ref_of(co);
-            }
-        }
-    }
     s.env.mode = d->env_mode;
     for (int k = 0; k < 3; k++) s.env.color[k] = d->env_color[k];
     s.env.ls = d->env_ls;
@@ -847,7 +768,6 @@ int mcpt_debug_env_tables(mcpt_ctx* c, float* marginal_y, float* conds_y, float*
     return MCPT_OK;
 }
 int mcpt_debug_node_layout(const mcpt_ctx* c) { return c ? c->node_layout : MCPT_E_INVALID; }
-int mcpt_debug_wall_set(const mcpt_ctx* c) { return c ? (int)c->nwalls : MCPT_E_INVALID; }
 int mcpt_debug_ray_counts(const mcpt_ctx* c, uint64_t* out) {
     if (!c || !out) return MCPT_E_INVALID;
     const CounterBlock& t = c->totals;
@@ -1156,8 +1076,6 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     ta.grab = &c->cnt->grab[0][0];  // reset by k_accumulate below
     ta.idle = &c->cnt->idle;
     ta.tiny_stack = c->tiny_stack ? 1 : 0;
-    ta.nwalls = c->nwalls;
-    if (c->nwalls) memcpy(ta.walls, c->walls.data(), c->walls.size() * sizeof(float4));
     launch_trace(ta, c->geom, c->stream);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 2), c->stream));
     launch_accumulate(c->cnt, c->geom.trace_parts, c->scene.occ ? c->scene.occ_gate : nullptr, c->stream);
@@ -1551,8 +1469,6 @@ int mcpt_stage_run(mcpt_ctx* c, int stage, const mcpt_soa_view* in, mcpt_soa_vie
     ta.grab = &c->cnt->grab[0][0];
     HIPCHK(c, hipEventRecord(ev(c, 0), c->stream));
     ta.tiny_stack = c->tiny_stack ? 1 : 0;
-    ta.nwalls = c->nwalls;
-    if (c->nwalls) memcpy(ta.walls, c->walls.data(), c->walls.size() * sizeof(float4));
     launch_trace(ta, c->geom, c->stream);
     HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
     uint32_t grab0 = 0;  // drain check: the one shard is partition 0's

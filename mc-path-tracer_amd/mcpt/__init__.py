@@ -120,7 +120,6 @@ ABI = {
     "mcpt_set_tiles": (C.c_int, [C.c_void_p, _u, C.c_uint32]),
     "mcpt_set_compact_paths": (C.c_int, [C.c_void_p, C.c_int32]),
     "mcpt_debug_tiny_lds_stack": (C.c_int, [C.c_void_p, C.c_int32]),
-    "mcpt_debug_wall_set": (C.c_int, [C.c_void_p]),
     "mcpt_set_path_slots": (C.c_int, [C.c_void_p, C.c_uint32]),
     "mcpt_set_trace_partitions": (C.c_int, [C.c_void_p, C.c_uint32]),
     "mcpt_gather": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_int32]),
@@ -477,11 +476,6 @@ class PathTracer:
         """Path state over the tile set only (mcpt_set_compact_paths); re-allocates and clears the film.
         In this layout set_tiles re-allocates and clears too."""
         self._ck(lib().mcpt_set_compact_paths(self.h, int(bool(on))))
-
-    @property
-    def wall_set(self) -> int:
-        """Walls k_trace tests ahead of the tree (mcpt_debug_wall_set), 0 when none."""
-        return int(lib().mcpt_debug_wall_set(self.h))
 
     def set_tiny_lds_stack(self, on=True):
         """Tests: the traversal's 2-entry LDS stack instantiation (mcpt_debug_tiny_lds_stack)."""

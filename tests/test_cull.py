@@ -437,46 +437,6 @@ def test_gpu_cull_adversarial(mcpt_mod, oracle, request, name, scale, n):
 
 
 @pytest.mark.gpu
-def test_gpu_wall_prepass_same_results(mcpt_mod, oracle, request):
-    """Config 2's walls (the root child of unbounded triangles) are tested at each ray's start
-    ahead of the tree (kernels.hip wall_prepass, back-facing skip by cull_back_tau) instead of
-    through their subtree: closest hits, t and visibility on adversarial and far-cut rays equal the
-    oracle's with the pre-pass on, and equal the subtree traversal's (MCPT_WALLS=0), bit for bit;
-    so does a config-2 film with path slots."""
-    from adversarial import far_cut_rays
-
-    s, a = _gpu_scene(mcpt_mod, request, "c2", 1.0)
-    ro, rd = adversarial_rays(a, 300000, seed=29)
-    o2, d2 = far_cut_rays(a, 200000, seed=31)
-    ro, rd = np.concatenate([ro, o2]), np.concatenate([rd, d2])
-    _gpu_vs_oracle(mcpt_mod, oracle, s, a, ro, rd)
-    out = {}
-    for walls in ("1", "0"):
-        os.environ["MCPT_WALLS"] = walls
-        try:
-            pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=6, max_depth=5))
-            pt.upload_scene(s)
-        finally:
-            del os.environ["MCPT_WALLS"]
-        nw = pt.wall_set
-        assert nw == (10 if walls == "1" else 0), nw
-        gp, _, gt = pt.trace_closest(ro, rd)
-        gv = pt.trace_any(ro, rd)
-        rc = mcpt_mod.CONFIGS[2]
-        pt.set_camera(mcpt_mod.config_camera(rc, 240, 136))
-        pt.set_path_slots(3)
-        pt.resize(240, 136, 64, 64)
-        st = pt.render()
-        L, smp = pt.film()
-        out[walls] = (gp, gt, gv, L, smp, st.extend_rays + st.shadow_rays + st.vis_rays)
-        pt.close()
-    A, B = out["1"], out["0"]
-    assert np.array_equal(A[0].view(np.uint32), B[0].view(np.uint32)) and np.array_equal(A[1], B[1])
-    assert np.array_equal(A[2], B[2])
-    assert np.array_equal(A[3].view(np.uint32), B[3].view(np.uint32)) and np.array_equal(A[4], B[4]) and A[5] == B[5]
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("name,scale,tiny", GPU_FAR)
 def test_gpu_far_cut_adversarial(mcpt_mod, oracle, request, name, scale, tiny):
     """k_trace on 1 M far-cut rays (tests/adversarial.py far_cut_rays: the grazed triangle bounded,
