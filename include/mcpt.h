@@ -38,7 +38,7 @@ enum {
  * wavefront_kernels.cu: max_depth 5 (:142), rr_depth 3 (:189), spp <= 250 (:124). */
 typedef struct mcpt_config {
     uint64_t seed;       /* keyed RNG seed; default 0x5EED2026 */
-    int32_t spp;         /* samples per pixel (< 2^19): gates processing and new samples */
+    int32_t spp;         /* samples per pixel (<= 2^19 - 256): gates processing and new samples */
     int32_t max_depth;   /* 'path_length > max_depth' terminates */
     int32_t rr_depth;    /* Russian roulette when 'path_length > rr_depth' */
     int32_t tile_w;      /* film tile (Film.cu:17: 256x256) */

@@ -63,6 +63,25 @@ __device__ inline void block_push(const bool (&want)[NQ], uint32_t* const (&coun
 
 __device__ inline V3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
 
+// The kernel's by-value argument struct read through an opaque copy of the kernarg segment
+// pointer.  Kernel arguments are invariant loads, so the compiler hoists every field a persistent
+// loop uses into SGPRs at kernel entry; ShadeArgs' ~60 uniform words then exceed the SGPR file and
+// spill into VGPR lanes (k_material: 78 SGPRs, 76 v_writelane / 281 v_readlane).  Behind the empty
+// asm the pointer is a new value wherever this is called, so the fields are loaded (s_load from the
+// scalar cache) where they are used.  The struct stays in the constant address space: the cast to
+// a generic reference is undone by address-space inference after inlining (scalar loads, no flat).
+// k_material: 128 -> 112 VGPRs, no SGPR spill, shade stage 142.9 -> 141.1 ms per config-2 frame
+// (interleaved A/B, two rounds).  The same re-read per k_trace loop trip removed its 12 SGPR spills
+// but cost 2.52 -> 2.59 ms per launch (scalar-load latency on every trip): not used there.
+template <class T>
+__device__ inline const T& kernarg_fresh() {
+    typedef const __attribute__((address_space(4))) T KT;
+    KT* p = (KT*)__builtin_amdgcn_kernarg_segment_ptr();
+    __asm__ volatile("" : "+s"(p));
+    return *(const T*)p;
+}
+
+
 // Path-state streams of the shading kernels (k_shade, k_material): every word is touched once per
 // kernel and iteration, over a state many times the L2 and MALL, so MCPT_NT marks these loads (bit
 // 1) and stores (bit 2) non-temporal -- streaming, not retained -- for the env tables, BVH and
@@ -561,7 +580,11 @@ __device__ inline void material_brdf_terms(const ShadeArgs& a, uint32_t pid, con
     st_s(a.p.flags + pid, nf);
 }
 
-#ifdef MCPT_SHADE_WPE
+// k_shade: 8 waves per SIMD (<= 64 VGPRs; the virtual-block loop left alone allocates 67, no spill at 64)
+#ifndef MCPT_SHADE_WPE
+#define MCPT_SHADE_WPE 8
+#endif
+#if MCPT_SHADE_WPE > 0
 #define MCPT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(MCPT_SHADE_WPE, MCPT_SHADE_WPE)))
 #else
 #define MCPT_SHADE_ATTR
@@ -574,27 +597,31 @@ __device__ inline void material_brdf_terms(const ShadeArgs& a, uint32_t pid, con
 #else
 #define MCPT_MAT_ATTR
 #endif
+// Finished-block flag of shading block vb (k_shade's virtual block: kBlock consecutive pixels of
+// one path slot and tile), kept per slot, film tile and block, so it outlives a change of tile set
+__device__ inline uint32_t shade_done_idx(const ShadeArgs& a, int vb) {
+    const int bpt = (a.tile_w * a.tile_h + kBlock - 1) / kBlock;
+    const int per_slot = a.ntiles * bpt;
+    const int slot = a.slots > 1 ? vb / per_slot : 0;
+    const int bs = vb - slot * per_slot;
+    const int tile = bs / bpt;
+    const int2 t = a.tiles[tile];
+    const uint32_t ntx = (uint32_t)((a.W + a.tile_w - 1) / a.tile_w), nty = (uint32_t)((a.H + a.tile_h - 1) / a.tile_h);
+    return (((uint32_t)slot * nty + (uint32_t)t.y) * ntx + (uint32_t)t.x) * (uint32_t)bpt + (uint32_t)(bs - tile * bpt);
+}
+
+// One shading block: logic + generate for kBlock pixels of a path slot, then the block's pushes.
 template <bool FIXED>
-__global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
-    if (a.cnt->idle) return;  // the tile set is complete (an earlier iteration of the call traced no ray)
+__device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeArgs& a, int vb, uint32_t done_idx) {
     const DevScene& sc = a.scene;
     const int tile_px = a.tile_w * a.tile_h;
     const int bpt = (tile_px + kBlock - 1) / kBlock;
     // path slots: blocks [k * ntiles * bpt, (k + 1) * ntiles * bpt) run slot k of every pixel
     const int per_slot = a.ntiles * bpt;
-    const int slot = a.slots > 1 ? (int)blockIdx.x / per_slot : 0;
-    const int bs = (int)blockIdx.x - slot * per_slot;
+    const int slot = a.slots > 1 ? vb / per_slot : 0;
+    const int bs = vb - slot * per_slot;
     const int tile = bs / bpt;
     const int li = (bs - tile * bpt) * kBlock + threadIdx.x;
-    // A block whose paths have all finished their last sample stays so until the film is
-    // cleared: its logic would load their state and change nothing, so it returns here.
-    uint32_t done_idx = 0;
-    if (a.blk_done) {
-        const int2 t = a.tiles[tile];
-        const uint32_t ntx = (uint32_t)((a.W + a.tile_w - 1) / a.tile_w), nty = (uint32_t)((a.H + a.tile_h - 1) / a.tile_h);
-        done_idx = (((uint32_t)slot * nty + (uint32_t)t.y) * ntx + (uint32_t)t.x) * (uint32_t)bpt + (uint32_t)(bs - tile * bpt);
-        if (a.blk_done[done_idx]) return;
-    }
     const int lane = threadIdx.x & 63;
     bool valid = tile < a.ntiles && li < tile_px;
     uint32_t pid = 0, pix = 0;  // path id (slot * pixels + pixel) and pixel id
@@ -629,7 +656,6 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         // primary miss, the MIS terms and visibility for len > 1) at pid when needed
         // and at a shared dummy index 0 otherwise (no extra bandwidth).
         const uint32_t fl = ld_s(a.p.flags + pid);
-        uint32_t samples = ld_s(a.p.samples + pid);
         const int32_t htri = ld_s(a.p.hit_tri + pid);
         const float4 b4 = ld_s(a.p.beta + ((((fl >> F_LEN_SHIFT) & 0xffu) > 1u) ? pid : 0u));  // len 1: beta is (1,1,1), not loaded
         const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
@@ -646,9 +672,12 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
         const uchar2 vv = reinterpret_cast<const uchar2*>(a.p.vis)[need_nee ? pid : 0u];
         bool dead = (fl & F_DEAD) != 0;
         const uint32_t spp = (uint32_t)a.spp;
-        // this slot's sample index (slot k runs samples k, k + S, ...; S = 1: the count itself),
-        // kept in the flags word from generation on (k_material keys its draws with it)
-        uint32_t sidx = (uint32_t)slot + (uint32_t)a.slots * samples;
+        // this slot's sample index (slot k runs samples k, k + S, ...; S = 1: the count itself):
+        // the flags word carries it, the one in progress for a live path (k_material keys its
+        // draws with it) and the next one for a dead path (k_clear: the slot's first), so the
+        // film's sample count is (sidx - slot) / S and its stream is only written
+        uint32_t sidx = fl >> F_SIDX_SHIFT;
+        uint32_t samples = a.slots > 1 ? (sidx - (uint32_t)slot) / (uint32_t)a.slots : sidx;
         if (!dead && sidx < spp) {  // wavefront_kernels.cu:124
             const Rng r{rng_key(a.seed, pix, sidx), len};
             const bool found = htri >= 0;
@@ -711,7 +740,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
             }
         }
         uint32_t nflags = fl;
-        if (dead) nflags = F_DEAD;
+        if (dead) nflags = F_DEAD | (sidx << F_SIDX_SHIFT);
         if (dead && sidx < spp) {  // :219-222 + wf_generate (:225-251)
             const Rng r0{rng_key(a.seed, pix, sidx), 0u};
             V3 new_o, new_d;
@@ -733,7 +762,7 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     // ---- pushes: generated extension rays and continuing paths (material queue); one
     // atomic per block and queue.  A continuing path's record and updated throughput go
     // to k_material densely (it writes p.beta with f_s/pdf_s in .w).
-    const int shard = blockIdx.x % kShards;
+    const int shard = vb % kShards;  // the queues' capacity assumes <= kBlock pushes per block and shard
     uint32_t* sc_ctr = a.cnt->shard[shard];
     {
         bool want[2] = {gen_ext, cont};
@@ -761,6 +790,44 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     if (a.blk_done && __syncthreads_and(finished ? 1 : 0) && threadIdx.x == 0) a.blk_done[done_idx] = 1;
 }
 
+// k_shade: a bounded grid of G blocks; block b runs shading blocks b, b + G, b + 2G, ... (at most
+// kBlock of them: launch_shade sizes G).  A block whose paths have all finished their last sample
+// stays so until the film is cleared, so it is skipped: thread k reads the flag of the block's k-th
+// shading block, all in one round trip, and the block loops over the live ones.  A one-pass grid
+// (one workgroup per shading block, G = the block count) paid ~0.2 ms per launch just to dispatch
+// and retire config 2's 246K workgroups once they had all finished (the frame's last ~20
+// iterations; 64 iterations per frame).
+template <bool FIXED>
+__global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
+    if (a.cnt->idle) return;  // the tile set is complete (an earlier iteration of the call traced no ray)
+    __shared__ uint64_t s_live[kBlock / 64];
+    const uint32_t G = gridDim.x, nvb = a.shade_vblocks;
+    const uint32_t mine = (nvb - blockIdx.x + G - 1) / G;  // <= kBlock
+    const uint32_t k = threadIdx.x;
+    bool live = false;
+    uint32_t didx = 0;
+    if (k < mine) {
+        const int vb = (int)(blockIdx.x + k * G);
+        if (a.blk_done) {
+            didx = shade_done_idx(a, vb);
+            live = a.blk_done[didx] == 0;
+        } else {
+            live = true;
+        }
+    }
+    const uint64_t m = __ballot(live);
+    if ((threadIdx.x & 63) == 0) s_live[threadIdx.x >> 6] = m;
+    __shared__ uint32_t s_didx[kBlock];
+    s_didx[k] = didx;
+    __syncthreads();
+    for (uint32_t j = 0; j < mine; j++) {
+        if (!((s_live[j >> 6] >> (j & 63)) & 1ull)) continue;
+        // the arguments re-read per shading block (kernarg_fresh): hoisted out of the loop, the
+        // struct's fields took the SGPR file and spilled (89 SGPRs, 54 -> 86 VGPRs)
+        shade_vblock<FIXED>(kernarg_fresh<ShadeArgs>(), (int)(blockIdx.x + j * G), s_didx[j]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // k_material: light choice + wf_mat_mix (wavefront_kernels.cu:207-215, 295-375) for
 // the paths k_shade found continuing, dense over the material queue: 256 paths per
@@ -768,24 +835,6 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
 // pushes meet at the barrier together.  Block b serves shard b mod kShards, chunks
 // b / kShards, + gridDim.x / kShards, ... of it (grid from the occupancy calculator).
 // ---------------------------------------------------------------------------
-// The kernel's by-value argument struct read through an opaque copy of the kernarg segment
-// pointer.  Kernel arguments are invariant loads, so the compiler hoists every field a persistent
-// loop uses into SGPRs at kernel entry; ShadeArgs' ~60 uniform words then exceed the SGPR file and
-// spill into VGPR lanes (k_material: 78 SGPRs, 76 v_writelane / 281 v_readlane).  Behind the empty
-// asm the pointer is a new value wherever this is called, so the fields are loaded (s_load from the
-// scalar cache) where they are used.  The struct stays in the constant address space: the cast to
-// a generic reference is undone by address-space inference after inlining (scalar loads, no flat).
-// k_material: 128 -> 112 VGPRs, no SGPR spill, shade stage 142.9 -> 141.1 ms per config-2 frame
-// (interleaved A/B, two rounds).  The same re-read per k_trace loop trip removed its 12 SGPR spills
-// but cost 2.52 -> 2.59 ms per launch (scalar-load latency on every trip): not used there.
-template <class T>
-__device__ inline const T& kernarg_fresh() {
-    typedef const __attribute__((address_space(4))) T KT;
-    KT* p = (KT*)__builtin_amdgcn_kernarg_segment_ptr();
-    __asm__ volatile("" : "+s"(p));
-    return *(const T*)p;
-}
-
 template <bool FIXED>
 __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a_kernarg) {
     (void)a_kernarg;  // read through kernarg_fresh (the same bytes: it is the kernel's only argument)
@@ -952,6 +1001,14 @@ constexpr int kGrabMax = MCPT_GRAB_MAX;  // rays one hand-out atomic may reserve
 #define MCPT_ANY_FIRST 0
 #endif
 constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
+// A trip's node phase ends for every lane once fewer than this many lanes still have node work
+// (0: each lane takes its kNodeSteps steps): per node width, MCPT_NODE_MIN_LANES2 / 4.
+#ifndef MCPT_NODE_MIN_LANES2
+#define MCPT_NODE_MIN_LANES2 0
+#endif
+#ifndef MCPT_NODE_MIN_LANES4
+#define MCPT_NODE_MIN_LANES4 0
+#endif
 
 // Waves per SIMD: 7 (<= 72 VGPRs) for child pairs with either LDS stack, 6 (80) for 4-wide nodes
 // (8 float4 of node data per step).  The attribute lets the register allocator park the
@@ -1358,6 +1415,11 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             }
             if (need_pop) ref = pop();
             if (ref < 0) break;  // parked-leaf slot full or traversal done: wait for the triangle phase
+            // the node phase ends for every lane once fewer than kNodeMin still have node work
+            // (they resume next trip, after the triangle phase and a refill)
+            constexpr int kNodeMin = kW == 4 ? MCPT_NODE_MIN_LANES4 : MCPT_NODE_MIN_LANES2;
+            if constexpr (kNodeMin > 0)
+                if ((uint32_t)__popcll(__ballot(true)) < (uint32_t)kNodeMin) break;
           }
         }
         if constexpr (kCount) {  // the node phase ran as many wave iterations as its busiest lane
@@ -1511,7 +1573,7 @@ __global__ void k_hit_record(HitRecordArgs a) {  // stage_run(EXTEND) outputs
 __global__ void k_clear(ClearArgs a) {  // g_clear_dfilm (wavefront_kernels.cu:55-66)
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
-    a.flags[i] = F_DEAD;
+    a.flags[i] = F_DEAD | ((i / a.npx) << F_SIDX_SHIFT);  // dead, next sample: the slot's first
     a.samples[i] = 0;
     a.Ld[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
@@ -1681,7 +1743,7 @@ static uint32_t env_u32(const char* name, int def, int lo, int hi) {
 //    0.777 for the 72-VGPR build at 28.  MCPT_TRACE_WAVES caps the waves per CU.
 //  * k_trace partitions: two per XCD, MCPT_TRACE_PARTS overrides.
 int launch_geometry(int dev, LaunchGeom& g) {
-    int cus = 0, nx = 1, per_cu = 0, mat0 = 0, mat1 = 0;
+    int cus = 0, nx = 1, per_cu = 0, mat0 = 0, mat1 = 0, sh0 = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
     if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess) nx = 1;
     int occ[2][2] = {};  // [width 2 / 4][LDS stack 8 / deep]
@@ -1690,7 +1752,8 @@ int launch_geometry(int dev, LaunchGeom& g) {
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1][0], k_trace<4, kLdsStack, false>, kTraceBlock, 0) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1][1], k_trace<4, kLdsStackDeep, false>, kTraceBlock, 0) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat0, k_material<false>, kBlock, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat1, k_material<true>, kBlock, 0) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&mat1, k_material<true>, kBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&sh0, k_shade<false>, kBlock, 0) != hipSuccess)
         return -1;
     if (cus <= 0) cus = 256;
     per_cu = 32;
@@ -1709,25 +1772,40 @@ int launch_geometry(int dev, LaunchGeom& g) {
     }
     g.mat_blocks[0] = (uint32_t)std::max(1, cus * std::max(1, mat0) / kShards) * (uint32_t)kShards;
     g.mat_blocks[1] = (uint32_t)std::max(1, cus * std::max(1, mat1) / kShards) * (uint32_t)kShards;
+    // k_shade grid: MCPT_SHADE_GRID times the resident blocks (0: one workgroup per shading block)
+    g.shade_grid = (uint32_t)std::max(1, cus * std::max(1, sh0)) * env_u32("MCPT_SHADE_GRID", 16, 0, 1024);
+    if (getenv("MCPT_SHADE_WGS")) g.shade_grid = env_u32("MCPT_SHADE_WGS", 0, 1, 1 << 30);  // tests: an absolute cap
     g.refill_min = env_u32("MCPT_REFILL_MIN", 0, 0, 64);  // 0: per instantiation (launch_trace)
     g.tri_min = env_u32("MCPT_TRI_MIN", 16, 0, 64);
     return 0;
 }
-void launch_shade(const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fixed_mode, hipStream_t s) {
+// k_shade's grid: nblocks shading blocks over at most g.shade_grid workgroups, and never fewer
+// than nblocks / kBlock (a workgroup reads its blocks' done flags one per thread)
+static uint32_t shade_grid(uint32_t nblocks, const LaunchGeom& g) {
+    uint32_t G = g.shade_grid ? std::min(nblocks, g.shade_grid) : nblocks;
+    return std::max(G, (nblocks + kBlock - 1) / kBlock);
+}
+void launch_shade(const ShadeArgs& args, int nblocks, const LaunchGeom& g, bool fixed_mode, hipStream_t s) {
+    ShadeArgs a = args;
+    a.shade_vblocks = (uint32_t)nblocks;
+    const uint32_t G = shade_grid((uint32_t)nblocks, g);
     if (fixed_mode) {
-        hipLaunchKernelGGL(k_shade<true>, dim3(nblocks), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(k_shade<true>, dim3(G), dim3(kBlock), 0, s, a);
         hipLaunchKernelGGL(k_material<true>, dim3(g.mat_blocks[1]), dim3(kBlock), 0, s, a);
     } else {
-        hipLaunchKernelGGL(k_shade<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(k_shade<false>, dim3(G), dim3(kBlock), 0, s, a);
         hipLaunchKernelGGL(k_material<false>, dim3(g.mat_blocks[0]), dim3(kBlock), 0, s, a);
     }
 }
 // One of the two shading kernels alone (mcpt_stage_run's LOGIC / GENERATE and MATERIAL stages).
-void launch_shade_stage(bool material_stage, const ShadeArgs& a, int nblocks, const LaunchGeom& g, bool fixed_mode,
+void launch_shade_stage(bool material_stage, const ShadeArgs& args, int nblocks, const LaunchGeom& g, bool fixed_mode,
                         hipStream_t s) {
+    ShadeArgs a = args;
+    a.shade_vblocks = (uint32_t)nblocks;
     if (!material_stage) {
-        if (fixed_mode) hipLaunchKernelGGL(k_shade<true>, dim3(nblocks), dim3(kBlock), 0, s, a);
-        else hipLaunchKernelGGL(k_shade<false>, dim3(nblocks), dim3(kBlock), 0, s, a);
+        const uint32_t G = shade_grid((uint32_t)nblocks, g);
+        if (fixed_mode) hipLaunchKernelGGL(k_shade<true>, dim3(G), dim3(kBlock), 0, s, a);
+        else hipLaunchKernelGGL(k_shade<false>, dim3(G), dim3(kBlock), 0, s, a);
     } else {
         if (fixed_mode) hipLaunchKernelGGL(k_material<true>, dim3(g.mat_blocks[1]), dim3(kBlock), 0, s, a);
         else hipLaunchKernelGGL(k_material<false>, dim3(g.mat_blocks[0]), dim3(kBlock), 0, s, a);

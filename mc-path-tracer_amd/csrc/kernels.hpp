@@ -52,7 +52,8 @@ enum : uint32_t {
     F_CONDB = 1u << 10,     // BRDF-sample MIS term valid when visible
     F_FZERO = 1u << 11,     // f_sample == 0 || pdf_sample == 0
     F_HASVIS = 1u << 12,    // non-delta light: a BRDF visibility ray was traced
-    F_SIDX_SHIFT = 13       // bits 13..31: the sample index the path renders (RNG key)
+    F_SIDX_SHIFT = 13       // bits 13..31: the sample index the path renders (RNG key); a dead
+                            // path's next one (k_shade derives the film's sample count from it)
 };
 constexpr uint32_t kMaxSpp = 1u << (32 - F_SIDX_SHIFT);  // sample indices must fit the flags word
 constexpr int kRecLenShift = 24;  // material record word 2: sample index (< kMaxSpp) | len << 24 (len < 256)
@@ -192,6 +193,7 @@ struct ShadeArgs {
     // the block is dead with its last sample finished, so later launches skip the block's loads
     // (cleared with the film; nullptr: off)
     uint8_t* blk_done;
+    uint32_t shade_vblocks;  // k_shade: shading blocks of the launch (launch_shade sets it and the grid)
 };
 
 // One ray set of a trace launch: rays ro/rd[rid] for queue entries
@@ -225,7 +227,7 @@ struct TraceArgs {
 };
 
 struct HitRecordArgs { DevScene scene; const float4 *ro, *rd; const int32_t* tri; float4 *hit_p, *hit_n; int32_t* scene_tri; uint32_t n; };
-struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n; };
+struct ClearArgs { uint32_t* flags; uint32_t* samples; float4* Ld; uint32_t n, npx; };  // n = npx * slots
 // n accumulators per slot.  tiles == nullptr: n = W * H pixels in pixel order (full layout); else the
 // compact layout's order (tile-set tile i's pixels at i * tile_w * tile_h, row by row), scattered to
 // out[y * W + x] for the pixels inside the W x H film
@@ -245,6 +247,7 @@ struct LaunchGeom {
     uint32_t trace_parts;    // k_trace work partitions, MCPT_TRACE_PARTS (1..kMaxParts)
     uint32_t ndies;          // XCDs
     uint32_t mat_blocks[2];  // k_material grid [reference mode, fixed mode]
+    uint32_t shade_grid;     // k_shade grid cap (resident blocks x MCPT_SHADE_GRID; 0: one block per shading block)
     uint32_t refill_min, tri_min;  // MCPT_REFILL_MIN, MCPT_TRI_MIN
 };
 int launch_geometry(int device, LaunchGeom& g);  // device must be current

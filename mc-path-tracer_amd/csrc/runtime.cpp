@@ -153,9 +153,10 @@ int mcpt_create(int device, const mcpt_config* cfg, mcpt_ctx** out) {
     snprintf(c->devname, sizeof(c->devname), "%s (%s, %d CUs)", prop.name, prop.gcnArchName, prop.multiProcessorCount);
     if (cfg) c->cfg = *cfg;
     else { c->cfg.seed = 0x5EED2026ull; c->cfg.spp = 16; c->cfg.max_depth = 5; c->cfg.rr_depth = 3; c->cfg.tile_w = 256; c->cfg.tile_h = 256; }
-    if (c->cfg.max_depth < 1 || c->cfg.max_depth > 200 || c->cfg.spp < 0 || (uint32_t)c->cfg.spp >= kMaxSpp) {
+    // a dead path's flags word holds its next sample index, up to spp - 1 + 256 path slots
+    if (c->cfg.max_depth < 1 || c->cfg.max_depth > 200 || c->cfg.spp < 0 || (uint32_t)c->cfg.spp > kMaxSpp - 256) {
         delete c;
-        return set_err(nullptr, MCPT_E_INVALID, "bad config (max_depth 1..200, spp 0..2^19-1)");
+        return set_err(nullptr, MCPT_E_INVALID, "bad config (max_depth 1..200, spp 0..2^19-256)");
     }
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -845,7 +846,7 @@ static std::vector<int2> all_tiles(const mcpt_ctx* c) {
 int mcpt_film_clear(mcpt_ctx* c) {
     if (!c || !c->P) return set_err(c, MCPT_E_INVALID, "film not allocated");
     HIPCHK(c, hipSetDevice(c->device));
-    ClearArgs a{c->p.flags, c->p.samples, c->p.Ld, (uint32_t)(c->npx * c->slots)};
+    ClearArgs a{c->p.flags, c->p.samples, c->p.Ld, (uint32_t)(c->npx * c->slots), (uint32_t)c->npx};
     launch_clear(a, c->stream);
     HIPCHK(c, hipGetLastError());
     if (c->compact) {  // the W x H film also holds pixels unpacked from other contexts (mcpt_film_unpack_tiles)
@@ -1282,6 +1283,19 @@ static int stage_run_paths(mcpt_ctx* c, int stage, const mcpt_path_view* in, mcp
     std::vector<uint32_t> fl(in->flags, in->flags + n), sm(n, 0u);
     if (in->samples) sm.assign(in->samples, in->samples + n);
     if (gen) std::fill(fl.begin(), fl.end(), (uint32_t)F_DEAD);
+    if (!mat) {
+        // The device's flags word carries a dead path's next sample index too, and k_shade derives
+        // the film's sample count from it (one path slot here: sample index = count).  In: a dead
+        // path's index is its samples; a live path's must equal them (the oracle's and the
+        // reference's states always agree: samples changes only when a path ends).  Out: dead
+        // paths' flags as the interface has them (F_DEAD alone).
+        for (uint32_t i = 0; i < n; i++) {
+            if (fl[i] & F_DEAD) fl[i] = (uint32_t)F_DEAD | (sm[i] << F_SIDX_SHIFT);
+            else if ((fl[i] >> F_SIDX_SHIFT) != sm[i])
+                return set_err(c, MCPT_E_INVALID, "LOGIC: a live path's sample index (flags) must equal its samples");
+            if (sm[i] >= kMaxSpp) return set_err(c, MCPT_E_INVALID, "samples must be < 2^19");
+        }
+    }
     std::vector<uint8_t> vis(2 * (size_t)n, 0);
     if (in->vis) vis.assign(in->vis, in->vis + 2 * (size_t)n);
     CounterBlock* hc = c->cnt_host;  // pinned staging (the context's counters stay on the device)
@@ -1402,6 +1416,9 @@ static int stage_run_paths(mcpt_ctx* c, int stage, const mcpt_path_view* in, mcp
     auto put4 = [n](float* dst, const std::vector<float4>& v) {
         if (dst) memcpy(dst, v.data(), n * sizeof(float4));
     };
+    if (!mat)
+        for (uint32_t& f : o_fl)
+            if (f & F_DEAD) f = F_DEAD;  // the interface's dead flags (the index lives in samples)
     if (out->flags) memcpy(out->flags, o_fl.data(), n * sizeof(uint32_t));
     if (out->samples) memcpy(out->samples, o_sm.data(), n * sizeof(uint32_t));
     if (out->hit_tri) memcpy(out->hit_tri, o_ht.data(), n * sizeof(int32_t));

@@ -26,9 +26,10 @@ def tiles_for_rank(rank, world, W, H, tile=256):
     return [(tx, ty) for ty in range(ny) for tx in range(nx) if (tx + ty) % world == rank]
 
 
-# Path state per path (126 B) and the budget the strong split may give it per GPU.
+# Path state per path (126 B).  The strong split has no byte budget of its own
+# since every rank holds only its tiles' state (compact layout): C5 at N = 8, the largest case, is
+# 2.1 M pixels x 128 slots x 126 B = 34 GB of a GPU's 288 GB.
 PATH_BYTES = 126
-SLOT_BUDGET_BYTES = 32 << 30
 
 
 def rank_path_pixels(world, W, H, tile):
@@ -37,15 +38,18 @@ def rank_path_pixels(world, W, H, tile):
     return max(len(tiles_for_rank(r, world, W, H, tile)) for r in range(world)) * tile * tile
 
 
-def strong_slots(base_slots, world, W, H, spp, tile=64, budget=SLOT_BUDGET_BYTES):
+def strong_slots(base_slots, world, W, H, spp, tile=64, budget=None):
     """Path slots for a frame split over `world` ranks: every rank keeps the paths in flight of the
     one-GPU run (base_slots x W x H) over its 1/world of the pixels, so slots scale with world --
-    bounded by spp (a slot renders >= 1 sample), by the ABI's 256, and by the per-GPU state budget
-    over the rank's own path state (compact layout: its tiles only) with fewer than 2^31 paths.  One
-    value for every rank: the slot count sets the film's summation order, so the gathered frame then
-    equals a one-rank frame rendered with the same slots bit for bit."""
+    bounded by spp (a slot renders >= 1 sample), by the ABI's 256 and by fewer than 2^31 paths of the
+    rank's own path state (compact layout: its tiles only); `budget` (bytes of path state per GPU)
+    caps them further when given.  One value for every rank: the slot count sets the film's
+    summation order, so the gathered frame then equals a one-rank frame rendered with the same slots
+    bit for bit."""
     px = rank_path_pixels(world, W, H, tile) if world > 1 else W * H
-    cap = max(1, min(budget // (PATH_BYTES * px), ((1 << 31) - 1) // px))
+    cap = max(1, ((1 << 31) - 1) // px)
+    if budget is not None:
+        cap = max(1, min(cap, budget // (PATH_BYTES * px)))
     return int(max(1, min(max(base_slots, min(base_slots * world, spp, 256)), cap)))  # mcpt_set_path_slots: 1..256
 
 

@@ -174,8 +174,8 @@ def test_gather_with_an_empty_rank_gloo_world3():
 
 def test_strong_split_slots():
     """The strong split (bench.py's N > 1 headline): path slots grow with the ranks so every GPU keeps
-    the one-GPU run's paths in flight, bounded by spp, by 256 and by the per-GPU state budget over
-    the rank's own (compact) path state; one value for all ranks."""
+    the one-GPU run's paths in flight, bounded by spp, by 256 and by 2^31 paths of the rank's own
+    (compact) path state, with an optional byte budget; one value for all ranks."""
     import bench
 
     T = bench.MULTI_TILE
@@ -187,7 +187,10 @@ def test_strong_split_slots():
             s = parallel.strong_slots(base, world, W, H, spp, T)
             px = parallel.rank_path_pixels(world, W, H, T)
             assert base <= s <= min(base * world, 256) and s * px < 2 ** 31
-            assert s * px * parallel.PATH_BYTES <= parallel.SLOT_BUDGET_BYTES
+            assert s * px * parallel.PATH_BYTES <= 40e9  # compact state: at most C5's 34 GB per GPU
+    # no byte budget by default: C5 at N = 8 keeps 8 x 16 slots over its 1/8 of 4096^2
+    assert parallel.strong_slots(16, 8, 4096, 4096, 4096, T) == 128
+    assert parallel.strong_slots(16, 8, 4096, 4096, 4096, T, budget=16 << 30) < 128
     assert parallel.strong_slots(16, 8, 256, 256, 16, T) == 16  # spp bound: a slot renders at least one sample
     a = bench.parse(["--gpus", "8", "--no-gather"])
     assert a.no_gather and not a.no_strong and not a.no_weak and not a.no_verify_gather and a.scaling == "strong"

@@ -333,13 +333,21 @@ def test_occluder_cache_same_film(request, mcpt_mod, which):
         assert resolved > 0
 
 
-def test_finished_blocks_skip_and_reset(mcpt_mod, scene_c2):
+@pytest.mark.parametrize("shade_wgs", [None, "3"])
+def test_finished_blocks_skip_and_reset(mcpt_mod, scene_c2, shade_wgs, monkeypatch):
     """k_shade's block done flags (ShadeArgs::blk_done): once a film is complete, further
     iterations trace nothing and leave it bit for bit; a film clear resets the flags, so the
     re-render equals the first one; turning a camera change into a stale film does too.  A
-    render with the flags off (MCPT_NO_BLOCK_DONE, new context) gives the same film."""
+    render with the flags off (MCPT_NO_BLOCK_DONE, new context) gives the same film.  With
+    shade_wgs = 3 (MCPT_SHADE_WGS) k_shade runs the 256 shading blocks on 3 workgroups, ~86 per
+    workgroup (the virtual-block loop and its done-flag prefetch); the film equals the one-pass
+    grid's (MCPT_SHADE_GRID=0)."""
     import os
 
+    if shade_wgs:
+        monkeypatch.setenv("MCPT_SHADE_WGS", shade_wgs)
+    else:
+        monkeypatch.setenv("MCPT_SHADE_GRID", "0")
     rc = mcpt_mod.CONFIGS[2]
     W, H, T = 200, 120, 64
     cam = mcpt_mod.config_camera(rc, W, H)
