@@ -147,8 +147,10 @@ enum { MCPT_STAGE_LOGIC = 0, MCPT_STAGE_GENERATE = 1, MCPT_STAGE_MATERIAL = 2,
  *             bit 2 light ray queued, bit 3 BRDF visibility ray queued (n)
  * LOGIC (k_shade): wf_logic + wf_generate of a film of film_w x film_h pixels, path i = pixel
  * (i % film_w, i / film_w), one path per pixel, the context's camera and config.  In: flags,
- * samples, hit_tri, ray_d, beta, nee0, nee1, vis, Ld.  Out: flags, samples, Ld, ray_o/_d of new
- * paths, beta (the updated throughput of continuing paths), hit_tri, queued.
+ * samples, hit_tri, ray_d, beta, nee0, nee1, vis, Ld; a live path's sample index (flags bits
+ * 13..31) must equal its samples, as in every state the reference or the oracle produces
+ * (MCPT_E_INVALID otherwise: the device derives the count from the index).  Out: flags, samples,
+ * Ld, ray_o/_d of new paths, beta (the updated throughput of continuing paths), hit_tri, queued.
  * GENERATE: LOGIC with every path dead (wf_generate for sample index `samples`).
  * MATERIAL (k_material): the light choice (:207-213) and wf_mat_mix (:295-375) of continuing path
  * i at pixel i.  In: flags (len, sample index), hit_tri, ray_o/_d, beta.  Out: flags, ray_o/_d

@@ -1001,13 +1001,21 @@ constexpr int kGrabMax = MCPT_GRAB_MAX;  // rays one hand-out atomic may reserve
 #define MCPT_ANY_FIRST 0
 #endif
 constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
-// A trip's node phase ends for every lane once fewer than this many lanes still have node work
-// (0: each lane takes its kNodeSteps steps): per node width, MCPT_NODE_MIN_LANES2 / 4.
+// A trip's node phase ends for every lane once fewer than this many lanes still have node work (0:
+// each lane takes its kNodeSteps steps); the others resume next trip, after the triangle phase and
+// a refill of the idle lanes.  Per instantiation, from a sweep of 0/24/32/40/48 (interleaved A/B,
+// one box, whole frames; profiles/ab_r05_node_min.txt): child pairs with the 8-entry stack
+// (config 2) 32: k_trace 2.54 -> 2.47 ms, frame -1.9 %; 4-wide nodes (configs 3, 5) 24: config 3
+// 2.70 -> 2.45 ms (-6 % frame), config 5 17.7 -> 16.9 ms (-3.4 %); child pairs with the deep stack
+// (config 4, 26 pair steps per ray) 0: 24 / 32 were 1.2 / 2.6 % slower.
 #ifndef MCPT_NODE_MIN_LANES2
-#define MCPT_NODE_MIN_LANES2 0
+#define MCPT_NODE_MIN_LANES2 32
+#endif
+#ifndef MCPT_NODE_MIN_LANES2_DEEP
+#define MCPT_NODE_MIN_LANES2_DEEP 0
 #endif
 #ifndef MCPT_NODE_MIN_LANES4
-#define MCPT_NODE_MIN_LANES4 0
+#define MCPT_NODE_MIN_LANES4 24
 #endif
 
 // Waves per SIMD: 7 (<= 72 VGPRs) for child pairs with either LDS stack, 6 (80) for 4-wide nodes
@@ -1417,7 +1425,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             if (ref < 0) break;  // parked-leaf slot full or traversal done: wait for the triangle phase
             // the node phase ends for every lane once fewer than kNodeMin still have node work
             // (they resume next trip, after the triangle phase and a refill)
-            constexpr int kNodeMin = kW == 4 ? MCPT_NODE_MIN_LANES4 : MCPT_NODE_MIN_LANES2;
+            constexpr int kNodeMin =
+                kW == 4 ? MCPT_NODE_MIN_LANES4 : (kLdsStack > ::mcpt_dev::kLdsStack ? MCPT_NODE_MIN_LANES2_DEEP : MCPT_NODE_MIN_LANES2);
             if constexpr (kNodeMin > 0)
                 if ((uint32_t)__popcll(__ballot(true)) < (uint32_t)kNodeMin) break;
           }

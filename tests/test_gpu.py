@@ -1101,6 +1101,32 @@ def test_stage_golden_vectors(mcpt_mod, oracle, stage):
     _check_stage(stage, got, ref, a, oracle)
 
 
+@pytest.mark.gpu
+def test_stage_logic_rejects_inconsistent_sample_index(mcpt_mod):
+    """The device derives a path's sample count from the sample index its flags word carries (a dead
+    path keeps its next one: DESIGN.md section 3), so LOGIC input where a live path's index differs
+    from its samples -- a state neither the reference nor the oracle produces -- fails loudly; dead
+    paths come back with the interface's F_DEAD-only flags."""
+    import stage_fixtures as sf
+
+    s = sf.stage_scene(mcpt_mod)
+    a = s.arrays()
+    pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=sf.SPP, max_depth=sf.DEPTH, rr_depth=sf.RR))
+    pt.upload_scene(s)
+    pt.set_camera(sf.stage_camera(mcpt_mod))
+    inp = sf.logic_state(len(a["mat"]))
+    live = np.flatnonzero((inp["flags"] & 1) == 0)
+    bad = dict(inp)
+    bad["samples"] = inp["samples"].copy()
+    bad["samples"][live[0]] += 1
+    with pytest.raises(mcpt_mod.McptError):
+        pt.stage("logic", bad, film=sf.FILM)
+    got = pt.stage("logic", inp, film=sf.FILM)
+    dead = (got["flags"] & 1) == 1
+    assert dead.any() and np.all(got["flags"][dead] == 1)
+    pt.close()
+
+
 def _check_stage(stage, got, ref, a, oracle):
     """mcpt_stage_run outputs against the oracle's stage restatement, field by field, bit for bit."""
     if stage in ("logic", "generate"):
