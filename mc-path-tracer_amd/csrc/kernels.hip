@@ -62,11 +62,6 @@ __device__ inline void block_push(const bool (&want)[NQ], uint32_t* const (&coun
 }
 
 __device__ inline V3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
-// k_shade generates the block's new samples on consecutive threads (shade_vblock); 0: in place
-#ifndef MCPT_DENSE_GEN
-#define MCPT_DENSE_GEN 1
-#endif
-constexpr bool kDenseGen = MCPT_DENSE_GEN != 0;
 
 // The kernel's by-value argument struct read through an opaque copy of the kernarg segment
 // pointer.  Kernel arguments are invariant loads, so the compiler hoists every field a persistent
@@ -644,8 +639,6 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
     }
     // ---- phase 1: logic + generate (one thread per pixel)
     bool gen_ext = false, gen_trivial = false, cont = false;
-    bool want_gen = false;      // kDenseGen: the path starts a new sample (generated below)
-    uint32_t gen_sidx = 0, gpid = pid;
     uint32_t cont_len = 0, cont_sidx = 0;
     int32_t cont_htri = -1;
     V3 beta_store = v3(0.f, 0.f, 0.f);
@@ -748,11 +741,7 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
         }
         uint32_t nflags = fl;
         if (dead) nflags = F_DEAD | (sidx << F_SIDX_SHIFT);
-        if (kDenseGen && dead && sidx < spp) {  // generated below, on consecutive threads
-            want_gen = true;
-            gen_sidx = sidx;
-            nflags = (1u << F_LEN_SHIFT) | (sidx << F_SIDX_SHIFT);
-        } else if (dead && sidx < spp) {  // :219-222 + wf_generate (:225-251)
+        if (dead && sidx < spp) {  // :219-222 + wf_generate (:225-251)
             const Rng r0{rng_key(a.seed, pix, sidx), 0u};
             V3 new_o, new_d;
             gen_ray(a.cam, a.W, a.H, x, y, r0, new_o, new_d);
@@ -770,51 +759,6 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
         if (!cont && nflags != fl) st_s(a.p.flags + pid, nflags);  // continuing paths: written by material()
         finished = dead && !(sidx < spp);
     }
-    if constexpr (kDenseGen) {
-        // ---- wf_generate (:225-251) for the block's new samples on consecutive threads.  A quarter
-        // to a third of a block's paths start a sample per iteration; run in place, the camera ray
-        // (fp64 NDC, two 4x4 products, divisions, normalisations) occupied every wave of the block
-        // with the other lanes masked.  Listed in LDS (thread index | sample index << 8), the
-        // generating paths fill ceil(n / 64) waves and the other waves skip the section.
-        __shared__ uint32_t s_gcnt[kBlock / 64];
-        __shared__ uint32_t s_gen[kBlock];
-        const uint64_t gm = __ballot(want_gen);
-        const uint32_t gpre = __builtin_amdgcn_mbcnt_hi((uint32_t)(gm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)gm, 0u));
-        const uint32_t wave = threadIdx.x >> 6;
-        if (lane == 0) s_gcnt[wave] = (uint32_t)__popcll(gm);
-        __syncthreads();
-        uint32_t gbase = 0, ngen = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < kBlock / 64; w++) {
-            const uint32_t c = s_gcnt[w];
-            gbase += w < wave ? c : 0u;
-            ngen += c;
-        }
-        if (want_gen) s_gen[gbase + gpre] = threadIdx.x | (gen_sidx << 8);
-        __syncthreads();
-        if (threadIdx.x < ngen) {
-            const uint32_t item = s_gen[threadIdx.x];
-            const int gli = (bs - tile * bpt) * kBlock + (int)(item & 0xffu);
-            const uint32_t gs = item >> 8;
-            const int2 gt = a.tiles[tile];
-            const int gx = gt.x * a.tile_w + gli % a.tile_w, gy = gt.y * a.tile_h + gli / a.tile_w;
-            const uint32_t gpix = (uint32_t)gy * (uint32_t)a.W + (uint32_t)gx;
-            const uint32_t glocal =
-                a.compact ? (uint32_t)(a.tile_base ? a.tile_base[tile] : tile) * (uint32_t)tile_px + (uint32_t)gli : gpix;
-            gpid = (uint32_t)slot * a.npx + glocal;
-            const Rng r0{rng_key(a.seed, gpix, gs), 0u};
-            V3 new_o, new_d;
-            gen_ray(a.cam, a.W, a.H, gx, gy, r0, new_o, new_d);
-            st_s(a.p.ray_o + gpid, f4(new_o, 0.f));
-            st_s(a.p.ray_d + gpid, f4(new_d, 0.f));
-            gen_ext = true;
-            if (ray_misses_scene(sc, new_o, new_d)) {  // resolved here: isect stays "not found"
-                a.p.hit_tri[gpid] = -1;
-                gen_ext = false;
-                gen_trivial = true;
-            }
-        }
-    }
     // ---- pushes: generated extension rays and continuing paths (material queue); one
     // atomic per block and queue.  A continuing path's record and updated throughput go
     // to k_material densely (it writes p.beta with f_s/pdf_s in .w).
@@ -825,7 +769,7 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
         uint32_t* ctr[2] = {sc_ctr + C_EXT, sc_ctr + C_MAT};
         uint32_t slot[2], total[2];
         block_push<2>(want, ctr, slot, total);
-        if (gen_ext) st_q(a.ext_q + shard * a.ext_cap + slot[0], kDenseGen ? gpid : pid);
+        if (gen_ext) st_q(a.ext_q + shard * a.ext_cap + slot[0], pid);
         if (cont) {
             const uint32_t qi = shard * a.ext_cap + slot[1];
             st_s(a.mat_rec + qi, make_uint4(pid, pix, cont_sidx | (cont_len << kRecLenShift), (uint32_t)cont_htri));
