@@ -92,7 +92,7 @@ PY
 import json; d = json.load(open('$O/abenv.json')); r = d['roofline']; p = r['per_ray']
 print('$e'.ljust(30), round(d['value'], 1), 'Mray/s', d['ms_per_step'], 'ms/frame trace', r['avg_launch_ms'], 'shade',
       d['stage_ms_per_step']['k_shade+k_material'], 'ext nodes/tests', p['ext_pair_nodes'], p['ext_tri_tests'],
-      'any', p['any_pair_nodes'], p['any_tri_tests'])"
+      'any', p['any_pair_nodes'], p['any_tri_tests'], 'occ', p['any_resolved_by_occluder_cache'])"
       done
     done ;;
   partition)
