@@ -17,6 +17,7 @@
 #   ab         whole-frame A/B of library builds, interleaved (LIBS="a:path.so b:path.so", CONFIGS,
 #              ROUNDS; tools/gpu/ab_libs.sh)
 #   abenv      the same for environment settings (ENVS="A=1|A=0 B=2", '|'-separated)
+#   abargs     the same for bench arguments (ARGSETS="--slots 16|--slots 24")
 #   partition  tools/partition_rehearsal.py (PART_ARGS)       -> gpurun_out/partition_$TAG.json
 #
 # Parameters (environment): CONFIG (2), TAG (r04), STEPS (bench frames, 3), BENCH_ARGS.
@@ -93,6 +94,18 @@ import json; d = json.load(open('$O/abenv.json')); r = d['roofline']; p = r['per
 print('$e'.ljust(30), round(d['value'], 1), 'Mray/s', d['ms_per_step'], 'ms/frame trace', r['avg_launch_ms'], 'shade',
       d['stage_ms_per_step']['k_shade+k_material'], 'ext nodes/tests', p['ext_pair_nodes'], p['ext_tri_tests'],
       'any', p['any_pair_nodes'], p['any_tri_tests'], 'occ', p['any_resolved_by_occluder_cache'])"
+      done
+    done ;;
+  abargs)
+    # the same for bench arguments (ARGSETS="--slots 16|--slots 24", '|'-separated), added to BARGS
+    IFS='|' read -ra sets <<< "$ARGSETS"
+    for r in $(seq ${ROUNDS:-2}); do
+      for e in "${sets[@]}"; do
+        timeout -k 10 600 python -u bench.py $BARGS $e > $O/abargs.json 2> $O/abargs.err || fail abargs 20 $O/abargs.err
+        python3 -c "
+import json; d = json.load(open('$O/abargs.json')); r = d['roofline']
+print('$e'.ljust(30), round(d['value'], 1), 'Mray/s', d['ms_per_step'], 'ms/frame trace', r['avg_launch_ms'], 'shade',
+      d['stage_ms_per_step']['k_shade+k_material'], 'slots', d['config']['path_slots'], 'iterations', d['config']['iterations_per_step_rank0'])"
       done
     done ;;
   partition)
