@@ -821,113 +821,6 @@ int Scene::build(int max_prims, std::string& err) {
     return build(p, err);
 }
 
-// Treelet restructuring (Karras & Aila, "Fast parallel construction of high-quality bounding
-// volume hierarchies", HPG 2013) as a host pass over a finished tree: for every interior node,
-// bottom-up, the treelet of up to kTL leaves grown from it by expanding the leaf of largest area is
-// re-paired by an exact dynamic program over leaf subsets (SAH cost ct A + children, a leaf ci n A),
-// and rebuilt with the treelet's own interior nodes when that is cheaper.  Leaves and their
-// triangle ranges are untouched, interior boxes are recomputed as exact unions, so every box still
-// contains its subtree and results do not depend on the tree.  keep_root:
-// the root's two children stay as they are (the unbounded-triangle subtree is not mixed in).
-static void bvh_treelet_optimize(std::vector<BuildNode>& nodes, int root, bool keep_root, double ct, double ci, int passes) {
-    constexpr int kTL = 7;
-    const int NN = (int)nodes.size();
-    std::vector<double> area(NN), cost(NN);
-    auto leaf_cost = [&](int i) { return ci * (double)nodes[i].n * area[i]; };
-    // post-order of the current tree
-    auto post_order = [&]() {
-        std::vector<int> order, st{root};
-        std::vector<char> done(NN, 0);
-        while (!st.empty()) {
-            const int i = st.back();
-            if (nodes[i].n > 0 || done[i]) {
-                st.pop_back();
-                order.push_back(i);
-                continue;
-            }
-            done[i] = 1;
-            st.push_back(nodes[i].child[1]);
-            st.push_back(nodes[i].child[0]);
-        }
-        return order;
-    };
-    for (int pass = 0; pass < passes; pass++) {
-        const std::vector<int> order = post_order();
-        for (int i : order) {
-            area[i] = nodes[i].b.area();
-            cost[i] = nodes[i].n > 0 ? leaf_cost(i) : ct * area[i] + cost[nodes[i].child[0]] + cost[nodes[i].child[1]];
-        }
-        for (int x : order) {
-            if (nodes[x].n > 0 || (keep_root && x == root)) continue;
-            // grow the treelet
-            int L[kTL], nl = 2, I[kTL], ni = 1;
-            L[0] = nodes[x].child[0];
-            L[1] = nodes[x].child[1];
-            I[0] = x;
-            while (nl < kTL) {
-                int bi = -1;
-                for (int k = 0; k < nl; k++)
-                    if (nodes[L[k]].n == 0 && (bi < 0 || area[L[k]] > area[L[bi]])) bi = k;
-                if (bi < 0) break;
-                const int e = L[bi];
-                I[ni++] = e;
-                L[bi] = nodes[e].child[0];
-                L[nl++] = nodes[e].child[1];
-            }
-            if (nl < 3) continue;
-            const int full = (1 << nl) - 1;
-            double sa[1 << kTL], copt[1 << kTL];
-            int part[1 << kTL];
-            for (int m = 1; m <= full; m++) {
-                Bounds b;
-                for (int k = 0; k < nl; k++)
-                    if (m >> k & 1) b.add(nodes[L[k]].b);
-                sa[m] = b.area();
-            }
-            for (int k = 0; k < nl; k++) { copt[1 << k] = cost[L[k]]; part[1 << k] = 0; }
-            for (int m = 1; m <= full; m++) {
-                if ((m & (m - 1)) == 0) continue;
-                const int low = m & -m;
-                double best = 1e300;
-                int bp = 0;
-                // proper subsets p of m containing m's lowest leaf (each split once)
-                for (int p = (m - 1) & m; p; p = (p - 1) & m) {
-                    if (!(p & low)) continue;
-                    const double c = copt[p] + copt[m ^ p];
-                    if (c < best) { best = c; bp = p; }
-                }
-                copt[m] = ct * sa[m] + best;
-                part[m] = bp;
-            }
-            if (!(copt[full] < cost[x] * (1.0 - 1e-9))) continue;
-            // rebuild: the treelet's interior nodes, x first (it keeps its parent's reference)
-            int next = 0;
-            std::function<int(int)> make = [&](int m) -> int {
-                if ((m & (m - 1)) == 0) {
-                    int k = 0;
-                    while (!(m >> k & 1)) k++;
-                    return L[k];
-                }
-                const int me = I[next++];
-                const int c0 = make(part[m]), c1 = make(m ^ part[m]);
-                BuildNode& n = nodes[me];
-                n.child[0] = c0;
-                n.child[1] = c1;
-                n.n = 0;
-                n.b = nodes[c0].b;
-                n.b.add(nodes[c1].b);
-                const V3 d = (nodes[c1].b.mn + nodes[c1].b.mx) - (nodes[c0].b.mn + nodes[c0].b.mx);
-                const float ax = std::fabs(d.x), ay = std::fabs(d.y), az = std::fabs(d.z);
-                n.axis = ax >= ay && ax >= az ? 0 : (ay >= az ? 1 : 2);
-                area[me] = n.b.area();
-                cost[me] = ct * area[me] + cost[c0] + cost[c1];
-                return me;
-            };
-            make(full);
-        }
-    }
-}
-
 int Scene::build(const mcpt_bvh_params& prm, std::string& err) {
     const int max_prims = prm.max_prims;
     if (max_prims < 1 || max_prims > 8) { err = "max_prims must be 1..8"; return MCPT_E_INVALID; }
@@ -993,24 +886,6 @@ int Scene::build(const mcpt_bvh_params& prm, std::string& err) {
             bld.max_depth = std::max(bld.max_depth, 1);
         } else {
             root = sub(0, (int)T, 0);
-        }
-        // MCPT_BVH_TREELET=P (SAH3 only): P passes of treelet restructuring over the finished tree
-        if (bld.mode == 1)
-            if (const char* tp = std::getenv("MCPT_BVH_TREELET")) {
-                const int passes = std::atoi(tp);
-                if (passes > 0) bvh_treelet_optimize(bld.nodes, root, nbig > 0, bld.ct, bld.ci, passes);
-            }
-        // depth after any restructuring
-        {
-            int md = 0;
-            std::vector<std::pair<int, int>> st{{root, 0}};
-            while (!st.empty()) {
-                auto [ni, dd] = st.back();
-                st.pop_back();
-                md = std::max(md, dd);
-                if (bld.nodes[ni].n == 0) { st.push_back({bld.nodes[ni].child[0], dd + 1}); st.push_back({bld.nodes[ni].child[1], dd + 1}); }
-            }
-            bld.max_depth = md;
         }
         bvh_depth = bld.max_depth;
         // flatten_tree (BVH.cu:312-333): depth-first, first child adjacent.
