@@ -53,10 +53,12 @@ B_HIT = 40            # per closest hit: 3 normals + material id
 B_SHADE = 195 + 172   # logic + material per path-bounce
 B_GEN = 49            # generate per new sample
 # Path slots (paths in flight per pixel) per BASELINE config: the measured best of the
-# whole-frame sweep (tools/gpu/run.sh kstats, DESIGN.md section 2: config 2 at 3/8/16/24/32 slots
-# 7287/7856/8064/8095/8081 Mray/s, config 3 at 3/16/32 4924/6624/6822, config 5 (64 spp) at
-# 4/8/16 5257/5458/5486); the parity tests and smoke() run the same layout.
-BENCH_SLOTS = {1: 16, 2: 24, 3: 32, 4: 16, 5: 16}
+# whole-frame sweeps (round 3, DESIGN.md section 2: config 2 at 3/8/16/24/32 slots
+# 7287/7856/8064/8095/8081 Mray/s; round 5 at the round-5 kernels, profiles/ab_r05_slots.txt:
+# config 2 20/24/32 289.1/287.2/292.3 ms per frame, config 3 32/48/64 252.4/251.8/248.4 ms,
+# config 4 16/24/32 5.82/5.75/5.75 s, config 5 (1024 spp) 16/24 11.85/11.72 s); the parity
+# tests and smoke() run the same layout.
+BENCH_SLOTS = {1: 16, 2: 24, 3: 64, 4: 24, 5: 24}
 STEP = "frame"  # what one step is; stamped into the PMC summaries (tools/pmc.py)
 
 

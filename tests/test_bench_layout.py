@@ -95,8 +95,9 @@ def test_bench_layout_config2_scattered_rows(mcpt_mod, oracle, scene_c2):
 @pytest.mark.parametrize("cid,tiles", [(4, [(7, 4), (3, 2)]), (5, [(8, 8)])], ids=["config4", "config5"])
 def test_full_spp_tiles_against_oracle(mcpt_mod, oracle, cid, tiles):
     """Configs 4 and 5 at their full sample counts -- 1024 spp depth 8, 4096 spp depth 12 -- at the
-    bench's path slots (16: every slot renders 64 / 256 samples, sample indices up to 4095 keyed
-    into the RNG, wavefront_kernels.cu:124,219-222) on whole 256 x 256 tiles (mcpt_set_tiles), one
+    bench's path slots (24: slot k renders samples k, k + 24, ..., 42-43 / 170-171 of them, sample
+    indices up to 4095 keyed into the RNG, wavefront_kernels.cu:124,219-222) on whole 256 x 256
+    tiles (mcpt_set_tiles), one
     row of each tile against the oracle (the one tile alone: part=(tx + ty, a modulus larger than
     any tx + ty))."""
     rc = mcpt_mod.CONFIGS[cid]
