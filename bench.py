@@ -131,11 +131,21 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
-def pmc_summary(config, slots, kind="pmc"):
+def stamp_spp(config, args_text):
+    """The spp a profiled bench command ran at: its --spp, else the config's."""
+    m = __import__("re").search(r"--spp[ =](\d+)", args_text or "")
+    if m:
+        return int(m.group(1))
+    import mcpt
+
+    return mcpt.CONFIGS[config].spp
+
+
+def pmc_summary(config, slots, kind="pmc", spp=None):
     """The newest committed rocprofv3 summary of this config (kind "pmc": FETCH/WRITE traffic,
     "pmcdetail": SQ/TCC counters; profiles/<kind>_rNN.json for config 2, <kind>_c<config>_rNN.json
     for the others) and whether it was measured on this code (source hash) and this workload
-    (config, path slots, step)."""
+    (config, path slots, step, spp: a launch's traffic depends on the spp through the path mix)."""
     pre = f"{kind}_r" if config == 2 else f"{kind}_c{config}_r"
     files = sorted(f for f in glob.glob(os.path.join(REPO, "profiles", f"{pre}*.json"))
                    if os.path.basename(f)[len(pre):][:1].isdigit())
@@ -153,6 +163,8 @@ def pmc_summary(config, slots, kind="pmc"):
         why.append(f"taken on config {stamp.get('config')} / {stamp.get('slots')} slots")
     if stamp.get("step", "iteration") != STEP:
         why.append(f"taken with {stamp.get('step', 'iteration')} steps")
+    if spp is not None and "spp" in stamp and stamp["spp"] != spp:
+        why.append(f"taken at {stamp['spp']} spp")
     return d, ("; ".join(why) or None)
 
 
@@ -250,7 +262,7 @@ class Acc:
         return int(self.extend_rays + self.shadow_rays + self.vis_rays)
 
 
-def roofline(st, ms_trace, ms_shade, config, slots, work=None):
+def roofline(st, ms_trace, ms_shade, config, slots, work=None, spp=None):
     """roofline object of the dominant kernel (k_trace) and of the shading stages.
 
     achieved = SURVEY.md 8(d)'s algorithmic bytes that live in HBM: the per-ray state (65 B per
@@ -277,9 +289,9 @@ def roofline(st, ms_trace, ms_shade, config, slots, work=None):
     bvh = (2 * B_NODE * (w.ext_nodes + w.any_nodes) + B_TRI * (w.ext_tests + w.any_tests) + B_HIT * w.ext_hits) / wn
     achieved = state / avg_s
     names = {"k_trace": ("mcpt_dev::k_trace<",), "shade": ("mcpt_dev::k_shade<", "mcpt_dev::k_material<")}
-    summary, stale = pmc_summary(config, slots)
+    summary, stale = pmc_summary(config, slots, spp=spp)
     fresh = summary if stale is None else None
-    detail, dstale = pmc_summary(config, slots, "pmcdetail")
+    detail, dstale = pmc_summary(config, slots, "pmcdetail", spp=spp)
     dfresh = detail if dstale is None else None
     traffic = pmc_traffic(fresh, names["k_trace"])
     roof = {"bound": None, "kernel": "k_trace", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
@@ -357,7 +369,7 @@ def trace_phases(work):
                     "the busiest lane's steps) and triangle phases, with the lanes doing work in each"}
 
 
-def extend_shade(st, frame_s, steps, config, slots):
+def extend_shade(st, frame_s, steps, config, slots, spp=None):
     """The metric's own roofline fraction: the whole wavefront step (extend + shade: k_shade,
     k_material, k_trace) against 8 TB/s, per frame.  state: SURVEY.md 8(d)'s algorithmic bytes
     (465 B per path-bounce split as logic+material 367 per continuing path-bounce, extend 65 per
@@ -372,7 +384,7 @@ def extend_shade(st, frame_s, steps, config, slots):
     out = {"frame_s": round(frame_s, 5), "iterations_per_frame": round(it, 1),
            "state_bytes_per_frame": int(state), "state_GBps": round(state / frame_s / 1e9, 1),
            "state_frac": round(state / frame_s / HBM_PEAK, 4)}
-    summary, stale = pmc_summary(config, slots)
+    summary, stale = pmc_summary(config, slots, spp=spp)
     if stale is None:
         per = [pmc_traffic(summary, (p,)) for p in ("mcpt_dev::k_trace<", "mcpt_dev::k_shade<", "mcpt_dev::k_material<")]
         if None not in per:
@@ -613,8 +625,8 @@ def main():
         return
 
     K = args.steps
-    roof = roofline(st, st.ms_extend, st.ms_shade, args.config, slots, work)
-    roof["extend_shade"] = extend_shade(st, dt_all / K, K, args.config, slots)
+    roof = roofline(st, st.ms_extend, st.ms_shade, args.config, slots, work, spp=spp)
+    roof["extend_shade"] = extend_shade(st, dt_all / K, K, args.config, slots, spp=spp)
     tp = trace_phases(work)
     if tp:
         roof["k_trace_phases"] = tp

@@ -50,6 +50,14 @@ def test_pmc_summary_stale_detection(tmp_path, monkeypatch):
     d, why = bench.pmc_summary(3, 32)
     assert why is None and d["stamp"]["config"] == 3
     assert bench.pmc_summary(5, 16)[0] is None
+    # a launch's traffic depends on the spp (the path mix): config 5's 64-spp summary is stale for its
+    # 4096-spp frame; summaries stamped before spp was recorded are not judged on it
+    st5 = dict(_stamp(h="def", config=5, slots=24), spp=bench.stamp_spp(5, "--config 5 --steps 1 --spp 64"))
+    assert st5["spp"] == 64 and bench.stamp_spp(5, "--config 5") == 4096
+    (prof / "pmc_c5_r12.json").write_text(json.dumps({"stamp": st5, "kernels": kern}))
+    assert bench.pmc_summary(5, 24, spp=64)[1] is None
+    assert "taken at 64 spp" in bench.pmc_summary(5, 24, spp=4096)[1]
+    assert bench.pmc_summary(3, 32, spp=999)[1] is None
 
 
 class _St:

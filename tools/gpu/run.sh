@@ -80,7 +80,7 @@ PY
         > $O/pmct_$sfx/p$i.log 2>&1 || fail "pmc pass $i" 10 $O/pmct_$sfx/p$i.log
     done
     PMC_CONFIG=$CONFIG PMC_ARGS="$BARGS" STATS_NAME=kernel_stats_$sfx python3 tools/pmc.py $sfx $R > /dev/null &&
-      PMC_CONFIG=$CONFIG python3 tools/pmc_detail.py $sfx $sfx $O || fail "pmc summary" 5 /dev/null
+      PMC_CONFIG=$CONFIG PMC_ARGS="$BARGS" python3 tools/pmc_detail.py $sfx $sfx $O || fail "pmc summary" 5 /dev/null
     ls profiles/*_$sfx* ;;
   ab)
     bash tools/gpu/ab_libs.sh || exit 1 ;;

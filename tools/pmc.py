@@ -53,7 +53,8 @@ import bench  # noqa: E402  (source_hash only)
 # PMC_CONFIG / PMC_SLOTS say otherwise; bench.py uses the traffic only when this stamp matches its run.
 cfg = int(os.environ.get("PMC_CONFIG", "2"))
 stamp = {"source_hash": bench.source_hash(), "config": cfg,
-         "slots": int(os.environ.get("PMC_SLOTS", str(bench.BENCH_SLOTS[cfg]))), "step": bench.STEP}
+         "slots": int(os.environ.get("PMC_SLOTS", str(bench.BENCH_SLOTS[cfg]))), "step": bench.STEP,
+         "spp": bench.stamp_spp(cfg, os.environ.get("PMC_ARGS", ""))}
 out = {"round": tag, "stamp": stamp,
        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on "
        f"'python3 bench.py {os.environ.get('PMC_ARGS', '--no-cpu-baseline')}'; durations from --kernel-trace --stats",
