@@ -610,9 +610,10 @@ __device__ inline uint32_t shade_done_idx(const ShadeArgs& a, int vb) {
     return (((uint32_t)slot * nty + (uint32_t)t.y) * ntx + (uint32_t)t.x) * (uint32_t)bpt + (uint32_t)(bs - tile * bpt);
 }
 
-// The path this thread shades in shading block vb: false when the block's thread has no pixel
-// (past the tile, or the last column / row, which are never rendered: wavefront_kernels.cu:110).
-__device__ inline bool shade_path(const ShadeArgs& a, int vb, uint32_t& pid, uint32_t& pix, int& x, int& y) {
+// One shading block: logic + generate for kBlock pixels of a path slot, then the block's pushes.
+template <bool FIXED>
+__device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeArgs& a, int vb, uint32_t done_idx) {
+    const DevScene& sc = a.scene;
     const int tile_px = a.tile_w * a.tile_h;
     const int bpt = (tile_px + kBlock - 1) / kBlock;
     // path slots: blocks [k * ntiles * bpt, (k + 1) * ntiles * bpt) run slot k of every pixel
@@ -621,43 +622,20 @@ __device__ inline bool shade_path(const ShadeArgs& a, int vb, uint32_t& pid, uin
     const int bs = vb - slot * per_slot;
     const int tile = bs / bpt;
     const int li = (bs - tile * bpt) * kBlock + threadIdx.x;
-    pid = pix = 0;
-    x = y = 0;
-    if (!(tile < a.ntiles && li < tile_px)) return false;
-    const int2 t = a.tiles[tile];
-    x = t.x * a.tile_w + li % a.tile_w;
-    y = t.y * a.tile_h + li / a.tile_w;
-    pix = (uint32_t)y * (uint32_t)a.W + (uint32_t)x;
-    // path index (ShadeArgs::npx): the pixel id, or its place in the compact tile-set layout
-    const uint32_t local = a.compact ? (uint32_t)(a.tile_base ? a.tile_base[tile] : tile) * (uint32_t)tile_px + (uint32_t)li : pix;
-    pid = (uint32_t)slot * a.npx + local;
-    return x < a.W - 1 && y < a.H - 1;
-}
-
-// One shading block: logic + generate for kBlock pixels of a path slot, then the block's pushes.
-// fl_in / ht_in: the block's flags and hit words, loaded ahead by the previous block (or the loop
-// head); the next live block's are loaded here (vb_next >= 0), so their round trip overlaps this
-// block's second load round and logic instead of following its pushes.
-template <bool FIXED>
-__device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeArgs& a, int vb, uint32_t done_idx,
-                                                                   uint32_t fl_in, int32_t ht_in, int vb_next,
-                                                                   uint32_t& fl_next, int32_t& ht_next) {
-    const DevScene& sc = a.scene;
-    const int tile_px = a.tile_w * a.tile_h;
-    const int bpt = (tile_px + kBlock - 1) / kBlock;
-    const int per_slot = a.ntiles * bpt;
-    const int slot = a.slots > 1 ? vb / per_slot : 0;
     const int lane = threadIdx.x & 63;
-    uint32_t pid, pix;  // path id (slot * pixels + pixel) and pixel id
-    int x, y;
-    bool valid = shade_path(a, vb, pid, pix, x, y);
-    if (vb_next >= 0) {
-        uint32_t npid, npix;
-        int nx, ny;
-        if (shade_path(a, vb_next, npid, npix, nx, ny)) {
-            fl_next = ld_s(a.p.flags + npid);
-            ht_next = ld_s(a.p.hit_tri + npid);
-        }
+    bool valid = tile < a.ntiles && li < tile_px;
+    uint32_t pid = 0, pix = 0;  // path id (slot * pixels + pixel) and pixel id
+    int x = 0, y = 0;
+    if (valid) {
+        int2 t = a.tiles[tile];
+        x = t.x * a.tile_w + li % a.tile_w;
+        y = t.y * a.tile_h + li / a.tile_w;
+        valid = x < a.W - 1 && y < a.H - 1;  // last column and row never rendered (wavefront_kernels.cu:110)
+        pix = (uint32_t)y * (uint32_t)a.W + (uint32_t)x;
+        // path index (ShadeArgs::npx): the pixel id, or its place in the compact tile-set layout
+        const uint32_t local = a.compact ? (uint32_t)(a.tile_base ? a.tile_base[tile] : tile) * (uint32_t)tile_px + (uint32_t)li
+                                         : pix;
+        pid = (uint32_t)slot * a.npx + local;
     }
     // ---- phase 1: logic + generate (one thread per pixel)
     bool gen_ext = false, gen_trivial = false, cont = false;
@@ -677,8 +655,8 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
         // per-path state unconditionally, the len-dependent streams (ray_d for a
         // primary miss, the MIS terms and visibility for len > 1) at pid when needed
         // and at a shared dummy index 0 otherwise (no extra bandwidth).
-        const uint32_t fl = fl_in;
-        const int32_t htri = ht_in;
+        const uint32_t fl = ld_s(a.p.flags + pid);
+        const int32_t htri = ld_s(a.p.hit_tri + pid);
         const float4 b4 = ld_s(a.p.beta + ((((fl >> F_LEN_SHIFT) & 0xffu) > 1u) ? pid : 0u));  // len 1: beta is (1,1,1), not loaded
         const uint32_t len = (fl >> F_LEN_SHIFT) & 0xffu;
         const bool need_rd = len == 1 && htri < 0;
@@ -842,32 +820,11 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     __shared__ uint32_t s_didx[kBlock];
     s_didx[k] = didx;
     __syncthreads();
-    auto live_at = [&](uint32_t j) { return ((s_live[j >> 6] >> (j & 63)) & 1ull) != 0; };
-    uint32_t j = 0;
-    while (j < mine && !live_at(j)) j++;
-    uint32_t fl = 0;
-    int32_t ht = -1;
-    if (j < mine) {  // the first live block's first load round
-        const ShadeArgs& a0 = kernarg_fresh<ShadeArgs>();
-        uint32_t pid, pix;
-        int x, y;
-        if (shade_path(a0, (int)(blockIdx.x + j * G), pid, pix, x, y)) {
-            fl = ld_s(a0.p.flags + pid);
-            ht = ld_s(a0.p.hit_tri + pid);
-        }
-    }
-    while (j < mine) {
-        uint32_t jn = j + 1;
-        while (jn < mine && !live_at(jn)) jn++;
-        uint32_t fl_n = 0;
-        int32_t ht_n = -1;
+    for (uint32_t j = 0; j < mine; j++) {
+        if (!((s_live[j >> 6] >> (j & 63)) & 1ull)) continue;
         // the arguments re-read per shading block (kernarg_fresh): hoisted out of the loop, the
         // struct's fields took the SGPR file and spilled (89 SGPRs, 54 -> 86 VGPRs)
-        shade_vblock<FIXED>(kernarg_fresh<ShadeArgs>(), (int)(blockIdx.x + j * G), s_didx[j], fl, ht,
-                            jn < mine ? (int)(blockIdx.x + jn * G) : -1, fl_n, ht_n);
-        fl = fl_n;
-        ht = ht_n;
-        j = jn;
+        shade_vblock<FIXED>(kernarg_fresh<ShadeArgs>(), (int)(blockIdx.x + j * G), s_didx[j]);
     }
 }
 
