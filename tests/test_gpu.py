@@ -872,13 +872,19 @@ def test_native_gather_equals_one_pass(mcpt_mod, scene_c2, slots, compact):
         pt.close()
 
 
-def test_compact_paths_layout(mcpt_mod, scene_c2):
+@pytest.mark.parametrize("shade_wgs", [None, "2"])
+def test_compact_paths_layout(mcpt_mod, scene_c2, shade_wgs, monkeypatch):
     """mcpt_set_compact_paths: path state over the tile set only (a multi-GPU rank's 1/N).  Films are
     the full layout's bit for bit: the whole tile set in a scrambled order, a partition's tiles with 3
     path slots, the reference's one-tile-per-call loop over the set's tiles, and a partition packed
     and unpacked into a compact root (the RCCL gather's two halves).  Tiles outside the set are
-    rejected by mcpt_wavefront_step, duplicates by mcpt_set_tiles; path slots keep the set."""
+    rejected by mcpt_wavefront_step, duplicates by mcpt_set_tiles; path slots keep the set.  With
+    shade_wgs = 2 (MCPT_SHADE_WGS) the compact contexts run k_shade's shading blocks on two
+    workgroups (the bounded grid's loop over tile-set blocks and their done flags)."""
     from mcpt import parallel
+
+    if shade_wgs:
+        monkeypatch.setenv("MCPT_SHADE_WGS", shade_wgs)
 
     rc = mcpt_mod.CONFIGS[2]
     W, H, T = 200, 120, 64  # ragged: the last tile row and column overhang the film
