@@ -883,16 +883,15 @@ def test_compact_paths_layout(mcpt_mod, scene_c2, shade_wgs, monkeypatch):
     workgroups (the bounded grid's loop over tile-set blocks and their done flags)."""
     from mcpt import parallel
 
-    if shade_wgs:
-        monkeypatch.setenv("MCPT_SHADE_WGS", shade_wgs)
-
     rc = mcpt_mod.CONFIGS[2]
     W, H, T = 200, 120, 64  # ragged: the last tile row and column overhang the film
     cam = mcpt_mod.config_camera(rc, W, H)
-    full = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)
+    full = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)  # the default grid
     full.set_path_slots(3)
     full.render()
     L0, s0 = full.film()
+    if shade_wgs:  # every context created from here on
+        monkeypatch.setenv("MCPT_SHADE_WGS", shade_wgs)
     nx, ny = parallel.tile_grid(W, H, T)
     every = [(tx, ty) for ty in range(ny) for tx in range(nx)]
     rng = np.random.default_rng(5)
