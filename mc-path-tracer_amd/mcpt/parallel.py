@@ -41,16 +41,18 @@ def rank_path_pixels(world, W, H, tile):
 def strong_slots(base_slots, world, W, H, spp, tile=64, budget=None):
     """Path slots for a frame split over `world` ranks: every rank keeps the paths in flight of the
     one-GPU run (base_slots x W x H) over its 1/world of the pixels, so slots scale with world --
-    bounded by spp (a slot renders >= 1 sample), by the ABI's 256 and by fewer than 2^31 paths of the
+    bounded by spp / 2 (a slot renders >= 2 samples: config 2 at N = 8 ran 43.4 ms per rank frame at
+    128 slots against 44.7 at 192, whose 1.3 samples per slot leave a long tail;
+    profiles/partition_r05_c2_slots.json), by the ABI's 256 and by fewer than 2^31 paths of the
     rank's own path state (compact layout: its tiles only); `budget` (bytes of path state per GPU)
-    caps them further when given.  One value for every rank: the slot count sets the film's
+    caps them further when given.  Never below base_slots.  One value for every rank: the slot count sets the film's
     summation order, so the gathered frame then equals a one-rank frame rendered with the same slots
     bit for bit."""
     px = rank_path_pixels(world, W, H, tile) if world > 1 else W * H
     cap = max(1, ((1 << 31) - 1) // px)
     if budget is not None:
         cap = max(1, min(cap, budget // (PATH_BYTES * px)))
-    return int(max(1, min(max(base_slots, min(base_slots * world, spp, 256)), cap)))  # mcpt_set_path_slots: 1..256
+    return int(max(1, min(max(base_slots, min(base_slots * world, max(1, spp // 2), 256)), cap)))  # 1..256
 
 
 def pack(Ld: np.ndarray, samples: np.ndarray, tiles, W, H, tile=256) -> np.ndarray:

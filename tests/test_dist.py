@@ -181,7 +181,8 @@ def test_strong_split_slots():
     T = bench.MULTI_TILE
     assert parallel.strong_slots(24, 1, 1920, 1080, 256) == 24
     assert parallel.strong_slots(24, 2, 1920, 1080, 256, T) == 48
-    assert parallel.strong_slots(24, 8, 1920, 1080, 256, T) == 192  # no longer capped by a whole-frame budget
+    assert parallel.strong_slots(24, 4, 1920, 1080, 256, T) == 96  # no longer capped by a whole-frame budget
+    assert parallel.strong_slots(24, 8, 1920, 1080, 256, T) == 128  # spp / 2: a slot renders >= 2 samples
     for W, H, base, spp in ((1920, 1080, 24, 256), (3840, 2160, 16, 1024), (4096, 4096, 16, 4096)):
         for world in (2, 4, 8):
             s = parallel.strong_slots(base, world, W, H, spp, T)

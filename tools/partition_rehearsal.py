@@ -28,7 +28,8 @@ def main():
     ap.add_argument("--configs", type=int, nargs="+", default=[2, 4, 5])
     ap.add_argument("--tiles", type=int, nargs="+", default=[64])
     ap.add_argument("--spp", type=int, default=None, help="override every config's spp (C5's 4096 spp frame: ~50 s)")
-    ap.add_argument("--slot-choices", default="strong,base", help="at the smallest tile: strong_slots and/or base")
+    ap.add_argument("--slot-choices", default="strong,base",
+                    help="at the smallest tile: strong_slots and/or base, and explicit counts (e.g. strong,base,96)")
     ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "partition_r05.json"))
     args = ap.parse_args()
@@ -75,6 +76,9 @@ def main():
                 choices.append((tile, parallel.strong_slots(base, world, W, H, spp, tile)))
             if "base" in args.slot_choices and base != choices[-1][1]:
                 choices.append((min(args.tiles), base))
+            for c in args.slot_choices.split(","):  # explicit slot counts at the smallest tile
+                if c.isdigit() and all(int(c) != sl for _, sl in choices):
+                    choices.append((min(args.tiles), int(c)))
             for tile, slots in choices:
                 # bench.py's rank layout: compact path state, film at one slot, the tiles, then the slots
                 pt.set_compact_paths(True)
