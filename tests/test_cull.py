@@ -270,7 +270,7 @@ def test_cull_margins_monotone_and_scale_free(oracle, adv_scenes):
 # with S anywhere or adjacent to T.  At x1e3 no C2 triangle is bounded (|e1||e2| grows against the
 # fixed det threshold 1e-6), at x1e-3 every one is (the walls included).
 FAR_SCENES = [("c2", 1.0), ("c2", 1e-3), ("c3", 1.0), ("c4", 1.0)]
-FAR_RAYS = 1000000
+FAR_RAYS = int(os.environ.get("MCPT_TEST_FAR_RAYS", "1000000"))  # per scene (a soak raises it)
 
 
 @pytest.fixture(scope="module")
