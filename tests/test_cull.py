@@ -431,6 +431,7 @@ def test_gpu_cull_adversarial(mcpt_mod, oracle, request, name, scale, n):
     oracle's cull-free reference traversal on adversarial rays: closest-hit triangle, t, position,
     normal and any-hit visibility bit for bit.  C5 (2 M triangles) runs the 4-wide nodes."""
     s, a = _gpu_scene(mcpt_mod, request, name, scale)
+    n = n * int(os.environ.get("MCPT_TEST_CULL_SCALE", "1"))  # a soak multiplies the ray counts
     ro, rd = adversarial_rays(a, n, seed=23, scale=scale)
     ot, ov = _gpu_vs_oracle(mcpt_mod, oracle, s, a, ro, rd)
     print(f"{name} x{scale}: {n} rays, {(ot >= 0).mean():.3f} hit, {(ov == 0).mean():.3f} occluded, 0 differ")
