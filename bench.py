@@ -61,6 +61,57 @@ B_GEN = 49            # generate per new sample
 BENCH_SLOTS = {1: 16, 2: 24, 3: 64, 4: 24, 5: 24}
 STEP = "frame"  # what one step is; stamped into the PMC summaries (tools/pmc.py)
 
+# MCPT_* environment knobs.  Every one that is set is stamped into the bench
+# line (config.knobs).  These change what is measured -- the culling, the launch geometry, the tree,
+# the occluder table, the library or the rank layout -- so a run with any of them set is marked
+# "not the product" (config.product = false, with the reasons); the rest only select host-side
+# options that do not change a device result or a launch (build threads of the host SAH).
+NON_PRODUCT_KNOBS = {
+    "MCPT_CULL": "culling switched (0: no culling, the reference-order traversal)",
+    "MCPT_CULL_PLANE": "axis-plane culling bound switched",
+    "MCPT_TRACE_WAVES": "k_trace launch geometry (waves per CU)",
+    "MCPT_TRACE_PARTS": "k_trace hand-out partitions",
+    "MCPT_REFILL_MIN": "k_trace refill threshold",
+    "MCPT_TRI_MIN": "k_trace triangle-phase threshold",
+    "MCPT_MAT_BLOCKS_PER_CU": "k_material grid",
+    "MCPT_SHADE_GRID": "k_shade grid",
+    "MCPT_SHADE_WGS": "k_shade grid (absolute)",
+    "MCPT_NO_BLOCK_DONE": "k_shade finished-block skip off",
+    "MCPT_SIBLING_LAYOUT": "BVH sibling layout",
+    "MCPT_BVH_WIDTH": "BVH node width forced",
+    "MCPT_BVH_ISOLATE": "BVH isolation of unbounded triangles switched",
+    "MCPT_GPU_BVH": "device-built BVH instead of the host SAH",
+    "MCPT_ENV_GUIDES": "env CDF search guides switched",
+    "MCPT_OCC_G": "occluder-table origin grid",
+    "MCPT_OCC_B": "occluder-table direction bins",
+    "MCPT_WORK_COUNTERS": "counting k_trace build in the timed frames",
+    "MCPT_LIB": "another libmcpt build",
+    "MCPT_BENCH_SLOTS": "path slots overridden",
+    "MCPT_BENCH_BACKEND": "collective backend overridden (rehearsal)",
+    "MCPT_BENCH_SHARE_GPU": "ranks share one GPU (rehearsal)",
+}
+
+
+def knobs(environ=None):
+    """Every MCPT_* variable set in the environment (they reach the library through getenv)."""
+    env = os.environ if environ is None else environ
+    return {k: env[k] for k in sorted(env) if k.startswith("MCPT_")}
+
+
+def product_check(args, kn):
+    """(product, reasons): whether the line measures the product as shipped -- no knob of
+    NON_PRODUCT_KNOBS set, the config's own spp and path slots."""
+    why = [f"{k}={v}: {NON_PRODUCT_KNOBS[k]}" for k, v in kn.items() if k in NON_PRODUCT_KNOBS]
+    why += [f"{k}={v}: unknown knob" for k, v in kn.items() if k not in NON_PRODUCT_KNOBS and k not in NEUTRAL_KNOBS]
+    if getattr(args, "spp", None):
+        why.append(f"--spp {args.spp}: not the config's spp")
+    if getattr(args, "slots", None) and "MCPT_BENCH_SLOTS" not in kn and args.slots != BENCH_SLOTS.get(args.config):
+        why.append(f"--slots {args.slots}: not the config's path slots ({BENCH_SLOTS.get(args.config)})")
+    return not why, why
+
+
+NEUTRAL_KNOBS = {"MCPT_BVH_THREADS", "MCPT_DIST_TIMEOUT_S"}  # host build threads; the collectives' timeout
+
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
@@ -287,7 +338,7 @@ def roofline(st, ms_trace, ms_shade, config, slots, work=None, spp=None):
     any_q = any_all - occ  # any-hit rays k_trace traced (the occluder cache resolved the rest)
     state = (B_EXT_STATE * ext_q + B_ANY_STATE * any_q) / n
     bvh = (2 * B_NODE * (w.ext_nodes + w.any_nodes) + B_TRI * (w.ext_tests + w.any_tests) + B_HIT * w.ext_hits) / wn
-    achieved = state / avg_s
+    achieved = state / avg_s if avg_s > 0 else 0.0
     names = {"k_trace": ("mcpt_dev::k_trace<",), "shade": ("mcpt_dev::k_shade<", "mcpt_dev::k_material<")}
     summary, stale = pmc_summary(config, slots, spp=spp)
     fresh = summary if stale is None else None
@@ -299,8 +350,8 @@ def roofline(st, ms_trace, ms_shade, config, slots, work=None, spp=None):
             "avg_launch_ms": round(ms_trace / n, 4), "launches": int(n),
             "algorithmic_bytes_per_launch": int(state),
             "algorithmic": "SURVEY 8(d) per-ray state bytes (65 B extension, 33 B any-hit) x rays per launch",
-            "cache_served": {"bytes_per_launch": int(bvh), "GBps": round(bvh / avg_s / 1e9, 1),
-                             "l2_peak_GBps": L2_PEAK / 1e9, "l2_frac": round(bvh / avg_s / L2_PEAK, 4),
+            "cache_served": {"bytes_per_launch": int(bvh), "GBps": round(bvh / avg_s / 1e9, 1) if avg_s > 0 else 0.0,
+                             "l2_peak_GBps": L2_PEAK / 1e9, "l2_frac": round(bvh / avg_s / L2_PEAK, 4) if avg_s > 0 else 0.0,
                              "what": "SURVEY 8(d) B_bvh: 64 B per child-pair node step, 36 B per triangle "
                                      "test, 40 B per closest hit (logical; served by L1/L2/MALL)"},
             "per_ray": {"ext_pair_nodes": round(w.ext_nodes / max(1, w_ext), 2),
@@ -311,18 +362,18 @@ def roofline(st, ms_trace, ms_shade, config, slots, work=None, spp=None):
                         "counted_on": "one extra untimed frame, counting k_trace build" if work is not None
                                       else "the timed frames"}}
     util = {"l2": roof["cache_served"]["l2_frac"]}
-    if traffic is not None:
+    if traffic is not None and avg_s > 0:
         roof["traffic_GBps"] = round(traffic / avg_s / 1e9, 1)
         roof["traffic_frac"] = round(traffic / avg_s / HBM_PEAK, 4)
         util["hbm"] = roof["traffic_frac"]
     else:
         roof["pmc_stale"] = stale
         util["hbm"] = roof["frac"]
-    r = pmc_detail(dfresh, names["k_trace"])
+    r = with_valu_useful(pmc_detail(dfresh, names["k_trace"]))
     if r:
         roof["counters"] = r
-        if "valu_busy" in r:
-            util["valu"] = r["valu_busy"]
+        if "valu_useful" in r:
+            util["valu"] = r["valu_useful"]
     elif dstale:
         roof["counters_stale"] = dstale
     roof["utilisation"] = util
@@ -330,8 +381,9 @@ def roofline(st, ms_trace, ms_shade, config, slots, work=None, spp=None):
     roof["bound"] = top if util[top] >= 0.5 else "latency"
     why = [f"{k} {v:.2f}" for k, v in sorted(util.items(), key=lambda kv: -kv[1])]
     roof["binding"] = (f"utilisation {', '.join(why)}" +
-                       (f"; waves wait on memory {r['wait_frac']:.2f} of their cycles, VALU lane "
-                        f"utilisation {r['lane_util']:.2f}" if r and "wait_frac" in r else ""))
+                       (f" (valu: busy {r['valu_busy']:.2f} x lane utilisation {r['lane_util']:.2f})"
+                        if r and "valu_useful" in r else "") +
+                       (f"; waves wait on memory {r['wait_frac']:.2f} of their cycles" if r and "wait_frac" in r else ""))
     # the streaming stages (logic + generate + material: k_shade and k_material) on their own
     t_shd = ms_shade / n * 1e-3
     b_shd = (B_SHADE * st.shadow_rays + B_GEN * max(0, st.extend_rays - st.shadow_rays)) / n
@@ -341,8 +393,24 @@ def roofline(st, ms_trace, ms_shade, config, slots, work=None, spp=None):
     if shd_traffic is not None and t_shd > 0:
         shade["traffic"] = shd_traffic
         shade["traffic_frac"] = round(shd_traffic / t_shd / HBM_PEAK, 4)
+    per = {k: with_valu_useful(pmc_detail(dfresh, (p,))) for k, p in (("k_shade", "mcpt_dev::k_shade<"),
+                                                                       ("k_material", "mcpt_dev::k_material<"))}
+    per = {k: v for k, v in per.items() if v}
+    if per:
+        shade["counters"] = per
     roof["shade_stages"] = shade
     return roof
+
+
+def with_valu_useful(r):
+    """Counter ratios with valu_useful = valu_busy x lane_util: the share of the VALU's lane-cycles
+    doing a lane's work (busy alone counts an instruction with most lanes masked off as busy)."""
+    if not r:
+        return r
+    r = dict(r)
+    if "valu_busy" in r and "lane_util" in r:
+        r["valu_useful"] = round(r["valu_busy"] * r["lane_util"], 4)
+    return r
 
 
 def trace_phases(work):
@@ -524,14 +592,56 @@ def gather_and_verify(pt, rc, rank, world, dist, spp, args, torch):
                 m[ty * tile:(ty + 1) * tile, tx * tile:(tx + 1) * tile] = True
             ok = ok and bool(np.array_equal(Lg[m].view(np.uint32), Lr[m].view(np.uint32)) and np.array_equal(sg[m], sr[m]))
             covered += int(m.sum())
-        out["gather_equals_one_rank_frame"] = bool(ok and covered == W * H and int(sg.sum()) > 0)
+        out["gather_equals_rerendered_tiles"] = bool(ok and covered == W * H and int(sg.sum()) > 0)
         out["verify"] = "rank 0 re-rendered every other rank's tiles alone; gathered pixels equal bit for bit"
     dist.barrier()
     return out
 
 
-def main():
-    args = parse()
+def make_tracer(local, args, rc, spp):
+    """The product path tracer on device `local` with the config's scene and camera."""
+    import mcpt
+
+    scene = mcpt.build_config_scene(args.config)
+    cam = mcpt.config_camera(rc, rc.width, rc.height)  # the config's view at any N (see docstring)
+    pt = mcpt.PathTracer(local, mcpt.default_config(spp=spp, max_depth=rc.max_depth))
+    # MCPT_GPU_BVH=ploc|lbvh: the device-built tree (A/B of tree quality; films do not depend on the tree)
+    pt.upload_scene(scene, gpu_bvh=os.environ.get("MCPT_GPU_BVH") or False)
+    pt.set_camera(cam)
+    return pt, scene, cam
+
+
+def dist_timeout_s():
+    """Timeout of every collective of an N > 1 run (MCPT_DIST_TIMEOUT_S, default 600 s): a rank that
+    fails or stalls in a step after the timed frames makes the others' collectives raise instead
+    of hanging, so rank 0 still prints the headline line."""
+    return float(os.environ.get("MCPT_DIST_TIMEOUT_S", "600"))
+
+
+def guarded(fn, *a, **kw):
+    """fn's result and None, or None and the error text: a step after the headline's timed frames
+    (the gather, its check, the other split) must not take the already-measured line with it."""
+    try:
+        return fn(*a, **kw), None
+    except Exception as e:  # noqa: BLE001
+        return None, f"{type(e).__name__}: {e}"[:600]
+
+
+def agree(dist, dev, ok, torch):
+    """Every rank's verdict on the step just run (a MIN all-reduce of the ok flags); False on any
+    rank that failed, and wherever the collective itself fails or times out."""
+    try:
+        t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(float(t[0]) > 0.5)
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def main(argv=None, tracer=make_tracer, torch_mod=None):
+    """tracer(local, args, rc, spp) -> (pt, scene, cam) and torch_mod are test seams: the gloo tests
+    run the multi-rank flow on the CPU with a stand-in tracer (tests/test_bench_robust.py)."""
+    args = parse(argv)
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(spawn_ranks(args))
@@ -542,33 +652,37 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
+    if torch_mod is None:
+        import torch
+    else:
+        torch = torch_mod
 
     dist = None
     # MCPT_BENCH_BACKEND=gloo + MCPT_BENCH_SHARE_GPU=1: rehearse the N-rank path on a 1-GPU box
     # (every rank on device local % ndev, host-side collectives); the driver's runs use RCCL.
     backend = os.environ.get("MCPT_BENCH_BACKEND", "nccl")
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
 
         if os.environ.get("MCPT_BENCH_SHARE_GPU") == "1":
             local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
+        timeout = datetime.timedelta(seconds=dist_timeout_s())
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # a timed-out RCCL collective raises in the waiting call (instead of the watchdog
+            # aborting the process), so guarded() can record it and rank 0 still prints its line
+            os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
 
     import mcpt
 
     rc = mcpt.CONFIGS[args.config]
     spp = args.spp or rc.spp
-    scene = mcpt.build_config_scene(args.config)
-    cam = mcpt.config_camera(rc, rc.width, rc.height)  # the config's view at any N (see docstring)
-    pt = mcpt.PathTracer(local, mcpt.default_config(spp=spp, max_depth=rc.max_depth))
-    # MCPT_GPU_BVH=ploc|lbvh: the device-built tree (A/B of tree quality; films do not depend on the tree)
-    pt.upload_scene(scene, gpu_bvh=os.environ.get("MCPT_GPU_BVH") or False)
-    pt.set_camera(cam)
+    pt, scene, cam = tracer(local, args, rc, spp)
 
     # the headline split (value); N = 1: the config's frame on one GPU (both splits are that frame)
     head = run_split(pt, rc, rank, world, dist, backend, args.scaling, spp, args, torch)
@@ -605,23 +719,39 @@ def main():
         work.phases = pt.trace_profile()
         pt.set_work_counters(False)
     per_rank = head["per_rank"]
+    # The steps after the headline's timed frames (the gather and its check, the other split) run
+    # guarded: an error on any rank lands in the line's gather.error / <split>.error, every rank
+    # agrees on it before the next step (which is then skipped), and rank 0 prints the line anyway.
     gather = None
+    extras_ok = True
+    dev = dev_of(backend)
     if dist and args.scaling == "strong" and not args.no_gather:
-        gather = gather_and_verify(pt, rc, rank, world, dist, spp, args, torch)
+        gather, err = guarded(gather_and_verify, pt, rc, rank, world, dist, spp, args, torch)
+        extras_ok = agree(dist, dev, err is None, torch)
+        if err or not extras_ok:
+            gather = {"error": err or "failed on another rank"}
     other = None
     other_kind = "weak" if args.scaling == "strong" else "strong"
     skip_other = args.no_weak if other_kind == "weak" else args.no_strong
     if dist and not skip_other:
-        orun = run_split(pt, rc, rank, world, dist, backend, other_kind, spp, args, torch)
-        orun["spp"] = spp
-        other = split_summary(orun, args, world)
-        if other_kind == "strong" and not args.no_gather:
-            other.update(gather_and_verify(pt, rc, rank, world, dist, spp, args, torch))
+        if not extras_ok:
+            other = {"error": "skipped: the gather failed"}
+        else:
+            orun, err = guarded(run_split, pt, rc, rank, world, dist, backend, other_kind, spp, args, torch)
+            extras_ok = agree(dist, dev, err is None, torch)
+            if err or not extras_ok:
+                other = {"error": err or "failed on another rank"}
+            else:
+                orun["spp"] = spp
+                other = split_summary(orun, args, world)
+                if other_kind == "strong" and not args.no_gather:
+                    g, err = guarded(gather_and_verify, pt, rc, rank, world, dist, spp, args, torch)
+                    extras_ok = agree(dist, dev, err is None, torch)
+                    other.update(g if err is None and extras_ok else {"gather_error": err or "failed on another rank"})
 
     if rank != 0:
         if dist:
-            dist.barrier()
-            dist.destroy_process_group()
+            finish_dist(dist)
         return
 
     K = args.steps
@@ -635,6 +765,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(scene.arrays(), cam, W, H, args.cpu_spp, rc.max_depth)
     value = rays_all / dt_all / 1e6
+    kn = knobs()
+    prod, not_prod = product_check(args, kn)
     names = {2: "Cornell-box + 5 spheres proxy (scene_show_off_spheres.glb missing), night_free_Env.hdr",
              3: "deep-BVH proxy, 871,416 tris (scene_show_off_dragon.glb missing), night_free_Env.hdr",
              4: "Suzanne x2 Loop-subdivided, 251,904 tris (scene_show_off_head.glb missing), HDR_029",
@@ -688,11 +820,16 @@ def main():
             "path_slots": slots,
             "occluder_cache": pt.occ_stats()[1],  # any-hit occluder cache: same results
             "device": pt.device_name,
+            "knobs": kn,  # every MCPT_* variable set (see NON_PRODUCT_KNOBS)
+            "product": prod,
         },
         "stage_ms_per_step": {"k_trace": round(st.ms_extend / K, 3), "k_shade+k_material": round(st.ms_shade / K, 3)},
         "roofline": roof,
         "cpu_baseline": cpu,
     }
+    if not prod:
+        out["config"]["not_product"] = not_prod
+        out["config"]["workload"] += " [NOT THE PRODUCT: " + "; ".join(not_prod) + "]"
     if steady:
         out["steady_state"] = {"mray_s": round(steady[1] / steady[0] / 1e6, 2),
                                "ms_per_iteration": round(steady[0] * 1e3 / 60, 4),
@@ -708,8 +845,16 @@ def main():
     print(json.dumps(out), flush=True)
     pt.close()
     if dist:
+        finish_dist(dist)
+
+
+def finish_dist(dist):
+    """Final barrier and teardown; after a failed step either may raise (the line is printed)."""
+    try:
         dist.barrier()
         dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        print(f"bench.py: process group teardown: {type(e).__name__}: {e}", file=sys.stderr)
 
 
 if __name__ == "__main__":

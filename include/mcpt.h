@@ -239,7 +239,9 @@ int mcpt_film_pack_tiles(mcpt_ctx *ctx, void *d_out, uint32_t *npix);       /* t
 /* The inverse on the gathering rank: scatter another rank's packed tile pixels (device memory on
  * ctx's GPU, 16 B/px in the order mcpt_film_pack_tiles wrote them for tiles tile_xy[0..ntiles))
  * into ctx's film accumulators.  The tiles must not be ctx's own (their other path slots would
- * be added in).  Synchronous. */
+ * be added in), and until the next film clear they cannot become ctx's own either: mcpt_set_tiles
+ * rejects a set holding one (MCPT_E_INVALID; the compact layout's set_tiles clears the film
+ * anyway).  Synchronous. */
 int mcpt_film_unpack_tiles(mcpt_ctx *ctx, const void *d_in, const uint32_t *tile_xy, uint32_t ntiles);
 int mcpt_film_tonemap_rgba8(mcpt_ctx *ctx, float exposure, uint8_t *out);   /* == draw_to_surface */
 int mcpt_film_size(const mcpt_ctx *ctx, uint32_t *w, uint32_t *h);

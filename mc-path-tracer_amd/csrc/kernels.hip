@@ -1995,15 +1995,19 @@ void launch_occ_records(const DevScene& sc, uint32_t nnodes, float4* rec, hipStr
     hipLaunchKernelGGL(k_occ_records, dim3(nnodes / 256 + 1), dim3(256), 0, s, sc, nnodes, rec);
 }
 void launch_clear(const ClearArgs& a, hipStream_t s) {
+    if (a.n == 0) return;  // an empty tile set (compact layout): nothing to launch, no zero-sized grid
     hipLaunchKernelGGL(k_clear, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s) {
+    if (a.n == 0) return;
     hipLaunchKernelGGL(k_hit_record, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 void launch_resolve(const ResolveArgs& a, hipStream_t s) {
+    if (a.n == 0) return;
     hipLaunchKernelGGL(k_resolve, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 void launch_tonemap(const TonemapArgs& a, hipStream_t s) {
+    if (a.n == 0) return;
     hipLaunchKernelGGL(k_tonemap, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 void launch_accumulate(CounterBlock* c, uint32_t nparts, uint32_t* occ_gate, hipStream_t s) {
@@ -2016,6 +2020,7 @@ void launch_unpack(const UnpackArgs& a, hipStream_t s) {
 }
 void launch_pack(const PackArgs& a, hipStream_t s) {
     uint32_t n = (uint32_t)(a.ntiles * a.tile_w * a.tile_h);
+    if (n == 0) return;
     hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, s, a);
 }
 

@@ -82,6 +82,10 @@ struct mcpt_ctx {
     int2* step_tile_h = nullptr;       // the tile, then its index in the tile set, ShadeArgs::tile_base)
     int2* tiles = nullptr;
     std::vector<int2> tiles_h;
+    // tiles holding pixels scattered in from another context (mcpt_film_unpack_tiles, mcpt_gather)
+    // since the last film clear: the full layout's slot 0 holds them, so they may not become own
+    // tiles before a clear (their sample count restarts from the flags word while Ld accumulates)
+    std::vector<int2> unpacked;
     uint32_t tiles_cap = 0;
     std::vector<hipEvent_t> events;
     // stage_run scratch
@@ -862,6 +866,7 @@ int mcpt_film_clear(mcpt_ctx* c) {
         HIPCHK(c, hipMemsetAsync(c->scene.occ_gate, 0, 2 * sizeof(uint32_t), c->stream));
     }
     c->film_stale = false;
+    c->unpacked.clear();
     HIPCHK(c, hipMemsetAsync(c->cnt, 0, sizeof(CounterBlock), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     memset(&c->totals, 0, sizeof(c->totals));  // the counters are now zero on the device too
@@ -947,17 +952,35 @@ int mcpt_film_resize(mcpt_ctx* c, uint32_t w, uint32_t h, uint32_t tw, uint32_t 
 
 // A new tile set.  In the compact layout the path state follows the tile set: it is re-allocated and
 // the film cleared (a tile listed twice would share its paths: rejected).
+static bool has_tile(const std::vector<int2>& v, int2 t) {
+    for (const int2& o : v)
+        if (o.x == t.x && o.y == t.y) return true;
+    return false;
+}
 static int set_tiles_checked(mcpt_ctx* c, const std::vector<int2>& t) {
-    if (!c->compact) return set_tiles_internal(c, t);
+    if (!c->compact) {
+        for (const int2& x : t)
+            if (has_tile(c->unpacked, x))
+                return set_err(c, MCPT_E_INVALID, "a tile of the set holds pixels unpacked from another context: clear the film first");
+        return set_tiles_internal(c, t);
+    }
     for (size_t i = 0; i < t.size(); i++)
         for (size_t j = 0; j < i; j++)
             if (t[i].x == t[j].x && t[i].y == t[j].y)
                 return set_err(c, MCPT_E_INVALID, "compact paths: a tile is listed twice");
+    const std::vector<int2> old = c->tiles_h;
     int rc = set_tiles_internal(c, t);
     if (rc) return rc;
     const size_t P = c->P;
     c->P = 0;  // the film is not allocated until the new path state is
-    if ((rc = alloc_film_state(c))) return rc;
+    if ((rc = alloc_film_state(c))) {  // e.g. out of memory: back to the previous tile set, as
+        const std::string err = c->err;  // mcpt_set_path_slots / mcpt_set_compact_paths do
+        if (set_tiles_internal(c, old) == MCPT_OK && alloc_film_state(c) == MCPT_OK) {
+            c->P = P;
+            (void)mcpt_film_clear(c);
+        }
+        return set_err(c, rc, err);
+    }
     c->P = P;
     return mcpt_film_clear(c);
 }
@@ -1656,8 +1679,8 @@ int mcpt_film_unpack_tiles(mcpt_ctx* c, const void* d_in, const uint32_t* xy, ui
     for (uint32_t i = 0; i < n; i++) {
         if (xy[2 * i] >= nx || xy[2 * i + 1] >= ny) return set_err(c, MCPT_E_INVALID, "tile out of range");
         t[i] = make_int2((int)xy[2 * i], (int)xy[2 * i + 1]);
-        for (const int2& o : c->tiles_h)  // the context's own pixels would mix with its other slots
-            if (o.x == t[i].x && o.y == t[i].y) return set_err(c, MCPT_E_INVALID, "unpack into one of the context's own tiles");
+        if (has_tile(c->tiles_h, t[i]))  // the context's own pixels would mix with its other slots
+            return set_err(c, MCPT_E_INVALID, "unpack into one of the context's own tiles");
     }
     HIPCHK(c, hipSetDevice(c->device));
     int2* dt = nullptr;
@@ -1677,6 +1700,8 @@ int mcpt_film_unpack_tiles(mcpt_ctx* c, const void* d_in, const uint32_t* xy, ui
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(dt);
     if (e != hipSuccess) return set_err(c, MCPT_E_HIP, std::string("unpack: ") + hipGetErrorString(e));
+    for (const int2& x : t)
+        if (!has_tile(c->unpacked, x)) c->unpacked.push_back(x);
     return MCPT_OK;
 }
 
@@ -1697,6 +1722,9 @@ int mcpt_gather(mcpt_ctx* const* ctxs, int32_t n, int32_t root) {
             return set_err(R, MCPT_E_INVALID, "gather: film or tile sizes differ between contexts");
         for (int32_t j = 0; j < i; j++)
             if (ctxs[j] == c) return set_err(R, MCPT_E_INVALID, "gather: a context is listed twice");
+        if (c != R)
+            for (const int2& x : c->tiles_h)
+                if (has_tile(R->tiles_h, x)) return set_err(R, MCPT_E_INVALID, "gather: a tile set overlaps the root's own tiles");
     }
     for (int32_t i = 0; i < n; i++) {
         mcpt_ctx* c = ctxs[i];
@@ -1747,6 +1775,8 @@ int mcpt_gather(mcpt_ctx* const* ctxs, int32_t n, int32_t root) {
         (void)hipSetDevice(c->device);
         (void)hipFree(src);
         if (e != hipSuccess) return set_err(R, MCPT_E_HIP, std::string("gather: ") + hipGetErrorString(e));
+        for (const int2& x : c->tiles_h)
+            if (!has_tile(R->unpacked, x)) R->unpacked.push_back(x);
     }
     (void)hipSetDevice(R->device);
     return MCPT_OK;

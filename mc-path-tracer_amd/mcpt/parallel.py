@@ -38,16 +38,18 @@ def rank_path_pixels(world, W, H, tile):
     return max(len(tiles_for_rank(r, world, W, H, tile)) for r in range(world)) * tile * tile
 
 
-def strong_slots(base_slots, world, W, H, spp, tile=64, budget=None):
+def strong_slots(base_slots, world, W, H, spp, tile, budget=None):
     """Path slots for a frame split over `world` ranks: every rank keeps the paths in flight of the
     one-GPU run (base_slots x W x H) over its 1/world of the pixels, so slots scale with world --
     bounded by spp / 2 (a slot renders >= 2 samples: config 2 at N = 8 ran 43.4 ms per rank frame at
     128 slots against 44.7 at 192, whose 1.3 samples per slot leave a long tail;
     profiles/partition_r05_c2_slots.json), by the ABI's 256 and by fewer than 2^31 paths of the
     rank's own path state (compact layout: its tiles only); `budget` (bytes of path state per GPU)
-    caps them further when given.  Never below base_slots.  One value for every rank: the slot count sets the film's
-    summation order, so the gathered frame then equals a one-rank frame rendered with the same slots
-    bit for bit."""
+    caps them further when given.  Not below base_slots unless the 2^31-path cap or the budget binds
+    (then the cap).  `tile` is the partition's tile edge (tiles_for_rank's): no default, so the
+    slots are sized for the partition the caller renders.  One value for every rank: the slot count
+    sets the film's summation order, so the gathered frame then equals a one-rank frame rendered
+    with the same slots bit for bit."""
     px = rank_path_pixels(world, W, H, tile) if world > 1 else W * H
     cap = max(1, ((1 << 31) - 1) // px)
     if budget is not None:

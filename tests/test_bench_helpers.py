@@ -92,7 +92,18 @@ def test_roofline_fields_never_exceed_one_and_bound_is_derived(tmp_path, monkeyp
             "ratios": {"valu_busy": 0.78, "wait_frac": 0.57, "lane_util": 0.5}}}}))
     r = bench.roofline(st, 7.2, 4.4, 2, 3)
     assert r["traffic"] == 420_000_000 and abs(r["traffic_frac"] - 420e6 / 0.72e-3 / 8e12) < 1e-4
-    assert r["bound"] == "valu" and r["utilisation"]["valu"] == 0.78 and "wait on memory 0.57" in r["binding"]
+    # the VALU is judged by its useful share, busy x lane utilisation: 0.39, so no
+    # resource reaches half its roof here
+    assert r["counters"]["valu_useful"] == 0.39 and r["utilisation"]["valu"] == 0.39 and r["bound"] == "latency"
+    assert "wait on memory 0.57" in r["binding"] and "busy 0.78 x lane utilisation 0.50" in r["binding"]
+    (prof / "pmcdetail_r03.json").write_text(json.dumps({"stamp": _stamp(), "kernels": {
+        "void mcpt_dev::k_trace<2, 8>(mcpt_dev::TraceArgs)": {"ratios": {"valu_busy": 0.9, "lane_util": 0.8}},
+        "void mcpt_dev::k_shade<false>(mcpt_dev::ShadeArgs)": {"ratios": {"valu_busy": 0.7, "lane_util": 0.5}},
+        "void mcpt_dev::k_material<false>(mcpt_dev::ShadeArgs)": {"ratios": {"valu_busy": 0.8, "lane_util": 0.75}}}}))
+    r = bench.roofline(st, 7.2, 4.4, 2, 3)
+    assert r["bound"] == "valu" and r["utilisation"]["valu"] == 0.72
+    assert r["shade_stages"]["counters"]["k_shade"]["valu_useful"] == 0.35
+    assert r["shade_stages"]["counters"]["k_material"]["valu_useful"] == 0.6
     assert r["shade_stages"]["traffic"] == 1_600_000_000
     for k in ("frac", "traffic_frac"):
         assert r[k] <= 1
@@ -151,3 +162,28 @@ def test_pmc_lookup_skips_the_counting_instantiation():
     assert bench.pmc_traffic(s, ("mcpt_dev::k_trace<",)) == 100
     assert bench.pmc_detail(s, ("mcpt_dev::k_trace<",)) == {"a": 1}
     assert bench.pmc_traffic(s, ("mcpt_dev::k_material<",)) == 7  # quality mode's <true> is a timed kernel
+
+
+def test_knobs_are_stamped_and_judged():
+    """Every MCPT_* variable is stamped into the line; one that changes the measured kernels, their
+    launch or the layout marks the line as not the product (VERDICT r5 next #6)."""
+    a = bench.parse([])
+    assert bench.product_check(a, bench.knobs({})) == (True, [])
+    kn = bench.knobs({"MCPT_CULL": "0", "PATH": "/bin", "MCPT_BVH_THREADS": "4"})
+    assert kn == {"MCPT_BVH_THREADS": "4", "MCPT_CULL": "0"}
+    ok, why = bench.product_check(a, kn)
+    assert not ok and len(why) == 1 and why[0].startswith("MCPT_CULL=0")
+    ok, why = bench.product_check(a, bench.knobs({"MCPT_TRACE_WAVES": "20", "MCPT_NEW_THING": "1"}))
+    assert not ok and any("launch geometry" in w for w in why) and any("unknown knob" in w for w in why)
+    assert not bench.product_check(bench.parse(["--spp", "64"]), {})[0]
+    assert not bench.product_check(bench.parse(["--slots", "16"]), {})[0]
+    assert bench.product_check(bench.parse(["--slots", "24"]), {})[0]  # the config's own
+    # every knob the library reads through getenv is classified
+    import re
+
+    src = ""
+    for root, _, files in os.walk(os.path.join(REPO, "mc-path-tracer_amd", "csrc")):
+        for f in files:
+            src += open(os.path.join(root, f)).read()
+    read = set(re.findall(r'getenv\("(MCPT_[A-Z0-9_]+)"', src)) | set(re.findall(r'env_u32\("(MCPT_[A-Z0-9_]+)"', src))
+    assert read and read <= set(bench.NON_PRODUCT_KNOBS) | bench.NEUTRAL_KNOBS, read - set(bench.NON_PRODUCT_KNOBS)

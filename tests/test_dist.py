@@ -179,7 +179,7 @@ def test_strong_split_slots():
     import bench
 
     T = bench.MULTI_TILE
-    assert parallel.strong_slots(24, 1, 1920, 1080, 256) == 24
+    assert parallel.strong_slots(24, 1, 1920, 1080, 256, 256) == 24
     assert parallel.strong_slots(24, 2, 1920, 1080, 256, T) == 48
     assert parallel.strong_slots(24, 4, 1920, 1080, 256, T) == 96  # no longer capped by a whole-frame budget
     assert parallel.strong_slots(24, 8, 1920, 1080, 256, T) == 128  # spp / 2: a slot renders >= 2 samples
@@ -193,6 +193,8 @@ def test_strong_split_slots():
     assert parallel.strong_slots(16, 8, 4096, 4096, 4096, T) == 128
     assert parallel.strong_slots(16, 8, 4096, 4096, 4096, T, budget=16 << 30) < 128
     assert parallel.strong_slots(16, 8, 256, 256, 16, T) == 16  # spp bound: a slot renders at least one sample
+    # the 2^31-path cap binds before base_slots: a 46341^2-pixel frame holds < 2 slots
+    assert parallel.strong_slots(4, 1, 46341, 46341, 64, 256) == 1
     a = bench.parse(["--gpus", "8", "--no-gather"])
     assert a.no_gather and not a.no_strong and not a.no_weak and not a.no_verify_gather and a.scaling == "strong"
 

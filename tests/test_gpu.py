@@ -872,6 +872,47 @@ def test_native_gather_equals_one_pass(mcpt_mod, scene_c2, slots, compact):
         pt.close()
 
 
+@pytest.mark.parametrize("compact", [False, True])
+def test_native_gather_with_a_context_without_tiles(mcpt_mod, scene_c2, compact):
+    """More contexts than tiles: a 2 x 1-tile film over three contexts leaves the third
+    with an empty tile set.  In the compact layout its path state is empty, and set_tiles, film
+    clears, the film readers and render launch nothing (no zero-sized grid).  The gather still
+    equals the one-context frame bit for bit.  Tiles gathered into the root cannot become its own
+    before a film clear (their sample counts would restart while their radiance accumulates)."""
+    from mcpt import parallel
+
+    rc = mcpt_mod.CONFIGS[2]
+    W, H, T = 100, 50, 64
+    cam = mcpt_mod.config_camera(rc, W, H)
+    full = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)
+    full.set_path_slots(2)
+    full.render()
+    L_full, s_full = full.film()
+    parts = []
+    for r in range(3):
+        pt = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 2, 5, tile=T)
+        if compact:
+            pt.set_compact_paths(True)
+        pt.set_path_slots(2)
+        pt.set_tiles(parallel.tiles_for_rank(r, 3, W, H, T))
+        pt.clear()
+        pt.render()
+        parts.append(pt)
+    assert parallel.tiles_for_rank(2, 3, W, H, T) == []
+    L2, s2 = parts[2].film()  # the empty context's film: all zero
+    assert not s2.any() and not L2.any()
+    mcpt_mod.gather(parts, root=0)
+    L, s = parts[0].film()
+    assert np.array_equal(s, s_full) and np.array_equal(L.view(np.uint32), L_full.view(np.uint32))
+    if not compact:
+        with pytest.raises(mcpt_mod.McptError):
+            parts[0].set_tiles([(0, 0), (1, 0)])  # (1, 0) holds pixels gathered from context 1
+        parts[0].clear()
+        parts[0].set_tiles([(0, 0), (1, 0)])
+    for pt in parts + [full]:
+        pt.close()
+
+
 @pytest.mark.parametrize("shade_wgs", [None, "2"])
 def test_compact_paths_layout(mcpt_mod, scene_c2, shade_wgs, monkeypatch):
     """mcpt_set_compact_paths: path state over the tile set only (a multi-GPU rank's 1/N).  Films are
