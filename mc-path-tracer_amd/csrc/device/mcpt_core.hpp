@@ -703,7 +703,11 @@ MCPT_HD void concentric_disk(const Rng& r, float& dx, float& dy) {  // Sample.cu
     dx = rr * ct;
     dy = rr * st;
 }
-MCPT_HD void gen_ray(const CamView& c, int W, int H, int xi, int yi, const Rng& r, V3& o, V3& d) {
+// dCamera::gen_ray in two parts.  gen_ray_pixel: everything that depends on the pixel alone (the
+// pinhole ray through it: the fp64 NDC island, both unprojections, the direction); k_cam_table
+// evaluates it once per pixel of the film.  gen_ray_lens: the per-sample thin-lens part from the
+// pixel's focal point (two RNG draws).  gen_ray = the two in sequence, the same operations.
+MCPT_HD void gen_ray_pixel(const CamView& c, int W, int H, int xi, int yi, V3& o, V3& d) {
     float x = (float)xi, y = (float)yi;
     float px = (float)(2.f * (((double)x + 0.5) / (double)(float)W) - 1.f);  // fp64 island :21-22
     float py = (float)(1.f - 2.f * (((double)y + 0.5) / (double)(float)H));
@@ -714,18 +718,22 @@ MCPT_HD void gen_ray(const CamView& c, int W, int H, int xi, int yi, const Rng& 
     V3 pFar = v3(af[0], af[1], af[2]) / af[3];
     o = pNear;
     d = normalize(pFar - pNear);
-    if (c.lens_radius > 0.f) {
-        V3 pFocal = o + d * c.focal;
-        float lx, ly;
-        concentric_disk(r, lx, ly);
-        lx = lx * c.lens_radius;
-        ly = ly * c.lens_radius;
-        float al[4];
-        mat_vec4(c.iv, lx, ly, 0.f, 1.f, al);
-        V3 pLens = v3(al[0], al[1], al[2]) / al[3];
-        o = pLens;
-        d = normalize(pFocal - o);
-    }
+}
+MCPT_HD V3 gen_ray_focal(const CamView& c, V3 o, V3 d) { return o + d * c.focal; }  // pFocal (:34)
+MCPT_HD void gen_ray_lens(const CamView& c, V3 pFocal, const Rng& r, V3& o, V3& d) {
+    float lx, ly;
+    concentric_disk(r, lx, ly);
+    lx = lx * c.lens_radius;
+    ly = ly * c.lens_radius;
+    float al[4];
+    mat_vec4(c.iv, lx, ly, 0.f, 1.f, al);
+    V3 pLens = v3(al[0], al[1], al[2]) / al[3];
+    o = pLens;
+    d = normalize(pFocal - o);
+}
+MCPT_HD void gen_ray(const CamView& c, int W, int H, int xi, int yi, const Rng& r, V3& o, V3& d) {
+    gen_ray_pixel(c, W, H, xi, yi, o, d);
+    if (c.lens_radius > 0.f) gen_ray_lens(c, gen_ray_focal(c, o, d), r, o, d);
 }
 
 // ---------------------------------------------------------------------------

@@ -580,6 +580,51 @@ __device__ inline void material_brdf_terms(const ShadeArgs& a, uint32_t pid, con
     st_s(a.p.flags + pid, nf);
 }
 
+// Diagnostics of k_shade's instruction attribution, off in the product:
+//  * -DMCPT_ISA_MARKERS: assembly comments at the section boundaries (tools/isa_sections.py counts the
+//    VALU instructions between them in hipcc -S output);
+//  * -DMCPT_DIAG_SHADE: per-section wave entries and active lanes, summed over a run in a device
+//    global (mcpt_debug_shade_sections reads it).
+#ifdef MCPT_ISA_MARKERS
+#define MCPT_MARK(name) __asm__ volatile("; MCPT_SEC " name)
+#else
+#define MCPT_MARK(name) \
+    do {                \
+    } while (0)
+#endif
+enum : int { SD_WAVES = 0, SD_VALID, SD_LOGIC, SD_NEE, SD_GEN, SD_CONT, SD_BG, SD_N };
+#ifdef MCPT_DIAG_SHADE
+__device__ unsigned long long g_shade_diag[2 * SD_N];
+#define SHADE_DIAG(k, cond)                                                      \
+    do {                                                                         \
+        const uint64_t m_ = __ballot(cond);                                      \
+        if ((threadIdx.x & 63) == 0 && m_) {                                     \
+            atomicAdd(&g_shade_diag[2 * (k)], 1ull);                             \
+            atomicAdd(&g_shade_diag[2 * (k) + 1], (unsigned long long)__popcll(m_)); \
+        }                                                                        \
+    } while (0)
+#else
+#define SHADE_DIAG(k, cond) \
+    do {                    \
+    } while (0)
+#endif
+int shade_sections(unsigned long long* out, int n, int reset) {
+#ifdef MCPT_DIAG_SHADE
+    unsigned long long h[2 * SD_N];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_shade_diag), sizeof(h)) != hipSuccess) return -1;
+    for (int i = 0; i < n && i < 2 * SD_N; i++) out[i] = h[i];
+    if (reset) {
+        memset(h, 0, sizeof(h));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_shade_diag), h, sizeof(h)) != hipSuccess) return -1;
+    }
+    return 2 * SD_N;
+#else
+    for (int i = 0; i < n; i++) out[i] = 0;
+    (void)reset;
+    return 0;
+#endif
+}
+
 // k_shade: 8 waves per SIMD (<= 64 VGPRs; the virtual-block loop left alone allocates 67, no spill at 64)
 #ifndef MCPT_SHADE_WPE
 #define MCPT_SHADE_WPE 8
@@ -638,7 +683,10 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
         pid = (uint32_t)slot * a.npx + local;
     }
     // ---- phase 1: logic + generate (one thread per pixel)
+    MCPT_MARK("load");
     bool gen_ext = false, gen_trivial = false, cont = false;
+    bool d_logic = false, d_nee = false, d_gen = false;  // (MCPT_DIAG_SHADE)
+    (void)d_logic; (void)d_nee; (void)d_gen;
     uint32_t cont_len = 0, cont_sidx = 0;
     int32_t cont_htri = -1;
     V3 beta_store = v3(0.f, 0.f, 0.f);
@@ -679,6 +727,9 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
         uint32_t sidx = fl >> F_SIDX_SHIFT;
         uint32_t samples = a.slots > 1 ? (sidx - (uint32_t)slot) / (uint32_t)a.slots : sidx;
         if (!dead && sidx < spp) {  // wavefront_kernels.cu:124
+            MCPT_MARK("logic");
+            d_logic = true;
+            d_nee = need_nee;
             const Rng r{rng_key(a.seed, pix, sidx), len};
             const bool found = htri >= 0;
             const V3 B = len == 1 ? v3(1.f, 1.f, 1.f) : xyz(b4);  // wf_generate's beta (:245)
@@ -742,6 +793,8 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
         uint32_t nflags = fl;
         if (dead) nflags = F_DEAD | (sidx << F_SIDX_SHIFT);
         if (dead && sidx < spp) {  // :219-222 + wf_generate (:225-251)
+            MCPT_MARK("generate");
+            d_gen = true;
             const Rng r0{rng_key(a.seed, pix, sidx), 0u};
             V3 new_o, new_d;
             gen_ray(a.cam, a.W, a.H, x, y, r0, new_o, new_d);
@@ -756,9 +809,18 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
                 gen_trivial = true;
             }
         }
+        MCPT_MARK("flags");
         if (!cont && nflags != fl) st_s(a.p.flags + pid, nflags);  // continuing paths: written by material()
         finished = dead && !(sidx < spp);
     }
+    SHADE_DIAG(SD_WAVES, true);
+    SHADE_DIAG(SD_VALID, valid);
+    SHADE_DIAG(SD_LOGIC, d_logic);
+    SHADE_DIAG(SD_NEE, d_nee);
+    SHADE_DIAG(SD_GEN, d_gen);
+    SHADE_DIAG(SD_CONT, cont);
+    SHADE_DIAG(SD_BG, bg);
+    MCPT_MARK("push");
     // ---- pushes: generated extension rays and continuing paths (material queue); one
     // atomic per block and queue.  A continuing path's record and updated throughput go
     // to k_material densely (it writes p.beta with f_s/pdf_s in .w).
@@ -779,6 +841,7 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
     uint32_t n_ext = (gen_ext || gen_trivial) ? 1u : 0u;  // queued + resolved-in-place rays
     for (int off = 32; off > 0; off >>= 1) n_ext += __shfl_xor(n_ext, off);
     if (lane == 0 && n_ext) atomicAdd(sc_ctr + C_EXT_RAYS, n_ext);
+    MCPT_MARK("background");
     if (bg) {  // wavefront_kernels.cu:129-140, len 1 and no hit: beta is (1,1,1)
         const int nbg = FIXED ? 1 : sc.nlights;  // the reference adds it once per light (A.4)
         V3 film = bg_film;
@@ -787,7 +850,9 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
             __float_as_uint(film.z) != __float_as_uint(bg_film.z))
             a.p.Ld[pid] = f4(film, 0.f);
     }
+    MCPT_MARK("done");
     if (a.blk_done && __syncthreads_and(finished ? 1 : 0) && threadIdx.x == 0) a.blk_done[done_idx] = 1;
+    MCPT_MARK("end");
 }
 
 // k_shade: a bounded grid of G blocks; block b runs shading blocks b, b + G, b + 2G, ... (at most
@@ -989,6 +1054,19 @@ __device__ inline void wave_stats(uint32_t* stats, int lane, uint32_t nodes, uin
 #ifndef MCPT_NODE_STEPS
 #define MCPT_NODE_STEPS 4
 #endif
+// Shared triangle phase (MCPT_TRI_SHARE=1; measured and not kept): a triangle
+// phase tests every triangle of every parked leaf of the wave, dealt over all 64 lanes (a lane tests
+// another lane's ray against one of that lane's triangles), instead of one triangle per lane holding
+// a leaf.  Parity held (110 GPU tests), but config 2's k_trace went 2.47 -> 2.79 ms per launch: a
+// phase finds 36 triangles in the wave's parked leaves on average (6.91 G tests in 190 M phases,
+// the same with and without sharing), so one round per phase does the same tests with the owner
+// search and ray exchange on top; the lanes without a leaf at a phase are traversing, not waiting
+// on another lane's leaf.  Applies to the instantiations with an LDS stack of <= kShareMaxStack
+// entries (its 512-B result slots per wave would cost the deep-stack kernels a resident wave per CU).
+#ifndef MCPT_TRI_SHARE
+#define MCPT_TRI_SHARE 0
+#endif
+constexpr int kShareMaxStack = 8;
 constexpr int kNodeSteps = MCPT_NODE_STEPS;
 #ifndef MCPT_GRAB_MAX
 #define MCPT_GRAB_MAX 0
@@ -1042,7 +1120,11 @@ constexpr bool kAnyFirst = MCPT_ANY_FIRST != 0;
 template <int kW, int kLdsStack, bool kCount>
 __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs a) {
     if (a.idle && *a.idle) return;  // the tile set is complete
+    constexpr bool kShare = MCPT_TRI_SHARE != 0 && kLdsStack <= kShareMaxStack;
     __shared__ int2 stk[kLdsStack][kTraceBlock];
+    // shared triangle phase: each lane's best (t, scene id, leaf position) key, min-combined by the
+    // lanes testing its triangles
+    __shared__ uint64_t s_key[kShare ? kTraceBlock : 1];
     const int lane = threadIdx.x;
     // ---- work distribution.  The queue shards are split into nparts partitions
     // (shard s -> partition s mod nparts; by default one per XCD) and each partition's
@@ -1149,6 +1231,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     // below +-0); io: the ray's signed culling scale (cull_iota; |io| = inf: an infinite inverse
     // component, the slab() path)
     float best = K_HUGE, cut = K_HUGE, io = K_INF_F;
+    uint32_t bsid = 0;  // shared triangle phase: scene id of the closest hit so far (tri >= 0)
     int2 spill[kMaxStack - kLdsStack];
     // Pop the next entry still in front of the current cut (any-hit rays keep
     // cut = +inf, so for them every entry is taken).
@@ -1440,7 +1523,85 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         // leaf, or no lane has node work left, each parked leaf tests one triangle
         const uint32_t n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
         const uint32_t n_node = (uint32_t)__popcll(__ballot(act && ref >= 0));
-        if (n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node)) {
+        if constexpr (kShare) {
+          if (n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node)) {
+            // ---- shared triangle phase: the wave's parked leaves hold T triangles in all; lane
+            // segment [excl, excl + cnt) of positions 0..T-1 is its leaf's, and position p is tested
+            // by lane p mod 64 in round p / 64 against the segment owner's ray.  A test that accepts
+            // min-combines the key (t, scene id, position in the leaf) into the owner's LDS slot:
+            // the closest hit keeps the smallest t with ties to the lower scene id, exactly as the
+            // one-at-a-time loop (Triangle.cu:174-179; the order of tests does not matter), and an
+            // any-hit ray takes any acceptance (Triangle.cu:222-224).  t is the same value and
+            // non-negative (-0 made +0, which compares equal), so its bits order as the floats.
+            const bool own = leaf != kEnd;
+            const uint32_t cnt = own ? (((uint32_t)leaf >> 24) & 7u) + 1u : 0u;
+            const uint32_t incl = wave_scan_incl(cnt);
+            const uint32_t excl = incl - cnt;
+            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+            // the owner's current best: any hit: none; closest hit: (best, its scene id, 7), or
+            // (K_HUGE, 0) without a hit, so that t == K_HUGE is rejected as by t < best
+            const uint64_t init = !own || best < 0.f
+                                      ? ~0ull
+                                      : ((uint64_t)__float_as_uint(best) << 32) | (tri >= 0 ? (bsid << 3) | 7u : 0u);
+            s_key[lane] = init;
+            __syncthreads();  // (one wave: orders the LDS writes before the other lanes' atomics)
+            if constexpr (kCount) {
+                if (own) tot_t += cnt;
+                ph[PH_TRI_LANES] += total;
+            }
+#pragma unroll 1
+            for (uint32_t base = 0; base < total; base += 64u) {
+                if constexpr (kCount) ph[PH_TRI_PHASES]++;
+                const uint32_t p = base + (uint32_t)lane;
+                // owner: the last lane whose segment starts at or before p (excl is non-decreasing;
+                // lanes after the owner start past p, empty segments before it do not matter)
+                uint32_t ow = 0;
+#pragma unroll
+                for (uint32_t sh = 32; sh > 0; sh >>= 1) {
+                    const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ow + sh) << 2), (int)excl);
+                    if (e <= p) ow += sh;
+                }
+                const int oa = (int)(ow << 2);
+                const uint32_t k = p - (uint32_t)__builtin_amdgcn_ds_bpermute(oa, (int)excl);
+                const int oleaf = __builtin_amdgcn_ds_bpermute(oa, leaf);
+                const V3 po = v3(__int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(o.x))),
+                                 __int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(o.y))),
+                                 __int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(o.z))));
+                const V3 pd = v3(__int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(d.x))),
+                                 __int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(d.y))),
+                                 __int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(d.z))));
+                if (p < total) {
+                    const int id = (oleaf & 0xffffff) + (int)k;
+                    const float4* tp = sc.tri + kTriF4 * id;
+                    const float4 w0 = tp[0], w1 = tp[1], w2 = tp[2];
+                    __asm__ volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z),
+                                     "v"(w1.w), "v"(w2.x), "v"(w2.y));
+                    float t;
+                    if (tri_test_t(po, pd, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t) &&
+                        !(t < 0.f) && t < K_HUGE) {
+                        const uint64_t key = ((uint64_t)__float_as_uint(t + 0.f) << 32) |
+                                             (((uint32_t)__float_as_int(w2.y) << 3) | k);
+                        __hip_atomic_fetch_min(&s_key[ow], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            }
+            __syncthreads();  // the atomics before the owners' reads
+            if (own) {
+                const uint64_t key = s_key[lane];
+                if (key < init) {
+                    tri = (leaf & 0xffffff) + (int)(key & 7u);
+                    if (best < 0.f) {
+                        ref = kEnd;  // occluded (tmax 1e32): drop the rest of the traversal
+                    } else {
+                        best = __uint_as_float((uint32_t)(key >> 32));
+                        bsid = (uint32_t)key >> 3;
+                        cut = best * __builtin_fmaf(__builtin_fabsf(io), sc.cull_p, kCullSlackF);
+                    }
+                }
+                leaf = kEnd;
+            }
+          }
+        } else if (n_tri != 0 && (n_tri >= a.tri_min || n_tri >= n_node)) {
             if constexpr (kCount) {
                 ph[PH_TRI_PHASES]++;
                 ph[PH_TRI_LANES] += n_tri;

@@ -304,6 +304,7 @@ int build_lbvh(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
 int build_ploc(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
 int trace_profile(unsigned long long* out, int reset);
 int wave_times(unsigned long long* out, int n);
+int shade_sections(unsigned long long* out, int n, int reset);  // -DMCPT_DIAG_SHADE builds (else 0)
 void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStream_t s);
 void launch_copy(const float4* src, float4* dst, size_t n, hipStream_t s);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);

@@ -1916,4 +1916,12 @@ int mcpt_debug_wave_times(mcpt_ctx* c, uint64_t* out, int n) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return wave_times(reinterpret_cast<unsigned long long*>(out), n);
 }
+// Diagnostics builds (-DMCPT_DIAG_SHADE) only, not part of mcpt.h: k_shade's per-section wave entries
+// and active lanes (SD_* pairs, kernels.hip) summed since the last reset; returns the word count or 0.
+int mcpt_debug_shade_sections(mcpt_ctx* c, uint64_t* out, int n, int reset) {
+    if (!c || !out || n < 0) return MCPT_E_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return shade_sections(reinterpret_cast<unsigned long long*>(out), n, reset);
+}
 }
