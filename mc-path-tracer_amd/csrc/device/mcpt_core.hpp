@@ -695,9 +695,11 @@ MCPT_HD void concentric_disk(const Rng& r, float& dx, float& dy) {  // Sample.cu
     float ux = r(SL_GEN_U), uy = r(SL_GEN_V);
     float ox = 2.f * ux - 1.f, oy = 2.f * uy - 1.f;
     if (ox == 0.f && oy == 0.f) { dx = 0.f; dy = 0.f; return; }
-    float theta, rr;
-    if (__builtin_fabsf(ox) > __builtin_fabsf(oy)) { rr = ox; theta = PI_4_F * (oy / ox); }
-    else { rr = oy; theta = PI_2_F - PI_4_F * (ox / oy); }
+    // the two branches' quotients as one division of selected operands (a wave whose lanes take
+    // both branches divides once)
+    const bool xm = __builtin_fabsf(ox) > __builtin_fabsf(oy);
+    const float q = (xm ? oy : ox) / (xm ? ox : oy);
+    const float theta = xm ? PI_4_F * q : PI_2_F - PI_4_F * q, rr = xm ? ox : oy;
     float st, ct;
     dsincos(theta, st, ct);
     dx = rr * ct;

@@ -140,6 +140,51 @@ __device__ inline V3 ld3f4(const float4* p) {
 }
 __device__ inline float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
+// Diagnostics of the shading kernels' instruction attribution, off in the product:
+//  * -DMCPT_ISA_MARKERS: assembly comments at the section boundaries (tools/isa_sections.py counts the
+//    VALU instructions between them in hipcc -S output);
+//  * -DMCPT_DIAG_SHADE: per-section wave entries and active lanes, summed over a run in a device
+//    global (mcpt_debug_shade_sections reads it).
+#ifdef MCPT_ISA_MARKERS
+#define MCPT_MARK(name) __asm__ volatile("; MCPT_SEC " name)
+#else
+#define MCPT_MARK(name) \
+    do {                \
+    } while (0)
+#endif
+enum : int { SD_WAVES = 0, SD_VALID, SD_LOGIC, SD_NEE, SD_GEN, SD_CONT, SD_BG, SD_N };
+#ifdef MCPT_DIAG_SHADE
+__device__ unsigned long long g_shade_diag[2 * SD_N];
+#define SHADE_DIAG(k, cond)                                                      \
+    do {                                                                         \
+        const uint64_t m_ = __ballot(cond);                                      \
+        if ((threadIdx.x & 63) == 0 && m_) {                                     \
+            atomicAdd(&g_shade_diag[2 * (k)], 1ull);                             \
+            atomicAdd(&g_shade_diag[2 * (k) + 1], (unsigned long long)__popcll(m_)); \
+        }                                                                        \
+    } while (0)
+#else
+#define SHADE_DIAG(k, cond) \
+    do {                    \
+    } while (0)
+#endif
+int shade_sections(unsigned long long* out, int n, int reset) {
+#ifdef MCPT_DIAG_SHADE
+    unsigned long long h[2 * SD_N];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_shade_diag), sizeof(h)) != hipSuccess) return -1;
+    for (int i = 0; i < n && i < 2 * SD_N; i++) out[i] = h[i];
+    if (reset) {
+        memset(h, 0, sizeof(h));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_shade_diag), h, sizeof(h)) != hipSuccess) return -1;
+    }
+    return 2 * SD_N;
+#else
+    for (int i = 0; i < n; i++) out[i] = 0;
+    (void)reset;
+    return 0;
+#endif
+}
+
 __device__ inline V3 light_L(const DevScene& sc, int id, V3 wi) {
     if (id == 0) return env_L(sc.env, wi);
     const float* p = sc.dirs + 7 * (id - 1);  // DirectionalLight.cu:34
@@ -446,6 +491,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
     mo.el = mo.eb = none;
     // the pixel and the sample index come with the record (k_shade: slot k of a pixel runs
     // samples k, k + S, k + 2S, ...)
+    MCPT_MARK("m_hit");
     const Rng r{rng_key(a.seed, pix, sidx), len};
     const V3 ro = xyz(ld_s(a.p.ray_o + pid)), rdir = xyz(ld_s(a.p.ray_d + pid));
     V3 pos, n;
@@ -463,6 +509,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
     uint32_t nf = 0;
     V3 rr;
     {
+        MCPT_MARK("m_cont");
         V3 wi_s = brdf_sample_wi<FIXED>(m, n, wo, r, SL_CONT_E0, r(SL_CONT_LOBE) < 0.5f);  // spec : diff
         float pdf_s;
         V3 f_s;
@@ -480,6 +527,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
             mo.trivial_ext = true;
         }
     }
+    MCPT_MARK("m_light");
     int l_id = (int)(r(SL_LIGHT) * (float)(sc.nlights - 0) + (float)0);
     const int light_id = (l_id == sc.nlights) ? 0 : l_id;
     const bool delta = light_id > 0;
@@ -530,6 +578,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
     }
     // the BRDF sample's direction and visibility ray (its light terms come after the occluder
     // cache, material_brdf_terms)
+    MCPT_MARK("m_bsdir");
     if (!delta) {
         const V3 wi_b = brdf_sample_wi<FIXED>(m, n, wo, r, SL_MAT_E0, r(SL_MAT_LOBE) < 0.5f);  // spec : diff
         const V3 so_b = pos + wi_b * 0.001f;
@@ -547,6 +596,7 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
             mo.want_b = true;
         }
     }
+    MCPT_MARK("m_ret");
     mo.n = n;
     mo.wo = wo;
     mo.matid = mat;
@@ -580,51 +630,6 @@ __device__ inline void material_brdf_terms(const ShadeArgs& a, uint32_t pid, con
     st_s(a.p.flags + pid, nf);
 }
 
-// Diagnostics of k_shade's instruction attribution, off in the product:
-//  * -DMCPT_ISA_MARKERS: assembly comments at the section boundaries (tools/isa_sections.py counts the
-//    VALU instructions between them in hipcc -S output);
-//  * -DMCPT_DIAG_SHADE: per-section wave entries and active lanes, summed over a run in a device
-//    global (mcpt_debug_shade_sections reads it).
-#ifdef MCPT_ISA_MARKERS
-#define MCPT_MARK(name) __asm__ volatile("; MCPT_SEC " name)
-#else
-#define MCPT_MARK(name) \
-    do {                \
-    } while (0)
-#endif
-enum : int { SD_WAVES = 0, SD_VALID, SD_LOGIC, SD_NEE, SD_GEN, SD_CONT, SD_BG, SD_N };
-#ifdef MCPT_DIAG_SHADE
-__device__ unsigned long long g_shade_diag[2 * SD_N];
-#define SHADE_DIAG(k, cond)                                                      \
-    do {                                                                         \
-        const uint64_t m_ = __ballot(cond);                                      \
-        if ((threadIdx.x & 63) == 0 && m_) {                                     \
-            atomicAdd(&g_shade_diag[2 * (k)], 1ull);                             \
-            atomicAdd(&g_shade_diag[2 * (k) + 1], (unsigned long long)__popcll(m_)); \
-        }                                                                        \
-    } while (0)
-#else
-#define SHADE_DIAG(k, cond) \
-    do {                    \
-    } while (0)
-#endif
-int shade_sections(unsigned long long* out, int n, int reset) {
-#ifdef MCPT_DIAG_SHADE
-    unsigned long long h[2 * SD_N];
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_shade_diag), sizeof(h)) != hipSuccess) return -1;
-    for (int i = 0; i < n && i < 2 * SD_N; i++) out[i] = h[i];
-    if (reset) {
-        memset(h, 0, sizeof(h));
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_shade_diag), h, sizeof(h)) != hipSuccess) return -1;
-    }
-    return 2 * SD_N;
-#else
-    for (int i = 0; i < n; i++) out[i] = 0;
-    (void)reset;
-    return 0;
-#endif
-}
-
 // k_shade: 8 waves per SIMD (<= 64 VGPRs; the virtual-block loop left alone allocates 67, no spill at 64)
 #ifndef MCPT_SHADE_WPE
 #define MCPT_SHADE_WPE 8
@@ -642,23 +647,19 @@ int shade_sections(unsigned long long* out, int n, int reset) {
 #else
 #define MCPT_MAT_ATTR
 #endif
-// Finished-block flag of shading block vb (k_shade's virtual block: kBlock consecutive pixels of
-// one path slot and tile), kept per slot, film tile and block, so it outlives a change of tile set
-__device__ inline uint32_t shade_done_idx(const ShadeArgs& a, int vb) {
-    const int bpt = (a.tile_w * a.tile_h + kBlock - 1) / kBlock;
-    const int per_slot = a.ntiles * bpt;
-    const int slot = a.slots > 1 ? vb / per_slot : 0;
-    const int bs = vb - slot * per_slot;
-    const int tile = bs / bpt;
-    const int2 t = a.tiles[tile];
-    const uint32_t ntx = (uint32_t)((a.W + a.tile_w - 1) / a.tile_w), nty = (uint32_t)((a.H + a.tile_h - 1) / a.tile_h);
-    return (((uint32_t)slot * nty + (uint32_t)t.y) * ntx + (uint32_t)t.x) * (uint32_t)bpt + (uint32_t)(bs - tile * bpt);
-}
-
-// One shading block: logic + generate for kBlock pixels of a path slot, then the block's pushes.
-template <bool FIXED>
-__device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeArgs& a, int vb, uint32_t done_idx) {
-    const DevScene& sc = a.scene;
+// Shading block vb (k_shade's virtual block: kBlock consecutive pixels of one path slot and tile),
+// decomposed once per launch by the k_shade workgroup that runs it (thread k for its k-th block, in
+// the prologue, into LDS): the per-block integer divisions by the slot and tile sizes are VALU
+// sequences (no scalar divide), which the block loop would otherwise repeat per wave and block.
+//   x0, y0: film position of the block's first pixel (with tile_w a multiple of kBlock a block is one
+//           run of a tile row, pixel x0 + k; otherwise x0, y0 are the tile's corner);
+//   loc0:   path index within the slot of the first pixel (ShadeArgs::npx);
+//   sr:     path slot | pixels of the block inside its tile << 8 (kBlock for all but a tile's last);
+//   li0:    the first pixel's index in its tile;
+//   done:   its finished-block flag, kept per slot, film tile and block so it outlives a change of
+//           tile set.
+struct VBlk { int x0, y0; uint32_t loc0, sr, li0, done; };
+__device__ inline VBlk vblock_of(const ShadeArgs& a, int vb) {
     const int tile_px = a.tile_w * a.tile_h;
     const int bpt = (tile_px + kBlock - 1) / kBlock;
     // path slots: blocks [k * ntiles * bpt, (k + 1) * ntiles * bpt) run slot k of every pixel
@@ -666,21 +667,55 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
     const int slot = a.slots > 1 ? vb / per_slot : 0;
     const int bs = vb - slot * per_slot;
     const int tile = bs / bpt;
-    const int li = (bs - tile * bpt) * kBlock + threadIdx.x;
+    const int bib = bs - tile * bpt;
+    const int li0 = bib * kBlock;
+    const int2 t = a.tiles[tile];
+    VBlk r;
+    if (a.tile_w % kBlock == 0) {
+        const int row = li0 / a.tile_w;
+        r.x0 = t.x * a.tile_w + (li0 - row * a.tile_w);
+        r.y0 = t.y * a.tile_h + row;
+    } else {
+        r.x0 = t.x * a.tile_w;
+        r.y0 = t.y * a.tile_h;
+    }
+    // path index (ShadeArgs::npx): the pixel id, or its place in the compact tile-set layout
+    r.loc0 = a.compact ? (uint32_t)(a.tile_base ? a.tile_base[tile] : tile) * (uint32_t)tile_px + (uint32_t)li0 : 0u;
+    r.sr = (uint32_t)slot | ((uint32_t)min(tile_px - li0, kBlock) << 8);
+    r.li0 = (uint32_t)li0;
+    const uint32_t ntx = (uint32_t)((a.W + a.tile_w - 1) / a.tile_w), nty = (uint32_t)((a.H + a.tile_h - 1) / a.tile_h);
+    r.done = (((uint32_t)slot * nty + (uint32_t)t.y) * ntx + (uint32_t)t.x) * (uint32_t)bpt + (uint32_t)bib;
+    return r;
+}
+// floor(n / d) for n < 2^23, d >= 1, from rcp = RN32(1 / d): the truncated float product is q or
+// q - 1 (relative error < 2^-22 on n / d, and 1 - frac(n / d) >= 1 / d), one correction
+__device__ inline uint32_t udiv_small(uint32_t n, uint32_t d, float rcp) {
+    uint32_t q = (uint32_t)((float)n * rcp);
+    if (n - __umul24(q, d) >= d) q++;
+    return q;
+}
+
+// One shading block: logic + generate for kBlock pixels of a path slot, then the block's pushes.
+template <bool FIXED>
+__device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeArgs& a, int vb, const VBlk& v) {
+    const DevScene& sc = a.scene;
+    const int slot = (int)(v.sr & 0xffu);
     const int lane = threadIdx.x & 63;
-    bool valid = tile < a.ntiles && li < tile_px;
+    bool valid = (int)threadIdx.x < (int)(v.sr >> 8);
     uint32_t pid = 0, pix = 0;  // path id (slot * pixels + pixel) and pixel id
     int x = 0, y = 0;
     if (valid) {
-        int2 t = a.tiles[tile];
-        x = t.x * a.tile_w + li % a.tile_w;
-        y = t.y * a.tile_h + li / a.tile_w;
+        if (a.tile_w % kBlock == 0) {
+            x = v.x0 + (int)threadIdx.x;
+            y = v.y0;
+        } else {
+            const int li = (int)v.li0 + (int)threadIdx.x;
+            x = v.x0 + li % a.tile_w;
+            y = v.y0 + li / a.tile_w;
+        }
         valid = x < a.W - 1 && y < a.H - 1;  // last column and row never rendered (wavefront_kernels.cu:110)
         pix = (uint32_t)y * (uint32_t)a.W + (uint32_t)x;
-        // path index (ShadeArgs::npx): the pixel id, or its place in the compact tile-set layout
-        const uint32_t local = a.compact ? (uint32_t)(a.tile_base ? a.tile_base[tile] : tile) * (uint32_t)tile_px + (uint32_t)li
-                                         : pix;
-        pid = (uint32_t)slot * a.npx + local;
+        pid = (uint32_t)slot * a.npx + (a.compact ? v.loc0 + threadIdx.x : pix);
     }
     // ---- phase 1: logic + generate (one thread per pixel)
     MCPT_MARK("load");
@@ -725,7 +760,7 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
         // draws with it) and the next one for a dead path (k_clear: the slot's first), so the
         // film's sample count is (sidx - slot) / S and its stream is only written
         uint32_t sidx = fl >> F_SIDX_SHIFT;
-        uint32_t samples = a.slots > 1 ? (sidx - (uint32_t)slot) / (uint32_t)a.slots : sidx;
+        uint32_t samples = a.slots > 1 ? udiv_small(sidx - (uint32_t)slot, (uint32_t)a.slots, a.slots_rcp) : sidx;
         if (!dead && sidx < spp) {  // wavefront_kernels.cu:124
             MCPT_MARK("logic");
             d_logic = true;
@@ -795,9 +830,15 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
         if (dead && sidx < spp) {  // :219-222 + wf_generate (:225-251)
             MCPT_MARK("generate");
             d_gen = true;
-            const Rng r0{rng_key(a.seed, pix, sidx), 0u};
-            V3 new_o, new_d;
-            gen_ray(a.cam, a.W, a.H, x, y, r0, new_o, new_d);
+            // dCamera::gen_ray (Camera.cu:18-45): the pixel's part from its camera record
+            // (k_cam_table), the thin lens per sample
+            V3 new_o = ld3f4(a.cam_px + pix), new_d;
+            if (a.cam.lens_radius > 0.f) {
+                const Rng r0{rng_key(a.seed, pix, sidx), 0u};
+                gen_ray_lens(a.cam, new_o, r0, new_o, new_d);
+            } else {
+                new_d = ld3f4(a.cam_dir + pix);
+            }
             // beta = (1,1,1) (:245) is implied by len 1: k_shade does not load it for len-1 paths
             nflags = (1u << F_LEN_SHIFT) | (sidx << F_SIDX_SHIFT);
             st_s(a.p.ray_o + pid, f4(new_o, 0.f));
@@ -851,7 +892,7 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
             a.p.Ld[pid] = f4(film, 0.f);
     }
     MCPT_MARK("done");
-    if (a.blk_done && __syncthreads_and(finished ? 1 : 0) && threadIdx.x == 0) a.blk_done[done_idx] = 1;
+    if (a.blk_done && __syncthreads_and(finished ? 1 : 0) && threadIdx.x == 0) a.blk_done[v.done] = 1;
     MCPT_MARK("end");
 }
 
@@ -870,26 +911,20 @@ __global__ __launch_bounds__(kBlock) MCPT_SHADE_ATTR void k_shade(ShadeArgs a) {
     const uint32_t mine = (nvb - blockIdx.x + G - 1) / G;  // <= kBlock
     const uint32_t k = threadIdx.x;
     bool live = false;
-    uint32_t didx = 0;
+    __shared__ VBlk s_vb[kBlock];  // thread k: the block's k-th shading block (vblock_of)
     if (k < mine) {
-        const int vb = (int)(blockIdx.x + k * G);
-        if (a.blk_done) {
-            didx = shade_done_idx(a, vb);
-            live = a.blk_done[didx] == 0;
-        } else {
-            live = true;
-        }
+        const VBlk v = vblock_of(a, (int)(blockIdx.x + k * G));
+        live = !a.blk_done || a.blk_done[v.done] == 0;
+        s_vb[k] = v;
     }
     const uint64_t m = __ballot(live);
     if ((threadIdx.x & 63) == 0) s_live[threadIdx.x >> 6] = m;
-    __shared__ uint32_t s_didx[kBlock];
-    s_didx[k] = didx;
     __syncthreads();
     for (uint32_t j = 0; j < mine; j++) {
         if (!((s_live[j >> 6] >> (j & 63)) & 1ull)) continue;
         // the arguments re-read per shading block (kernarg_fresh): hoisted out of the loop, the
         // struct's fields took the SGPR file and spilled (89 SGPRs, 54 -> 86 VGPRs)
-        shade_vblock<FIXED>(kernarg_fresh<ShadeArgs>(), (int)(blockIdx.x + j * G), s_didx[j]);
+        shade_vblock<FIXED>(kernarg_fresh<ShadeArgs>(), (int)(blockIdx.x + j * G), s_vb[j]);
     }
 }
 
@@ -930,6 +965,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a_k
                                  (int32_t)q.w, &s_any[0][0], occ_on);
             // the occluder cache (see occ_hit1), before the BRDF sample's light terms: a ray it
             // resolves gets its wf_shadow result here and is not queued
+            MCPT_MARK("m_occ");
             if (occ_on) {
                 try_l = mo.want_l;
                 try_b = mo.want_b;
@@ -949,8 +985,10 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a_k
                     mo.trivial_any++;
                 }
             }
+            MCPT_MARK("m_bterms");
             material_brdf_terms<FIXED>(a, mpid, mo);
         }
+        MCPT_MARK("m_push");
         bool want[3] = {mo.want_ext, mo.want_l, mo.want_b};
         uint32_t* ctr[3] = {sc_ctr + C_EXT, sc_ctr + C_ANY, sc_ctr + C_ANY};
         uint32_t slot[3], total[3];
@@ -978,6 +1016,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a_k
                 a.p.sray_d[k] = s_any[3][threadIdx.x];
             }
         }
+        MCPT_MARK("m_count");
         // per-wave ray counts from lane masks (wave-uniform scalars: no registers held across the
         // next trip's material())
         n_occ += (uint32_t)(__popcll(__ballot(occ_l)) + __popcll(__ballot(occ_b)));
@@ -1676,6 +1715,21 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 if (ph[k]) atomicAdd(pw + k, ph[k]);
         }
     }
+}
+
+// Camera records of a W x H film: gen_ray_pixel of every pixel (ShadeArgs::cam_px / cam_dir)
+__global__ void k_cam_table(mcpt::CamView cam, int W, int H, float4* px, float4* dir) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint32_t)W * (uint32_t)H) return;
+    const int x = (int)(i % (uint32_t)W), y = (int)(i / (uint32_t)W);
+    V3 o, d;
+    gen_ray_pixel(cam, W, H, x, y, o, d);
+    px[i] = f4(cam.lens_radius > 0.f ? gen_ray_focal(cam, o, d) : o, 0.f);
+    dir[i] = f4(d, 0.f);
+}
+void launch_cam_table(const mcpt::CamView& cam, int W, int H, float4* px, float4* dir, hipStream_t s) {
+    const uint32_t n = (uint32_t)W * (uint32_t)H;
+    if (n) hipLaunchKernelGGL(k_cam_table, dim3((n + 255) / 256), dim3(256), 0, s, cam, W, H, px, dir);
 }
 
 // The env texture's device copy takes the pdf table into its alpha plane (EnvView::tex)

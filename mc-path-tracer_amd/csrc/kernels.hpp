@@ -170,6 +170,7 @@ struct ShadeArgs {
     int ntiles, tile_w, tile_h, W, H;
     int spp, max_depth, rr_depth;
     int slots;  // path slots per pixel (paths in flight per pixel; slot k runs samples k, k + slots, ...)
+    float slots_rcp;  // RN32(1 / slots) (k_shade's udiv_small)
     // Path index of a pixel: slot * npx + its index within the slot.  Full layout (compact 0): npx =
     // W * H and the index is the pixel id (the reference's path_id = pixel_id, wavefront_kernels.cu:
     // 108,114).  Compact layout (mcpt_set_compact_paths): the path state covers only the context's tile
@@ -194,6 +195,10 @@ struct ShadeArgs {
     // (cleared with the film; nullptr: off)
     uint8_t* blk_done;
     uint32_t shade_vblocks;  // k_shade: shading blocks of the launch (launch_shade sets it and the grid)
+    // Per-pixel camera records of the W x H film (k_cam_table; gen_ray_pixel of every pixel): the
+    // pixel's focal point (thin lens) or pinhole origin in cam_px, the pinhole direction in cam_dir
+    const float4* cam_px;
+    const float4* cam_dir;
 };
 
 // One ray set of a trace launch: rays ro/rd[rid] for queue entries
@@ -305,6 +310,7 @@ int build_ploc(const LbvhInput& in, LbvhOutput& out, hipStream_t s);
 int trace_profile(unsigned long long* out, int reset);
 int wave_times(unsigned long long* out, int n);
 int shade_sections(unsigned long long* out, int n, int reset);  // -DMCPT_DIAG_SHADE builds (else 0)
+void launch_cam_table(const mcpt::CamView& cam, int W, int H, float4* px, float4* dir, hipStream_t s);
 void launch_quot(const float* a, const float* b, float* out, uint32_t n, hipStream_t s);
 void launch_copy(const float4* src, float4* dst, size_t n, hipStream_t s);
 void launch_hit_record(const HitRecordArgs& a, hipStream_t s);

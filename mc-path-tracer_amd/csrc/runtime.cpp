@@ -51,6 +51,12 @@ struct mcpt_ctx {
     // camera
     mcpt::CamView cam{};
     bool has_cam = false;
+    // per-pixel camera records (cam_table): for the film size and camera they were built for
+    float4* cam_tab = nullptr;
+    size_t cam_tab_cap = 0;  // pixels allocated
+    uint32_t cam_tab_W = 0, cam_tab_H = 0;
+    mcpt::CamView cam_tab_cam{};
+    bool cam_tab_ok = false;
     // Film observes camera and scene (Film::update -> clear(), Film.cu:278-281; notified by
     // Camera::update, Camera.cu:207, and Scene::notify, Scene.cu:534-545): a change marks the
     // film stale and the next iteration clears it first (unless MCPT_FLAG_NO_AUTO_CLEAR).
@@ -196,6 +202,7 @@ void mcpt_destroy(mcpt_ctx* c) {
     if (c->any_q) (void)hipFree(c->any_q);
     if (c->mat_q) (void)hipFree(c->mat_q);
     if (c->any_ray) (void)hipFree(c->any_ray);
+    if (c->cam_tab) (void)hipFree(c->cam_tab);
     for (auto e : c->events) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1030,6 +1037,33 @@ static hipEvent_t ev(mcpt_ctx* c, size_t i) {
     return c->events[i];
 }
 
+// The camera records of a W x H film under the current camera (k_cam_table: gen_ray_pixel of every
+// pixel, 32 B each), rebuilt on the context's stream when the film size or the camera changed.
+static int cam_table(mcpt_ctx* c, uint32_t W, uint32_t H, const float4** px, const float4** dir) {
+    const size_t n = (size_t)W * H;
+    if (!(c->cam_tab_ok && c->cam_tab_W == W && c->cam_tab_H == H && memcmp(&c->cam_tab_cam, &c->cam, sizeof(c->cam)) == 0)) {
+        if (n > c->cam_tab_cap) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            if (c->cam_tab) (void)hipFree(c->cam_tab);
+            c->cam_tab = nullptr;
+            c->cam_tab_cap = 0;
+            c->cam_tab_ok = false;
+            if (hipMalloc(&c->cam_tab, 2 * n * sizeof(float4)) != hipSuccess)
+                return set_err(c, MCPT_E_NOMEM, "camera table allocation failed");
+            c->cam_tab_cap = n;
+        }
+        launch_cam_table(c->cam, (int)W, (int)H, c->cam_tab, c->cam_tab + n, c->stream);
+        HIPCHK(c, hipGetLastError());
+        c->cam_tab_W = W;
+        c->cam_tab_H = H;
+        c->cam_tab_cam = c->cam;
+        c->cam_tab_ok = true;
+    }
+    *px = c->cam_tab;
+    *dir = c->cam_tab + n;
+    return MCPT_OK;
+}
+
 static int check_ready(mcpt_ctx* c) {
     if (!c) return MCPT_E_INVALID;
     if (!c->has_scene) return set_err(c, MCPT_E_INVALID, "no scene uploaded");
@@ -1057,6 +1091,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     sa.rr_depth = c->cfg.rr_depth;
     sa.seed = c->cfg.seed;
     sa.slots = (int)c->slots;
+    sa.slots_rcp = 1.0f / (float)c->slots;
     sa.npx = (uint32_t)c->npx;
     sa.compact = c->compact ? 1 : 0;
     sa.tile_base = tile_base;
@@ -1068,6 +1103,7 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     sa.any_cap = c->any_cap;
     sa.cnt = c->cnt;
     sa.blk_done = c->blk_done_off ? nullptr : c->blk_done;
+    if (int rc = cam_table(c, c->W, c->H, &sa.cam_px, &sa.cam_dir)) return rc;
     const int bpt = shade_blocks_per_tile((int)(c->tile_w * c->tile_h), (int)c->slots);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 0), c->stream));
     if (sa.ntiles > 0)
@@ -1369,7 +1405,9 @@ static int stage_run_paths(mcpt_ctx* c, int stage, const mcpt_path_view* in, mcp
     sa.rr_depth = c->cfg.rr_depth;
     sa.seed = c->cfg.seed;
     sa.slots = 1;
+    sa.slots_rcp = 1.0f;
     sa.npx = n;  // path i is pixel i of the W x H stage film
+    if ((rc = cam_table(c, W, H, &sa.cam_px, &sa.cam_dir))) return rc;
     sa.ext_q = ext_q;
     sa.any_q = any_q;
     sa.mat_rec = mrec;
