@@ -186,6 +186,16 @@ MCPT_HD float pow5(float x) {  // pow(x, 5.f) in fresnel_schlick (dMaterial.cu:1
     return x4 * x;
 }
 
+// Assembly markers for the static instruction attribution (-DMCPT_ISA_MARKERS analysis builds of
+// the device code, tools/isa_sections.py; nothing otherwise)
+#if defined(MCPT_ISA_MARKERS) && defined(__HIP_DEVICE_COMPILE__)
+#define MCPT_MARK(name) __asm__ volatile("; MCPT_SEC " name)
+#else
+#define MCPT_MARK(name) \
+    do {                \
+    } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Keyed RNG around lowerbias32 (cuda_math/Random.cu:5-13)
 // ---------------------------------------------------------------------------
@@ -807,6 +817,7 @@ MCPT_HD bool tri_test_t(V3 o, V3 d, V3 p0, V3 e1, V3 e2, float& t) {
         }
     }
 #endif
+    MCPT_MARK("rare");  // (a subnormal quotient or an out-of-range det: the fp64 island itself)
     t = (float)((double)tf * (1.0 / (double)detf));
     return true;
 }

@@ -141,17 +141,10 @@ __device__ inline V3 ld3f4(const float4* p) {
 __device__ inline float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
 // Diagnostics of the shading kernels' instruction attribution, off in the product:
-//  * -DMCPT_ISA_MARKERS: assembly comments at the section boundaries (tools/isa_sections.py counts the
-//    VALU instructions between them in hipcc -S output);
+//  * -DMCPT_ISA_MARKERS: assembly comments at the section boundaries (MCPT_MARK, mcpt_core.hpp;
+//    tools/isa_sections.py counts the VALU instructions between them in hipcc -S output);
 //  * -DMCPT_DIAG_SHADE: per-section wave entries and active lanes, summed over a run in a device
 //    global (mcpt_debug_shade_sections reads it).
-#ifdef MCPT_ISA_MARKERS
-#define MCPT_MARK(name) __asm__ volatile("; MCPT_SEC " name)
-#else
-#define MCPT_MARK(name) \
-    do {                \
-    } while (0)
-#endif
 enum : int { SD_WAVES = 0, SD_VALID, SD_LOGIC, SD_NEE, SD_GEN, SD_CONT, SD_BG, SD_N };
 #ifdef MCPT_DIAG_SHADE
 __device__ unsigned long long g_shade_diag[2 * SD_N];
@@ -307,6 +300,68 @@ __device__ inline void quad_axis(const float4& mn, const float4& mx, float o, fl
     }
 }
 
+// The same slab tests with the ray held as (o_a, 1 / d_a) register pairs, one per axis: the packed
+// subtract takes o_a from the pair's low half for both lanes (op_sel_hi) and the packed multiply
+// 1 / d_a from its high half (op_sel), so no duplicated {o_a, o_a} / {inv_a, inv_a} pairs are built
+// per trip (9 VALU moves per k_trace loop trip were the compiler's copies for pair_slab's
+// broadcasts).  The operations and their order are pair_slab's: q + (-o) is q - o exactly; min and
+// max are exact.  Written as inline assembly because the compiler neither folds the broadcasts into
+// op_sel nor knows an asm result is a canonical float (it would canonicalise each before min / max);
+// the operands are finite here (finite inverse: no NaN product).
+__device__ inline f2v pk_slab(f2v q, f2v p) {  // ((q.x - p.x) * p.y, (q.y - p.x) * p.y)
+    f2v r;
+    __asm__("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %0, %0, %2 op_sel:[0,1] op_sel_hi:[1,1]"
+            : "=&v"(r)
+            : "v"(q), "v"(p));
+    return r;
+}
+// entry / exit of one box from its six plane products: max3 of the per-axis minima, min3 of the maxima
+__device__ inline void box_t(float ax, float bx, float ay, float by, float az, float bz, float& t0, float& t1) {
+    float m0, m1, m2, n0, n1, n2;
+    __asm__("v_min_f32 %2, %8, %9\n\t"
+            "v_min_f32 %3, %10, %11\n\t"
+            "v_min_f32 %4, %12, %13\n\t"
+            "v_max_f32 %5, %8, %9\n\t"
+            "v_max_f32 %6, %10, %11\n\t"
+            "v_max_f32 %7, %12, %13\n\t"
+            "v_max3_f32 %0, %2, %3, %4\n\t"
+            "v_min3_f32 %1, %5, %6, %7"
+            : "=v"(t0), "=v"(t1), "=&v"(m0), "=&v"(m1), "=&v"(m2), "=&v"(n0), "=&v"(n1), "=&v"(n2)
+            : "v"(ax), "v"(bx), "v"(ay), "v"(by), "v"(az), "v"(bz));
+}
+__device__ inline void pair_slab2(float4 qx, float4 qy, float4 qz, f2v px, f2v py, f2v pz, float& t0a, float& t1a,
+                                  float& t0b, float& t1b) {
+    const f2v ax = pk_slab(f2v{qx.x, qx.y}, px), bx = pk_slab(f2v{qx.z, qx.w}, px);
+    const f2v ay = pk_slab(f2v{qy.x, qy.y}, py), by = pk_slab(f2v{qy.z, qy.w}, py);
+    const f2v az = pk_slab(f2v{qz.x, qz.y}, pz), bz = pk_slab(f2v{qz.z, qz.w}, pz);
+    box_t(ax.x, bx.x, ay.x, by.x, az.x, bz.x, t0a, t1a);
+    box_t(ax.y, bx.y, ay.y, by.y, az.y, bz.y, t0b, t1b);
+}
+// quad_axis with the (o_a, 1 / d_a) pair (pk_slab); the folds over the axes as quad_axis (min / max in
+// asm as well: their inputs are asm results)
+__device__ inline float vmin(float a, float b) {
+    float r;
+    __asm__("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ inline float vmax(float a, float b) {
+    float r;
+    __asm__("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ inline void quad_axis2(const float4& mn, const float4& mx, f2v p, float (&lo)[4], float (&hi)[4], bool first) {
+    const f2v a0 = pk_slab(f2v{mn.x, mn.y}, p), a1 = pk_slab(f2v{mn.z, mn.w}, p);
+    const f2v b0 = pk_slab(f2v{mx.x, mx.y}, p), b1 = pk_slab(f2v{mx.z, mx.w}, p);
+    const float l[4] = {vmin(a0.x, b0.x), vmin(a0.y, b0.y), vmin(a1.x, b1.x), vmin(a1.y, b1.y)};
+    const float h[4] = {vmax(a0.x, b0.x), vmax(a0.y, b0.y), vmax(a1.x, b1.x), vmax(a1.y, b1.y)};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        lo[k] = first ? l[k] : vmax(lo[k], l[k]);
+        hi[k] = first ? h[k] : vmin(hi[k], h[k]);
+    }
+}
+
 // The first test the traversal makes: a NaN/zero direction or a ray that misses
 // the root box (after the cull) can hit nothing.  k_shade resolves such rays in
 // place instead of queueing them.
@@ -419,8 +474,8 @@ __device__ inline bool occ_test(V3 o, V3 d, V3 inv, float io, float4 bmn, float4
 // The cell's entries of (o, d): kOccWays triangle records (k_trace writes way tri mod kOccWays).
 // MCPT_NT bit 16: the table's random 8-B reads and the occluder stores are non-temporal (the 96 MB
 // table cannot stay in L2; its lines would evict the env tables' and occluder records').
-__device__ inline uint2 occ_entry(const DevScene& sc, V3 o, V3 d) {
-    const uint2* e = reinterpret_cast<const uint2*>(sc.occ) + occ_index(sc, o, d);
+__device__ inline uint2 occ_entry(const DevScene& sc, uint32_t cell) {
+    const uint2* e = reinterpret_cast<const uint2*>(sc.occ) + cell;
     if constexpr (MCPT_NT & 16) {
         typedef uint32_t u2v_t __attribute__((ext_vector_type(2)));
         const u2v_t v = __builtin_nontemporal_load(reinterpret_cast<const u2v_t*>(e));
@@ -568,12 +623,14 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
             a.p.vis[2 * pid] = 1;
             mo.trivial_any++;
         } else {
-            // staged: stored at its any-queue position after the block push
-            stage[0 * kBlock + threadIdx.x] = f4(so_l, 0.f);
-            stage[1 * kBlock + threadIdx.x] = f4(ldir, 0.f);
+            // staged: stored at its any-queue position after the block push, with the ray's
+            // result index (vis) in o.w and its occluder-table cell in d.w (k_trace's finish)
+            const uint32_t cell = sc.occ ? occ_index(sc, so_l, ldir) : 0u;
+            stage[0 * kBlock + threadIdx.x] = f4(so_l, __uint_as_float(2 * pid));
+            stage[1 * kBlock + threadIdx.x] = f4(ldir, __uint_as_float(cell));
             mo.want_l = true;
             // the occluder-cache entry, loaded now and used after material()
-            if (occ_on) mo.el = occ_entry(sc, so_l, ldir);
+            if (occ_on) mo.el = occ_entry(sc, cell);
         }
     }
     // the BRDF sample's direction and visibility ray (its light terms come after the occluder
@@ -590,9 +647,10 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
             a.p.vis[2 * pid + 1] = 1;
             mo.trivial_any++;
         } else {
-            if (occ_on) mo.eb = occ_entry(sc, so_b, wi_b);
-            stage[2 * kBlock + threadIdx.x] = f4(so_b, 0.f);
-            stage[3 * kBlock + threadIdx.x] = f4(wi_b, 0.f);
+            const uint32_t cell = sc.occ ? occ_index(sc, so_b, wi_b) : 0u;
+            if (occ_on) mo.eb = occ_entry(sc, cell);
+            stage[2 * kBlock + threadIdx.x] = f4(so_b, __uint_as_float(2 * pid + 1));
+            stage[3 * kBlock + threadIdx.x] = f4(wi_b, __uint_as_float(cell));
             mo.want_b = true;
         }
     }
@@ -994,9 +1052,9 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a_k
         uint32_t slot[3], total[3];
         block_push<3>(want, ctr, slot, total);
         if (mo.want_ext) st_q(a.ext_q + shard * a.ext_cap + slot[0], mpid);
+        // (the any-hit rays carry their result index in o.w: no queue entries)
         if (mo.want_l) {
             const uint32_t k = shard * a.any_cap + slot[1];
-            st_q(a.any_q + k, 2 * mpid);
             if constexpr (MCPT_NT & 8) {
                 st_s(a.p.sray_o + k, s_any[0][threadIdx.x]);
                 st_s(a.p.sray_d + k, s_any[1][threadIdx.x]);
@@ -1007,7 +1065,6 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a_k
         }
         if (mo.want_b) {
             const uint32_t k = shard * a.any_cap + slot[2];
-            st_q(a.any_q + k, 2 * mpid + 1);
             if constexpr (MCPT_NT & 8) {
                 st_s(a.p.sray_o + k, s_any[2][threadIdx.x]);
                 st_s(a.p.sray_d + k, s_any[3][threadIdx.x]);
@@ -1096,11 +1153,11 @@ __device__ inline void wave_stats(uint32_t* stats, int lane, uint32_t nodes, uin
 // Shared triangle phase (MCPT_TRI_SHARE=1; measured and not kept): a triangle
 // phase tests every triangle of every parked leaf of the wave, dealt over all 64 lanes (a lane tests
 // another lane's ray against one of that lane's triangles), instead of one triangle per lane holding
-// a leaf.  Parity held (110 GPU tests), but config 2's k_trace went 2.47 -> 2.79 ms per launch: a
-// phase finds 36 triangles in the wave's parked leaves on average (6.91 G tests in 190 M phases,
-// the same with and without sharing), so one round per phase does the same tests with the owner
-// search and ray exchange on top; the lanes without a leaf at a phase are traversing, not waiting
-// on another lane's leaf.  Applies to the instantiations with an LDS stack of <= kShareMaxStack
+// a leaf.  Parity held (110 GPU tests), but config 2's k_trace went 2.47 -> 2.79 ms per launch: the
+// upload expands every multi-triangle leaf into pair nodes over one-triangle leaves (their own
+// boxes: the tree-independent acceptance), so a parked leaf is one triangle and a phase holds 36 of
+// them on average (6.91 G tests in 190 M phases, the same with and without sharing); one round per
+// phase then does the same tests with the owner search and ray exchange on top.  Applies to the instantiations with an LDS stack of <= kShareMaxStack
 // entries (its 512-B result slots per wave would cost the deep-stack kernels a resident wave per CU).
 #ifndef MCPT_TRI_SHARE
 #define MCPT_TRI_SHARE 0
@@ -1264,7 +1321,11 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     uint32_t buf_lo = 0, buf_hi = 0, last_p = 0;  // wave-uniform reservation of the partition (refill)
     bool act = false;
     uint32_t rid = 0;
-    V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
+    // origin and inverse direction axis by axis as (o_a, 1 / d_a) register pairs (pair_slab2)
+    f2v px = {0.f, 0.f}, py = px, pz = px;
+    V3 d = v3(0.f, 0.f, 0.f);
+#define RAY_O v3(px.x, py.x, pz.x)
+#define RAY_INV v3(px.y, py.y, pz.y)
     int ref = kEnd, leaf = kEnd, sp = 0, tri = -1;
     // best: the closest hit's t, or -1 for an any-hit ray (its kind: best < 0; an accepted t is never
     // below +-0); io: the ray's signed culling scale (cull_iota; |io| = inf: an infinite inverse
@@ -1300,10 +1361,15 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             }
         }
         if (kind) {
-            if constexpr (MCPT_NT & 4) __builtin_nontemporal_store((uint8_t)(tri < 0), a.vis + rid);
-            else a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
+            // a dense any-hit set (ray_at_slot: rid is the ray's queue position) carries the result
+            // index in o.w and the occluder-table cell in d.w (k_material)
+            const bool rec = a.set[1].ray_at_slot != 0;
+            const uint32_t vi = rec ? __float_as_uint(a.set[1].ro[rid].w) : rid;
+            if constexpr (MCPT_NT & 4) __builtin_nontemporal_store((uint8_t)(tri < 0), a.vis + vi);
+            else a.vis[vi] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
             if (tri >= 0 && occ_rec) {  // the cell's occluder (occ_hit1)
-                uint32_t* w = sc.occ + (size_t)occ_index(sc, o, d) * kOccWays + (uint32_t)tri % kOccWays;
+                const uint32_t cell = rec ? __float_as_uint(a.set[1].rd[rid].w) : occ_index(sc, RAY_O, d);
+                uint32_t* w = sc.occ + (size_t)cell * kOccWays + (uint32_t)tri % kOccWays;
                 if constexpr (MCPT_NT & 16) __builtin_nontemporal_store((uint32_t)tri, w);
                 else *w = (uint32_t)tri;
             }
@@ -1315,6 +1381,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
     };
     for (;;) {
         // ---- refill idle lanes with the partition's next rays
+        MCPT_MARK("t_top");
         const uint64_t idle = __ballot(!act);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if ((more || buf_lo < buf_hi) && (nidle >= a.refill_min || nidle == 64u)) {
@@ -1343,6 +1410,7 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 buf_lo = g0;
                 buf_hi = g0 < T ? min(g0 + G, T) : g0;
             }
+            MCPT_MARK("t_refill");
             const uint32_t p0 = buf_lo;
             const uint32_t take = min(nidle, buf_hi - buf_lo);
             buf_lo += take;
@@ -1374,18 +1442,19 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     // positions) issues its ray loads with the queue-entry load, not after it
                     const bool at_slot = kind ? a.set[1].ray_at_slot : a.set[0].ray_at_slot;
                     float4 o4, d4;
+                    // (a dense set's ray keeps its queue position as rid: its result index rides in o.w)
                     if constexpr (MCPT_NT & 4) {
                         rid = at_slot ? qslot : (qp ? __builtin_nontemporal_load(qp + qslot) : qslot);
                         o4 = ld_s(rop + rid);
                         d4 = ld_s(rdp + rid);
-                        if (at_slot && qp) rid = __builtin_nontemporal_load(qp + qslot);  // the result index
                     } else {
                         rid = at_slot ? qslot : (qp ? qp[qslot] : qslot);
                         o4 = rop[rid];
                         d4 = rdp[rid];
-                        if (at_slot && qp) rid = qp[qslot];  // the result index, needed only when the ray finishes
                     }
-                    o = xyz(o4);
+                    px.x = o4.x;
+                    py.x = o4.y;
+                    pz.x = o4.z;
                     d = xyz(d4);
                     tri = -1;
                     best = kind ? -1.f : K_HUGE;
@@ -1404,14 +1473,16 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                         (!(d.x == d.x && d.y == d.y && d.z == d.z) || (d.x == 0.f && d.y == 0.f && d.z == 0.f))) {
                         finish();
                     } else {
-                        inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-                        io = cull_iota(sc, d, inv);
+                        px.y = 1.f / d.x;
+                        py.y = 1.f / d.y;
+                        pz.y = 1.f / d.z;
+                        io = cull_iota(sc, d, RAY_INV);
                         cut = kind ? K_INF_F : best * __builtin_fmaf(__builtin_fabsf(io), sc.cull_p, kCullSlackF);
                         float t0, t1, key;
                         // (k_shade resolved the rays that miss the root box in place, so the
                         // queued sets skip this test: same outcome, ray_misses_scene())
                         if (!pre && (!slab(sc.root_mn[0], sc.root_mn[1], sc.root_mn[2], sc.root_mx[0],
-                                           sc.root_mx[1], sc.root_mx[2], o, inv, inv.x < 0.f, inv.y < 0.f, inv.z < 0.f,
+                                           sc.root_mx[1], sc.root_mx[2], RAY_O, RAY_INV, px.y < 0.f, py.y < 0.f, pz.y < 0.f,
                                            t0, t1) ||
                                      !keep_box(t0, t1, sc.root_w * io, cut, key)))
                             finish();
@@ -1421,11 +1492,13 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 }
             }
         }
-        if (__ballot(act) == 0) {
-            if (!more && buf_lo >= buf_hi) break;  // partition drained, every lane idle
-            continue;
-        }
-        uint32_t itc = 0;  // node steps this lane took in this trip (kCount)
+        // (one back edge: a trip without rays skips its phases instead of continuing the loop, so
+        // the ray state has one version at the loop header -- fewer register copies per trip)
+        const bool any_ray = __ballot(act) != 0;
+        if (!any_ray && !more && buf_lo >= buf_hi) break;  // partition drained, every lane idle
+        if (any_ray) {
+        MCPT_MARK("t_trip");
+        uint32_t itc = 0, ipop = 0;  // node steps / iterations with a pop in the wave, this trip (kCount)
         if constexpr (kCount) {
             ph[PH_TRIPS]++;
             ph[PH_TRIP_NODE] += (uint32_t)__popcll(__ballot(act && ref >= 0));
@@ -1437,11 +1510,12 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         if (act) {
 #pragma unroll 1
           for (int it = 0; it < kNodeSteps; it++) {
+            MCPT_MARK("t_node");
             if constexpr (kCount) itc++;
             bool need_pop = false;
             if (ref >= 0) {
               if constexpr (kCount) tot_n++;
-              const int nx = inv.x < 0.f, ny = inv.y < 0.f, nz = inv.z < 0.f;  // slow-path slab only
+              const int nx = px.y < 0.f, ny = py.y < 0.f, nz = pz.y < 0.f;  // slow-path slab only
               if constexpr (kW == 4) {
                 // 4-wide node: test the four child boxes, visit the nearest hit, push the
                 // other hits far-to-near with their entry t (popped nearest-first)
@@ -1451,18 +1525,20 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 float t0[4], t1[4];
                 bool hk[4];
                 if (__builtin_fabsf(io) < K_INF_F) {  // finite inverse: pair arithmetic
-                    quad_axis(mnx, mxx, o.x, inv.x, t0, t1, true);
-                    quad_axis(mny, mxy, o.y, inv.y, t0, t1, false);
-                    quad_axis(mnz, mxz, o.z, inv.z, t0, t1, false);
+                    quad_axis2(mnx, mxx, px, t0, t1, true);
+                    quad_axis2(mny, mxy, py, t0, t1, false);
+                    quad_axis2(mnz, mxz, pz, t0, t1, false);
 #pragma unroll
                     for (int k = 0; k < 4; k++) hk[k] = t0[k] <= t1[k];
                 } else {
+                    V3 so = RAY_O, si = RAY_INV;
+                    __asm__ volatile("" : "+v"(so.x), "+v"(so.y), "+v"(so.z), "+v"(si.x), "+v"(si.y), "+v"(si.z));
                     const float* fmnx = &mnx.x; const float* fmxx = &mxx.x;
                     const float* fmny = &mny.x; const float* fmxy = &mxy.x;
                     const float* fmnz = &mnz.x; const float* fmxz = &mxz.x;
 #pragma unroll
                     for (int k = 0; k < 4; k++)
-                        hk[k] = slab(fmnx[k], fmny[k], fmnz[k], fmxx[k], fmxy[k], fmxz[k], o, inv, nx, ny, nz, t0[k],
+                        hk[k] = slab(fmnx[k], fmny[k], fmnz[k], fmxx[k], fmxy[k], fmxz[k], so, si, nx, ny, nz, t0[k],
                                      t1[k]);
                 }
                 int rr[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
@@ -1506,13 +1582,19 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 // node layout (SoA pairs): q0 = (mn.x, mn.x', mx.x, mx.x'), q1 = y, q2 = z,
                 // q3 = (child ref, child ref', margin, margin'); unprimed = first child
                 if (__builtin_fabsf(io) < K_INF_F) {  // finite inverse: pair arithmetic
-                    pair_slab(q0, q1, q2, o, inv, a0, b0, a1, b1);
+                    pair_slab2(q0, q1, q2, px, py, pz, a0, b0, a1, b1);
                     h0 = a0 <= b0;
                     h1 = a1 <= b1;
                 } else {
-                    h0 = slab(q0.x, q1.x, q2.x, q0.z, q1.z, q2.z, o, inv, nx, ny, nz, a0, b0);
-                    h1 = slab(q0.y, q1.y, q2.y, q0.w, q1.w, q2.w, o, inv, nx, ny, nz, a1, b1);
+                    MCPT_MARK("rare");  // (an infinite inverse component: the reference's slab)
+                    // the ray through opaque copies made here: the compiler would otherwise build its
+                    // vectorised slab's operand pairs once per trip, for this rarely taken branch
+                    V3 so = RAY_O, si = RAY_INV;
+                    __asm__ volatile("" : "+v"(so.x), "+v"(so.y), "+v"(so.z), "+v"(si.x), "+v"(si.y), "+v"(si.z));
+                    h0 = slab(q0.x, q1.x, q2.x, q0.z, q1.z, q2.z, so, si, nx, ny, nz, a0, b0);
+                    h1 = slab(q0.y, q1.y, q2.y, q0.w, q1.w, q2.w, so, si, nx, ny, nz, a1, b1);
                 }
+                MCPT_MARK("t_node2");
                 // the children's margins ride in q3.z / q3.w (see keep_box)
                 // (evaluated unconditionally: a key assigned only under h0 / h1 costs the
                 // allocator a live range per step -- 7 -> 23 spilled VGPRs)
@@ -1543,6 +1625,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     need_pop = true;
                 }
             }
+            MCPT_MARK("t_pop");
+            if constexpr (kCount) ipop += __ballot(need_pop) != 0 ? 1u : 0u;  // (the active lanes agree)
             if (need_pop) ref = pop();
             if (ref < 0) break;  // parked-leaf slot full or traversal done: wait for the triangle phase
             // the node phase ends for every lane once fewer than kNodeMin still have node work
@@ -1554,12 +1638,17 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
           }
         }
         if constexpr (kCount) {  // the node phase ran as many wave iterations as its busiest lane
-            uint32_t m = itc;
-            for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+            uint32_t m = itc, mp = ipop;
+            for (int off = 32; off > 0; off >>= 1) {
+                m = max(m, (uint32_t)__shfl_xor((int)m, off));
+                mp = max(mp, (uint32_t)__shfl_xor((int)mp, off));
+            }
             ph[PH_NODE_ITERS] += m;
+            ph[PH_POP_ITERS] += mp;
         }
         // ---- triangle phase (wave-uniform): when enough lanes have a parked
         // leaf, or no lane has node work left, each parked leaf tests one triangle
+        MCPT_MARK("t_tri");
         const uint32_t n_tri = (uint32_t)__popcll(__ballot(leaf != kEnd));
         const uint32_t n_node = (uint32_t)__popcll(__ballot(act && ref >= 0));
         if constexpr (kShare) {
@@ -1603,9 +1692,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 const int oa = (int)(ow << 2);
                 const uint32_t k = p - (uint32_t)__builtin_amdgcn_ds_bpermute(oa, (int)excl);
                 const int oleaf = __builtin_amdgcn_ds_bpermute(oa, leaf);
-                const V3 po = v3(__int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(o.x))),
-                                 __int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(o.y))),
-                                 __int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(o.z))));
+                const V3 po = v3(__int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(px.x))),
+                                 __int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(py.x))),
+                                 __int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(pz.x))));
                 const V3 pd = v3(__int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(d.x))),
                                  __int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(d.y))),
                                  __int_as_float(__builtin_amdgcn_ds_bpermute(oa, __float_as_int(d.z))));
@@ -1657,8 +1746,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                                  "v"(w1.w), "v"(w2.x), "v"(w2.y));
                 float t;
                 bool done = false;
-                if (tri_test_t(o, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t) &&
-                    !(t < 0.f) &&
+                const bool acc = tri_test_t(RAY_O, d, v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), v3(w1.z, w1.w, w2.x), t);
+                MCPT_MARK("t_tri2");
+                if (acc && !(t < 0.f) &&
                     (best < 0.f ? t < K_HUGE
                           : (t < best ||
                              (t == best && tri >= 0 && __float_as_int(w2.y) < __float_as_int(sc.tri[kTriF4 * tri + 2].y))))) {
@@ -1683,8 +1773,13 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                 }
             }
         }
+        MCPT_MARK("t_finish");
+        if constexpr (kCount) ph[PH_FINISH_TRIPS] += __ballot(act && ref == kEnd && leaf == kEnd) != 0 ? 1u : 0u;
         if (act && ref == kEnd && leaf == kEnd) finish();
+        }
+        MCPT_MARK("t_end");
     }
+    MCPT_MARK("t_scan");
     // ---- partition scan: read every counter (one lane each) and join the first
     // partition after the current one that still holds rays.  A stale read (this die's
     // L2 holding an old copy of a counter line) can only be lower than the true count, so
@@ -1705,6 +1800,8 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
         enter(63u - (__builtin_amdgcn_readfirstlane(key) & 63u));
     }
     }
+#undef RAY_O
+#undef RAY_INV
     if constexpr (kCount) {
         wave_stats(a.set[0].stats, lane, tot_n - tot_n1, tot_t - tot_t1, tot_h - tot_h1);
         wave_stats(a.set[1].stats, lane, tot_n1, tot_t1, tot_h1);

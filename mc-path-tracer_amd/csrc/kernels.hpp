@@ -145,7 +145,9 @@ enum : int {
     PH_TRIP_NODE = 6,      // lanes with node work at a trip's start
     PH_TRIP_LEAF = 7,      // lanes holding a parked leaf at a trip's start
     PH_TRIP_IDLE = 8,      // lanes without a ray at a trip's start (after the refill)
-    kPhaseWords = 9
+    PH_FINISH_TRIPS = 9,   // trips in which at least one lane finished its ray
+    PH_POP_ITERS = 10,     // node-phase wave iterations in which at least one lane popped the stack
+    kPhaseWords = 11
 };
 struct CounterBlock {
     uint32_t shard[kShards][C_WORDS];  // [0] ext pushes [1] any-hit pushes [2] vis rays [3..8] traversal stats [9,10] rays [11] material pushes

@@ -1253,8 +1253,15 @@ int mcpt_render(mcpt_ctx* c, mcpt_stage_stats* st) {
     mcpt_stage_stats acc{}, one{};
     const uint64_t cap = (uint64_t)(c->cfg.spp + 1) * (uint64_t)(c->cfg.max_depth + 2) + 16;
     uint64_t done = 0;
+    // Iterations per batch (one host synchronisation each).  Once the film is done, the rest of a
+    // batch are no-op launches (~24 us per iteration, mostly dispatching k_shade's grid), so the
+    // first batch is sized to the expected frame -- samples per path slot x (max depth + 1)
+    // iterations, the lockstep schedule of paths that all start together -- and later ones are
+    // short.  (Config 2 at N = 8: 12 iterations of work ran in a batch of 32.)
+    const uint64_t expect = (uint64_t)((c->cfg.spp + c->slots - 1) / c->slots) * (uint64_t)(c->cfg.max_depth + 1);
     for (;;) {
-        if ((rc = run_iterations(c, 32, &one))) return rc;
+        const uint32_t batch = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, expect > done ? expect - done : 0));
+        if ((rc = run_iterations(c, batch, &one))) return rc;
         acc.extend_rays += one.extend_rays;
         acc.shadow_rays += one.shadow_rays;
         acc.vis_rays += one.vis_rays;
@@ -1266,7 +1273,7 @@ int mcpt_render(mcpt_ctx* c, mcpt_stage_stats* st) {
         acc.live_paths = one.live_paths;
         acc.ext_nodes += one.ext_nodes; acc.ext_tests += one.ext_tests; acc.ext_hits += one.ext_hits;
         acc.any_nodes += one.any_nodes; acc.any_tests += one.any_tests; acc.any_hits += one.any_hits;
-        done += 32;
+        done += one.iterations;
         if (one.live_paths == 0 || done > cap) break;
     }
     if (st) *st = acc;
@@ -1421,7 +1428,7 @@ static int stage_run_paths(mcpt_ctx* c, int stage, const mcpt_path_view* in, mcp
     HIPCHK(c, hipEventRecord(ev(c, 1), c->stream));
     HIPCHK(c, hipMemcpyAsync(hc, cnt, sizeof(CounterBlock), hipMemcpyDeviceToHost, c->stream));
     std::vector<float4> o_ro(n), o_rd(n), o_be(n), o_n0(n), o_n1(n), o_ld(n);
-    std::vector<uint32_t> o_fl(n), o_sm(n), o_eq(qn), o_aq(2 * qn);
+    std::vector<uint32_t> o_fl(n), o_sm(n), o_eq(qn);
     std::vector<int32_t> o_ht(n);
     std::vector<uint8_t> o_vis(2 * (size_t)n);
     std::vector<uint4> o_rec(qn);
@@ -1440,7 +1447,6 @@ static int stage_run_paths(mcpt_ctx* c, int stage, const mcpt_path_view* in, mcp
     if (e == hipSuccess) e = dn(o_ht.data(), p.hit_tri, n * sizeof(int32_t));
     if (e == hipSuccess) e = dn(o_vis.data(), p.vis, 2 * (size_t)n);
     if (e == hipSuccess) e = dn(o_eq.data(), ext_q, qn * sizeof(uint32_t));
-    if (e == hipSuccess) e = dn(o_aq.data(), any_q, 2 * qn * sizeof(uint32_t));
     if (e == hipSuccess) e = dn(o_rec.data(), mrec, qn * sizeof(uint4));
     if (e == hipSuccess) e = dn(o_rb.data(), mbeta, qn * sizeof(float4));
     if (e == hipSuccess) e = dn(o_so.data(), p.sray_o, 2 * qn * sizeof(float4));
@@ -1462,7 +1468,9 @@ static int stage_run_paths(mcpt_ctx* c, int stage, const mcpt_path_view* in, mcp
             }
         for (uint32_t k = 0; k < hc->shard[sh][C_ANY]; k++) {
             const size_t q = (size_t)sh * any_cap + k;
-            const uint32_t r = o_aq[q], pid = r >> 1;
+            uint32_t r;  // the ray's result index (2 pid + BRDF ray) rides in its origin's .w
+            memcpy(&r, &o_so[q].w, sizeof(r));
+            const uint32_t pid = r >> 1;
             float* so = (r & 1) ? bo.data() : lo.data();
             float* sd = (r & 1) ? bd.data() : ldr.data();
             queued[pid] |= (r & 1) ? 8 : 4;

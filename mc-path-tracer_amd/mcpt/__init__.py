@@ -575,7 +575,7 @@ class PathTracer:
         v = (C.c_uint64 * 12)()
         n = lib().mcpt_debug_trace_profile(self.h, v, int(reset))
         names = ("trips", "refills", "refill_lanes", "node_iters", "tri_phases", "tri_lanes", "trip_node_lanes",
-                 "trip_leaf_lanes", "trip_idle_lanes")
+                 "trip_leaf_lanes", "trip_idle_lanes", "finish_trips", "pop_iters")
         return {k: int(x) for k, x in zip(names, v)} if n > 0 else None
 
     def hbm_copy_gbps(self, nbytes=1 << 30, iters=20) -> float:

@@ -452,3 +452,16 @@ def test_stage_golden_vectors_oracle(mcpt_mod, oracle, stage):
     for k, v in out.items():
         ref = g["out_" + k]
         assert np.array_equal(np.asarray(v).view(np.uint8), ref.view(np.uint8)), k
+
+
+def test_udiv_small_exact():
+    """k_shade's udiv_small (kernels.hip): floor(n / d) from the truncated fp32 product n * RN32(1/d)
+    plus one correction, for every sample index n < 2^19 (kMaxSpp) and path-slot count d <= 256
+    (the ABI's range) -- the float estimate is never above the quotient and at most one below."""
+    n = np.arange(1 << 19, dtype=np.uint32)
+    nf = n.astype(np.float32)
+    for d in range(1, 257):
+        r = np.float32(1.0) / np.float32(d)
+        q = (nf * r).astype(np.uint32)  # v_mul_f32 (RN) then v_cvt_u32_f32 (toward zero)
+        q = q + ((n - q * np.uint32(d)) >= d).astype(np.uint32)
+        assert np.array_equal(q, n // np.uint32(d)), d

@@ -1,7 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --config 2 --steps 2 --warmup 1 > gpurun_out/c2_share.json 2> gpurun_out/c2_share.err || { tail -20 gpurun_out/c2_share.err; exit 1; }
-MCPT_LIB=$PWD/mc-path-tracer_amd/libmcpt_base.so timeout -k 10 300 python -u bench.py --no-cpu-baseline --config 2 --steps 2 --warmup 1 > gpurun_out/c2_base.json 2> gpurun_out/c2_base.err || { tail -20 gpurun_out/c2_base.err; exit 1; }
-MCPT_LIB=$PWD/mc-path-tracer_amd/libmcpt_diagshade.so timeout -k 10 300 python -u tools/shade_sections.py --config 2 --out gpurun_out/shade_sections_c2.json > gpurun_out/shade_sections.log 2>&1 || { tail -20 gpurun_out/shade_sections.log; exit 1; }
-CONFIG=2 TAG=r06x ENVS="MCPT_TRI_MIN=32|MCPT_TRI_MIN=48|MCPT_TRI_MIN=8" ROUNDS=1 bash tools/gpu/run.sh abenv
+rm -rf gpurun_out/rk8
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --config 2 --steps 1 --warmup 0 > gpurun_out/c2_phases.json 2> gpurun_out/c2_phases.err || { tail -20 gpurun_out/c2_phases.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/rk8 -o rk --output-format csv -- python3 tools/rank_frames.py --config 2 --world 8 --rank 0 --frames 2 > gpurun_out/rk8.log 2>&1 || { tail -20 gpurun_out/rk8.log; exit 1; }
+grep frame gpurun_out/rk8.log
+python3 tools/iter_gaps.py 'gpurun_out/rk8/**/*kernel_trace.csv' > gpurun_out/rk8_gaps.json && cat gpurun_out/rk8_gaps.json
