@@ -1361,15 +1361,13 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
             }
         }
         if (kind) {
-            // a dense any-hit set (ray_at_slot: rid is the ray's queue position) carries the result
-            // index in o.w and the occluder-table cell in d.w (k_material)
-            const bool rec = a.set[1].ray_at_slot != 0;
-            const uint32_t vi = rec ? __float_as_uint(a.set[1].ro[rid].w) : rid;
-            if constexpr (MCPT_NT & 4) __builtin_nontemporal_store((uint8_t)(tri < 0), a.vis + vi);
-            else a.vis[vi] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
+            // (rid: the result index -- a dense set's ray carried it in o.w, see the refill)
+            if constexpr (MCPT_NT & 4) __builtin_nontemporal_store((uint8_t)(tri < 0), a.vis + rid);
+            else a.vis[rid] = (uint8_t)(tri < 0);  // wf_shadow (wavefront_kernels.cu:274-293)
             if (tri >= 0 && occ_rec) {  // the cell's occluder (occ_hit1)
-                const uint32_t cell = rec ? __float_as_uint(a.set[1].rd[rid].w) : occ_index(sc, RAY_O, d);
-                uint32_t* w = sc.occ + (size_t)cell * kOccWays + (uint32_t)tri % kOccWays;
+                // (hashed again here rather than kept from d.w: a register held over the whole
+                // traversal, or a reload of the record, costs more than the hash on occluded rays)
+                uint32_t* w = sc.occ + (size_t)occ_index(sc, RAY_O, d) * kOccWays + (uint32_t)tri % kOccWays;
                 if constexpr (MCPT_NT & 16) __builtin_nontemporal_store((uint32_t)tri, w);
                 else *w = (uint32_t)tri;
             }
@@ -1442,7 +1440,6 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                     // positions) issues its ray loads with the queue-entry load, not after it
                     const bool at_slot = kind ? a.set[1].ray_at_slot : a.set[0].ray_at_slot;
                     float4 o4, d4;
-                    // (a dense set's ray keeps its queue position as rid: its result index rides in o.w)
                     if constexpr (MCPT_NT & 4) {
                         rid = at_slot ? qslot : (qp ? __builtin_nontemporal_load(qp + qslot) : qslot);
                         o4 = ld_s(rop + rid);
@@ -1452,6 +1449,9 @@ __global__ __launch_bounds__(kTraceBlock) MCPT_TRACE_ATTR void k_trace(TraceArgs
                         o4 = rop[rid];
                         d4 = rdp[rid];
                     }
+                    // a dense set's ray carries its result index in o.w (k_material): the finish
+                    // writes there, with no queue entry loaded or record re-read
+                    if (at_slot) rid = __float_as_uint(o4.w);
                     px.x = o4.x;
                     py.x = o4.y;
                     pz.x = o4.z;

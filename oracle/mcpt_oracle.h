@@ -145,6 +145,13 @@ uint64_t or_model_tri_tests(void); /* triangle tests of the last or_model_trace 
 void or_model_trace(const or_scene *sc, int32_t n, const float *ro, const float *rd, int32_t mode,
                     const float *node_w, const float *tri_w, float p, int32_t *tri, float *t, uint8_t *visible,
                     uint64_t *nodes);
+/* traversal study (trav_model.c): per-ray steps / origin-box steps / triangle tests / outcome and
+ * the 128-B lines fetched under a node numbering; or_lru_sim: LRU misses over those line streams */
+void or_model_study(const or_scene *sc, int32_t n, const float *ro, const float *rd, int32_t mode, int32_t kind,
+                    const float *node_w, const float *tri_w, float p, const int32_t *pair_line, int32_t tri_line0,
+                    int32_t *steps, int32_t *origin_steps, int32_t *tris, uint8_t *hit, int32_t *lines, int64_t cap,
+                    int64_t *off);
+int64_t or_lru_sim(const int32_t *lines, const int64_t *off, int32_t n, int32_t batch, int32_t sets, int32_t ways);
 
 #ifdef __cplusplus
 }

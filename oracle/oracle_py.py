@@ -79,6 +79,10 @@ def lib():
             "or_model_tri_tests": (C.c_uint64, []),
             "or_model_trace": (None, [C.POINTER(OrScene), C.c_int32, _f, _f, C.c_int32, _f, _f, C.c_float, _i, _f,
                                       C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)]),
+            "or_model_study": (None, [C.POINTER(OrScene), C.c_int32, _f, _f, C.c_int32, C.c_int32, _f, _f, C.c_float,
+                                      _i, C.c_int32, _i, _i, _i, C.POINTER(C.c_uint8), _i, C.c_int64,
+                                      C.POINTER(C.c_int64)]),
+            "or_lru_sim": (C.c_int64, [_i, C.POINTER(C.c_int64), C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
         }
         for n, (r, a) in sig.items():
             fn = getattr(l, n)
@@ -255,6 +259,37 @@ def model_trace(arrays, ro, rd, mode, margins=None, nthreads=1, safe_c=0.0):
     finally:
         lib().or_model_set_safe(0.0)
     return tri, t, vis, boxes
+
+
+def model_study(arrays, ro, rd, mode, kind, pair_line, tri_line0, margins=None, cap_per_ray=256):
+    """trav_model.c or_model_study: per ray (steps, origin-box steps, triangle tests, hit) and the
+    128-B line stream of its traversal under the node numbering pair_line (analysis only)."""
+    s = scene_struct(arrays)
+    m = margins or model_margins(arrays)
+    ro = np.ascontiguousarray(ro, np.float32).reshape(-1, 3)
+    rd = np.ascontiguousarray(rd, np.float32).reshape(-1, 3)
+    n = len(ro)
+    pl = np.ascontiguousarray(pair_line, np.int32)
+    steps, osteps, tris = (np.zeros(n, np.int32) for _ in range(3))
+    hit = np.zeros(n, np.uint8)
+    cap = n * cap_per_ray
+    lines = np.zeros(cap, np.int32)
+    off = np.zeros(n + 1, np.int64)
+    lib().or_model_study(C.byref(s), n, fptr(ro), fptr(rd), mode, kind, fptr(m["node_w"]), fptr(m["tri_w"]), m["p"],
+                         pl.ctypes.data_as(_i), int(tri_line0), steps.ctypes.data_as(_i), osteps.ctypes.data_as(_i),
+                         tris.ctypes.data_as(_i), hit.ctypes.data_as(C.POINTER(C.c_uint8)), lines.ctypes.data_as(_i),
+                         C.c_int64(cap), off.ctypes.data_as(C.POINTER(C.c_int64)))
+    if off[-1] > cap:
+        raise ValueError("line buffer too small: raise cap_per_ray")
+    return {"steps": steps, "origin_steps": osteps, "tris": tris, "hit": hit, "lines": lines[:off[-1]], "off": off}
+
+
+def lru_sim(lines, off, batch, sets, ways):
+    """trav_model.c or_lru_sim: misses of a sets x ways LRU over the rays' line streams."""
+    lines = np.ascontiguousarray(lines, np.int32)
+    off = np.ascontiguousarray(off, np.int64)
+    return int(lib().or_lru_sim(lines.ctypes.data_as(_i), off.ctypes.data_as(C.POINTER(C.c_int64)), len(off) - 1,
+                                int(batch), int(sets), int(ways)))
 
 
 def model_tri_tests():

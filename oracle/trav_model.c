@@ -225,6 +225,35 @@ static int m_keep(int mode, float t0, float t1, float w, const mray *r, float cu
 
 static int tri_key(const or_scene *sc, int id) { return sc->tri_id ? sc->tri_id[id] : id; }
 
+/* Traversal study (or_model_study): what one m_trace call visits, recorded when g_rec is set */
+typedef struct {
+    const int32_t *pair_line; /* desc node -> 128-B line of its child pair, or of a multi-triangle
+                               * leaf's first expansion pair (the layout under study) */
+    int32_t tri_line0;        /* first line of the 48-B triangle records */
+    int32_t steps, origin_steps, tris;
+    int32_t *lines;
+    int64_t n, cap;
+} study_rec;
+static __thread study_rec *g_rec = NULL;
+static void rec_line(int32_t l) {
+    if (g_rec->n < g_rec->cap) g_rec->lines[g_rec->n] = l;
+    g_rec->n++;
+}
+static void rec_step(const or_scene *sc, int cur, mv3 o) {
+    if (!g_rec) return;
+    g_rec->steps++;
+    const float *mn = sc->bmin + 3 * (int64_t)cur, *mx = sc->bmax + 3 * (int64_t)cur;
+    g_rec->origin_steps += mn[0] <= o.x && o.x <= mx[0] && mn[1] <= o.y && o.y <= mx[1] && mn[2] <= o.z && o.z <= mx[2];
+    rec_line(g_rec->pair_line[cur]);
+}
+static void rec_tri(int id) {
+    if (!g_rec) return;
+    g_rec->tris++;
+    const int64_t b0 = (int64_t)id * 48, b1 = b0 + 47;
+    rec_line(g_rec->tri_line0 + (int32_t)(b0 >> 7));
+    if ((b1 >> 7) != (b0 >> 7)) rec_line(g_rec->tri_line0 + (int32_t)(b1 >> 7));
+}
+
 /* triangle tests of the last or_model_trace call (its rays, both kinds): work counts for the
  * culling variants (single-threaded callers only) */
 static uint64_t g_tri_tests = 0;
@@ -264,6 +293,7 @@ static int m_trace(const or_scene *sc, int mode, const float *node_w, const floa
     for (;;) {
         if (sc->nprims[cur] > 0) {
             const int np = sc->nprims[cur];
+            if (g_rec && np > 1) rec_line(g_rec->pair_line[cur]);  /* the leaf's expansion pairs */
             for (int i = 0; i < np; i++) {
                 const int id = sc->offset[cur] + i;
                 if (np > 1) {  /* own box (the product's one-triangle leaves) */
@@ -278,6 +308,7 @@ static int m_trace(const or_scene *sc, int mode, const float *node_w, const floa
                 }
                 float t;
                 g_tri_tests++;
+                rec_tri(id);
                 if (m_tri(sc, id, o, d, &t) && !(t < 0.f)) {
                     if (kind) {
                         if (t < M_HUGE) { *tout = t; return 1; }
@@ -291,6 +322,7 @@ static int m_trace(const or_scene *sc, int mode, const float *node_w, const floa
         } else {
             const int c[2] = {cur + 1, sc->offset[cur]};
             int h[2];
+            rec_step(sc, cur, o);
             float k2[2];
             for (int j = 0; j < 2; j++) {
                 (*nodes)++;
@@ -381,4 +413,75 @@ void or_model_trace(const or_scene *sc, int32_t n, const float *ro, const float 
     }
     free(pl);
     *nodes = nn;
+}
+
+/* Round-6 traversal study, analysis only: per ray of `kind` (0 closest, 1 any
+ * hit) under rule `mode`, the pair steps, the steps whose node box contains the ray origin, the
+ * triangle tests and the outcome (hit / occluded); and the 128-B lines those steps fetch under a
+ * node numbering: pair_line[node] for an interior desc node's child pair, tri_line0 + the lines of
+ * triangle record id (48 B each).  Lines of ray i: lines[off[i] .. off[i+1]) (truncated at cap;
+ * off[n] is the full count). */
+void or_model_study(const or_scene *sc, int32_t n, const float *ro, const float *rd, int32_t mode, int32_t kind,
+                    const float *node_w, const float *tri_w, float p, const int32_t *pair_line, int32_t tri_line0,
+                    int32_t *steps, int32_t *origin_steps, int32_t *tris, uint8_t *hit, int32_t *lines, int64_t cap,
+                    int64_t *off) {
+    study_rec r;
+    memset(&r, 0, sizeof r);
+    r.pair_line = pair_line;
+    r.tri_line0 = tri_line0;
+    r.lines = lines;
+    r.cap = cap;
+    g_rec = &r;
+    uint64_t nn = 0;
+    for (int32_t i = 0; i < n; i++) {
+        off[i] = r.n;
+        r.steps = r.origin_steps = r.tris = 0;
+        float tb;
+        const int res = m_trace(sc, mode, node_w, tri_w, p, mld(ro, i), mld(rd, i), kind, &tb, &nn);
+        steps[i] = r.steps;
+        origin_steps[i] = r.origin_steps;
+        tris[i] = r.tris;
+        hit[i] = (uint8_t)(kind ? res != 0 : res >= 0);
+    }
+    off[n] = r.n;
+    g_rec = NULL;
+}
+
+/* Misses of a set-associative LRU cache (sets x ways lines) over the line streams of n rays, the
+ * rays taken `batch` at a time and interleaved one access per ray per round (a crude model of the
+ * rays in flight on one L2). */
+int64_t or_lru_sim(const int32_t *lines, const int64_t *off, int32_t n, int32_t batch, int32_t sets, int32_t ways) {
+    int32_t *tag = malloc(sizeof(int32_t) * (size_t)sets * ways);
+    uint32_t *age = malloc(sizeof(uint32_t) * (size_t)sets * ways);
+    int64_t *cur = malloc(sizeof(int64_t) * (size_t)(batch > 0 ? batch : 1));
+    for (int64_t k = 0; k < (int64_t)sets * ways; k++) { tag[k] = -1; age[k] = 0; }
+    uint32_t clock = 0;
+    int64_t miss = 0;
+    for (int32_t b0 = 0; b0 < n; b0 += batch) {
+        const int32_t nb = n - b0 < batch ? n - b0 : batch;
+        for (int32_t j = 0; j < nb; j++) cur[j] = off[b0 + j];
+        int live = 1;
+        while (live) {
+            live = 0;
+            for (int32_t j = 0; j < nb; j++) {
+                if (cur[j] >= off[b0 + j + 1]) continue;
+                live = 1;
+                const int32_t l = lines[cur[j]++];
+                const int32_t s = (int32_t)((uint32_t)l % (uint32_t)sets);
+                int32_t *tg = tag + (int64_t)s * ways;
+                uint32_t *ag = age + (int64_t)s * ways;
+                int w = -1, lru = 0;
+                for (int k = 0; k < ways; k++) {
+                    if (tg[k] == l) { w = k; break; }
+                    if (ag[k] < ag[lru]) lru = k;
+                }
+                if (w < 0) { miss++; w = lru; tg[w] = l; }
+                ag[w] = ++clock;
+            }
+        }
+    }
+    free(tag);
+    free(age);
+    free(cur);
+    return miss;
 }

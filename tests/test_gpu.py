@@ -762,20 +762,26 @@ def test_trace_schedule_knobs_same_film(mcpt_mod, scene_c2, knob):
 
 
 def test_node_layouts_same_hits(mcpt_mod, oracle, scene_c2):
-    """Pair-node numberings 0 (depth-first), 1 (sibling pairs, depth-first) and 2 (breadth-first)
-    are layout only: bit-identical hits and visibility; out-of-range MCPT_SIBLING_LAYOUT values
-    are ignored (the size-based default, 2 for config 2's small tree)."""
+    """Pair-node numberings 0 (depth-first), 1 (sibling pairs, depth-first), 2 (breadth-first) and
+    3 (line pairs with pad nodes) are layout only: bit-identical hits and visibility, also through
+    4-wide nodes collapsed from layout 3's pairs; out-of-range MCPT_SIBLING_LAYOUT values are
+    ignored (the size-based default, 2 for config 2's small tree)."""
     s, a = scene_c2
     ro, rd = random_rays(100000, 33)
     ref = None
     old = os.environ.get("MCPT_SIBLING_LAYOUT")
     try:
-        for layout in ("0", "1", "2", "3", "x"):
+        for layout, width in (("0", None), ("1", None), ("2", None), ("3", None), ("3", "4"), ("4", None), ("x", None)):
             os.environ["MCPT_SIBLING_LAYOUT"] = layout
-            pt = mcpt_mod.PathTracer(0)
-            pt.upload_scene(s)
+            if width:
+                os.environ["MCPT_BVH_WIDTH"] = width
+            try:
+                pt = mcpt_mod.PathTracer(0)
+                pt.upload_scene(s)
+            finally:
+                os.environ.pop("MCPT_BVH_WIDTH", None)
             got = mcpt_mod.lib().mcpt_debug_node_layout(pt.h)
-            assert got == (int(layout) if layout in "012" else 2)
+            assert got == (int(layout) if layout in "0123" else 2)
             p, n, t = pt.trace_closest(ro, rd)
             v = pt.trace_any(ro, rd)
             if ref is None:
