@@ -2,6 +2,7 @@
 # A/B of whole-frame bench runs between library builds on one box (interleaved):
 #   LIBS="new:mc-path-tracer_amd/libmcpt.so r3:mc-path-tracer_amd/libmcpt_r3.so" CONFIGS="2 3" ROUNDS=2 \
 #   TEST=1 bash tools/gpu/ab_libs.sh
+# An entry may set environment variables for its runs: "l3:mc-path-tracer_amd/libmcpt.so:MCPT_SIBLING_LAYOUT=3".
 # TEST=1 first runs the GPU test suite on the default library.  Every GPU step has its own limit.
 set -o pipefail
 mkdir -p gpurun_out
@@ -13,8 +14,10 @@ fi
 for r in $(seq ${ROUNDS:-2}); do
   for cfg in ${CONFIGS:-2}; do
     for lv in ${LIBS}; do
-      name=${lv%%:*}; lib=${lv#*:}
-      MCPT_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py --no-cpu-baseline --config $cfg --steps ${STEPS:-4} --warmup 1 ${BENCH_ARGS} > gpurun_out/ab_$name.json 2> gpurun_out/ab_$name.err || { tail -20 gpurun_out/ab_$name.err; exit 1; }
+      # name:lib[:VAR=VAL,VAR=VAL] -- optional environment for that entry
+      name=${lv%%:*}; spec=${lv#*:}; lib=${spec%%:*}; envs=${spec#"$lib"}; envs=${envs#:}
+      ( [[ -n "$envs" ]] && export ${envs//,/ }
+      MCPT_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py --no-cpu-baseline --config $cfg --steps ${STEPS:-4} --warmup 1 ${BENCH_ARGS} > gpurun_out/ab_$name.json 2> gpurun_out/ab_$name.err || { tail -20 gpurun_out/ab_$name.err; exit 1; } ) || exit 1
       python - "$name" "$cfg" "gpurun_out/ab_$name.json" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[3])); r = d["roofline"]; p = r["per_ray"]
