@@ -151,6 +151,7 @@ void or_model_study(const or_scene *sc, int32_t n, const float *ro, const float 
                     const float *node_w, const float *tri_w, float p, const int32_t *pair_line, int32_t tri_line0,
                     int32_t *steps, int32_t *origin_steps, int32_t *tris, uint8_t *hit, int32_t *lines, int64_t cap,
                     int64_t *off);
+void or_model_set_any_order(int32_t m); /* study: any-hit visiting order (0 near-first) */
 int64_t or_lru_sim(const int32_t *lines, const int64_t *off, int32_t n, int32_t batch, int32_t sets, int32_t ways);
 
 #ifdef __cplusplus

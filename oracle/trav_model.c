@@ -259,6 +259,20 @@ static void rec_tri(int id) {
 static uint64_t g_tri_tests = 0;
 uint64_t or_model_tri_tests(void) { return g_tri_tests; }
 
+/* Any-hit visiting order under study (or_model_set_any_order; the product visits near-first):
+ * 1 the child with the larger box surface first, 2 the far child first */
+static int g_any_order = 0;
+void or_model_set_any_order(int32_t m) { g_any_order = m; }
+static double m_area(const or_scene *sc, int i) {
+    const float *mn = sc->bmin + 3 * (int64_t)i, *mx = sc->bmax + 3 * (int64_t)i;
+    const double x = fmax(mx[0] - mn[0], 0.0), y = fmax(mx[1] - mn[1], 0.0), z = fmax(mx[2] - mn[2], 0.0);
+    return x * y + y * z + z * x;
+}
+static int m_any_first(const or_scene *sc, const int c[2], const float k2[2]) {
+    if (g_any_order == 1) return m_area(sc, c[1]) > m_area(sc, c[0]);
+    return k2[1] > k2[0];
+}
+
 /* kind 0: closest hit (index, t), kind 1: any hit (1 = occluded) */
 static int m_trace(const or_scene *sc, int mode, const float *node_w, const float *tri_w, float pg, mv3 o, mv3 d,
                    int kind, float *tout, uint64_t *nodes) {
@@ -330,7 +344,8 @@ static int m_trace(const or_scene *sc, int mode, const float *node_w, const floa
                        m_keep(mode, t0, t1, node_w[c[j]], &r, cut, &k2[j]);
             }
             if (h[0] && h[1]) {
-                const int f = k2[1] < k2[0];
+                int f = k2[1] < k2[0];
+                if (kind && g_any_order) f = m_any_first(sc, c, k2);
                 stack[sp] = c[1 - f];
                 skey[sp++] = k2[1 - f];
                 cur = c[f];
