@@ -624,13 +624,12 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
             mo.trivial_any++;
         } else {
             // staged: stored at its any-queue position after the block push, with the ray's
-            // result index (vis) in o.w and its occluder-table cell in d.w (k_trace's finish)
-            const uint32_t cell = sc.occ ? occ_index(sc, so_l, ldir) : 0u;
+            // result index (vis) in o.w (k_trace's refill keeps it for the finish)
             stage[0 * kBlock + threadIdx.x] = f4(so_l, __uint_as_float(2 * pid));
-            stage[1 * kBlock + threadIdx.x] = f4(ldir, __uint_as_float(cell));
+            stage[1 * kBlock + threadIdx.x] = f4(ldir, 0.f);
             mo.want_l = true;
             // the occluder-cache entry, loaded now and used after material()
-            if (occ_on) mo.el = occ_entry(sc, cell);
+            if (occ_on) mo.el = occ_entry(sc, occ_index(sc, so_l, ldir));
         }
     }
     // the BRDF sample's direction and visibility ray (its light terms come after the occluder
@@ -647,10 +646,9 @@ __device__ inline MatOut material(const ShadeArgs& a, uint32_t pid, uint32_t pix
             a.p.vis[2 * pid + 1] = 1;
             mo.trivial_any++;
         } else {
-            const uint32_t cell = sc.occ ? occ_index(sc, so_b, wi_b) : 0u;
-            if (occ_on) mo.eb = occ_entry(sc, cell);
+            if (occ_on) mo.eb = occ_entry(sc, occ_index(sc, so_b, wi_b));
             stage[2 * kBlock + threadIdx.x] = f4(so_b, __uint_as_float(2 * pid + 1));
-            stage[3 * kBlock + threadIdx.x] = f4(wi_b, __uint_as_float(cell));
+            stage[3 * kBlock + threadIdx.x] = f4(wi_b, 0.f);
             mo.want_b = true;
         }
     }
