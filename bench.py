@@ -78,7 +78,6 @@ NON_PRODUCT_KNOBS = {
     "MCPT_SHADE_WGS": "k_shade grid (absolute)",
     "MCPT_NO_BLOCK_DONE": "k_shade finished-block skip off",
     "MCPT_SIBLING_LAYOUT": "BVH sibling layout",
-    "MCPT_SHARD_BANDS": "k_shade queue shards by image band forced",
     "MCPT_BVH_WIDTH": "BVH node width forced",
     "MCPT_BVH_ISOLATE": "BVH isolation of unbounded triangles switched",
     "MCPT_GPU_BVH": "device-built BVH instead of the host SAH",

@@ -710,8 +710,7 @@ __device__ inline void material_brdf_terms(const ShadeArgs& a, uint32_t pid, con
 //   x0, y0: film position of the block's first pixel (with tile_w a multiple of kBlock a block is one
 //           run of a tile row, pixel x0 + k; otherwise x0, y0 are the tile's corner);
 //   loc0:   path index within the slot of the first pixel (ShadeArgs::npx);
-//   sr:     path slot | pixels of the block inside its tile << 8 (kBlock for all but a tile's last) |
-//           queue shard << 24 (shade_shard);
+//   sr:     path slot | pixels of the block inside its tile << 8 (kBlock for all but a tile's last);
 //   li0:    the first pixel's index in its tile;
 //   done:   its finished-block flag, kept per slot, film tile and block so it outlives a change of
 //           tile set.
@@ -738,8 +737,7 @@ __device__ inline VBlk vblock_of(const ShadeArgs& a, int vb) {
     }
     // path index (ShadeArgs::npx): the pixel id, or its place in the compact tile-set layout
     r.loc0 = a.compact ? (uint32_t)(a.tile_base ? a.tile_base[tile] : tile) * (uint32_t)tile_px + (uint32_t)li0 : 0u;
-    r.sr = (uint32_t)slot | ((uint32_t)min(tile_px - li0, kBlock) << 8) |
-           (shade_shard((uint32_t)vb, (uint32_t)bs, (uint32_t)per_slot, a.shard_bands != 0) << 24);
+    r.sr = (uint32_t)slot | ((uint32_t)min(tile_px - li0, kBlock) << 8);
     r.li0 = (uint32_t)li0;
     const uint32_t ntx = (uint32_t)((a.W + a.tile_w - 1) / a.tile_w), nty = (uint32_t)((a.H + a.tile_h - 1) / a.tile_h);
     r.done = (((uint32_t)slot * nty + (uint32_t)t.y) * ntx + (uint32_t)t.x) * (uint32_t)bpt + (uint32_t)bib;
@@ -759,7 +757,7 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
     const DevScene& sc = a.scene;
     const int slot = (int)(v.sr & 0xffu);
     const int lane = threadIdx.x & 63;
-    bool valid = (int)threadIdx.x < (int)((v.sr >> 8) & 0xffffu);
+    bool valid = (int)threadIdx.x < (int)(v.sr >> 8);
     uint32_t pid = 0, pix = 0;  // path id (slot * pixels + pixel) and pixel id
     int x = 0, y = 0;
     if (valid) {
@@ -923,7 +921,7 @@ __device__ __attribute__((always_inline)) inline void shade_vblock(const ShadeAr
     // ---- pushes: generated extension rays and continuing paths (material queue); one
     // atomic per block and queue.  A continuing path's record and updated throughput go
     // to k_material densely (it writes p.beta with f_s/pdf_s in .w).
-    const int shard = (int)(v.sr >> 24);  // (shade_shard: the queues' capacity counts its blocks per shard)
+    const int shard = vb % kShards;  // the queues' capacity assumes <= kBlock pushes per block and shard
     uint32_t* sc_ctr = a.cnt->shard[shard];
     {
         bool want[2] = {gen_ext, cont};

@@ -130,21 +130,6 @@ struct DevPaths {
 // statistics adds per iteration would otherwise cost.
 constexpr int kShards = 64;
 constexpr int kMaxParts = kShards;  // k_trace work partitions (at most one per queue shard)
-// Queue shard of k_shade's shading block vb (pb: its index within its path slot, per_slot blocks per
-// slot).  Interleaved (bands false): vb mod kShards.  Image bands (ShadeArgs::shard_bands, trees beyond
-// the L2): a slot's blocks in kBands contiguous runs of the tile set (rows of tiles: one image region
-// each), band b on partition (b mod 2) * kBandDies + b / 2 -- k_trace homes partition q on die
-// q mod kBandDies at the default kBands partitions, so a die's two partitions hold two adjacent bands --
-// and a band's blocks dealt over its kShards / kBands shards.  A die's L2 then caches the part of the
-// tree around its region's hit points, which its rays' first steps visit.  Any other partition count
-// keeps the mapping correct (shard s still goes to partition s mod nparts), only not die-aligned.
-constexpr uint32_t kBands = 16, kBandDies = 8;
-__host__ __device__ inline uint32_t shade_shard(uint32_t vb, uint32_t pb, uint32_t per_slot, bool bands) {
-    if (!bands) return vb % (uint32_t)kShards;
-    const uint32_t b = pb * kBands / per_slot;  // pb < 2^27: no overflow
-    const uint32_t q = (b % (kBands / kBandDies)) * kBandDies + b / (kBands / kBandDies);
-    return q + kBands * (pb % ((uint32_t)kShards / kBands));
-}
 enum : int { C_EXT = 0, C_ANY = 1, C_VIS = 2, C_STATS = 3, C_EXT_RAYS = 9, C_ANY_RAYS = 10, C_MAT = 11, C_OCC = 12,
               C_OCC_TRY = 13, C_PH = 14, C_WORDS = 32 };  // C_STATS..+5; C_OCC / C_OCC_TRY: any-hit rays resolved by /
                                                           // tested against the occluder cache; C_PH..+kPhaseWords-1:
@@ -216,7 +201,6 @@ struct ShadeArgs {
     // pixel's focal point (thin lens) or pinhole origin in cam_px, the pinhole direction in cam_dir
     const float4* cam_px;
     const float4* cam_dir;
-    int shard_bands;  // k_shade's queue shards by image band (shade_shard); 0: interleaved
 };
 
 // One ray set of a trace launch: rays ro/rd[rid] for queue entries

@@ -48,7 +48,6 @@ struct mcpt_ctx {
     // per-lane counters cost the fast one its spill-free registers -- off by default
     bool count_work = getenv("MCPT_WORK_COUNTERS") != nullptr;
     int node_layout = 0;  // pair-node numbering the last upload used (mcpt_debug_node_layout)
-    bool shard_bands = false;  // k_shade's queue shards by image band (set at scene upload, shade_shard)
     // camera
     mcpt::CamView cam{};
     bool has_cam = false;
@@ -629,11 +628,6 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     const size_t tree_pairs = gpu_bvh ? (size_t)lb.nnodes : pn.size() / 4;
     uint32_t nnodes = (uint32_t)tree_pairs;  // nodes of the uploaded width (the leaf-box pass)
     int width = tree_pairs * 64 > ((size_t)32 << 20) ? 4 : 2;
-    // k_shade's queue shards by image band (shade_shard): a die's L2 caches the tree around its
-    // region's hit points.  MCPT_SHARD_BANDS=0/1 forces it; off by default until measured.
-    c->shard_bands = false;
-    if (const char* e = getenv("MCPT_SHARD_BANDS"))
-        if ((e[0] == '0' || e[0] == '1') && e[1] == 0) c->shard_bands = e[0] == '1';
     if (const char* we = getenv("MCPT_BVH_WIDTH"))
         if ((we[0] == '2' || we[0] == '4') && we[1] == 0) width = we[0] - '0';
     int quad_root = 0, quad_push = 0;
@@ -879,15 +873,9 @@ int mcpt_camera_set(mcpt_ctx* c, const mcpt_camera* cam) {
 }
 
 static int set_tiles_internal(mcpt_ctx* c, const std::vector<int2>& t) {
-    // per-shard queue capacity: the most k_shade blocks any shard takes (a block pushes <= one ray per
-    // thread) under either shard mapping (shade_shard: block mod kShards, or the image bands of a
-    // launch over the whole set -- the same for every slot)
+    // per-shard queue capacity: shard = k_shade block mod kShards (a block pushes <= one ray per thread)
     const uint32_t nblocks = (uint32_t)t.size() * (uint32_t)shade_blocks_per_tile((int)(c->tile_w * c->tile_h), (int)c->slots);
-    const uint32_t per_slot = (uint32_t)t.size() * (uint32_t)shade_blocks_per_tile((int)(c->tile_w * c->tile_h), 1);
-    uint32_t banded[kShards] = {}, most = (nblocks + kShards - 1) / kShards;
-    for (uint32_t pb = 0; pb < per_slot; pb++) banded[shade_shard(0, pb, per_slot, true)]++;
-    for (uint32_t k = 0; k < (uint32_t)kShards; k++) most = std::max(most, banded[k] * (uint32_t)c->slots);
-    c->ext_cap = std::max<uint32_t>(1, most) * kBlock;
+    c->ext_cap = std::max<uint32_t>(1, (nblocks + kShards - 1) / kShards) * kBlock;
     c->any_cap = 2 * c->ext_cap;
     const size_t need = (size_t)kShards * c->ext_cap;
     if (need > c->queue_alloc) {
@@ -1176,9 +1164,6 @@ static int enqueue_iteration(mcpt_ctx* c, size_t evbase, bool timing, const int2
     sa.any_cap = c->any_cap;
     sa.cnt = c->cnt;
     sa.blk_done = c->blk_done_off ? nullptr : c->blk_done;
-    // image-band shards (shade_shard) only for a launch over the whole tile set, whose block counts
-    // per shard the queue capacity was sized for (set_tiles_internal)
-    sa.shard_bands = c->shard_bands && ntiles == (int)c->tiles_h.size() ? 1 : 0;
     if (int rc = cam_table(c, c->W, c->H, &sa.cam_px, &sa.cam_dir)) return rc;
     const int bpt = shade_blocks_per_tile((int)(c->tile_w * c->tile_h), (int)c->slots);
     if (timing) HIPCHK(c, hipEventRecord(ev(c, evbase + 0), c->stream));

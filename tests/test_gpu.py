@@ -761,55 +761,6 @@ def test_trace_schedule_knobs_same_film(mcpt_mod, scene_c2, knob):
     pt.close()
 
 
-@pytest.mark.parametrize("slots,tile,compact", [(1, 256, False), (4, 64, False), (3, 64, True)])
-def test_shard_bands_same_film(mcpt_mod, scene_c2, slots, tile, compact):
-    """Image-band queue shards (MCPT_SHARD_BANDS=1, kernels.hpp shade_shard) only move k_shade's
-    blocks between queue shards and so between k_trace's partitions: the film, sample counts and ray
-    counts are bit-identical to the interleaved shards' -- full and compact path state, ragged 64-px
-    tiles, several path slots -- and the one-tile step (a launch over part of the tile set, which
-    keeps the interleaved shards the queues were sized for) gives the same film as well."""
-    from mcpt import parallel
-    rc = mcpt_mod.CONFIGS[2]
-    W, H = 320, 180
-    cam = mcpt_mod.config_camera(rc, W, H)
-    tiles = parallel.tiles_for_rank(0, 2, W, H, tile) if compact else None
-
-    def run(bands, stepped=False):
-        old = os.environ.get("MCPT_SHARD_BANDS")
-        os.environ["MCPT_SHARD_BANDS"] = bands
-        try:
-            pt = make_pt(mcpt_mod, scene_c2[0], cam, W, H, 3, rc.max_depth, tile=tile)
-        finally:
-            if old is None:
-                os.environ.pop("MCPT_SHARD_BANDS", None)
-            else:
-                os.environ["MCPT_SHARD_BANDS"] = old
-        if compact:
-            pt.set_compact_paths(True)
-            pt.set_path_slots(1)
-            pt.resize(W, H, tile, tile)
-            pt.set_tiles(tiles)
-        pt.set_path_slots(slots)
-        if stepped:  # the reference's orchestration: one tile per call until the film is done
-            for _ in range(200):
-                pt.step(0, 0)
-            st = None
-        else:
-            st = pt.render()
-        L, s = pt.film()
-        pt.close()
-        return st, L, s
-
-    st0, L0, s0 = run("0")
-    st1, L1, s1 = run("1")
-    assert np.array_equal(s1, s0) and st1.rays == st0.rays
-    assert np.array_equal(L1.view(np.uint32), L0.view(np.uint32))
-    if not compact:
-        _, L2, s2 = run("0", stepped=True)
-        _, L3, s3 = run("1", stepped=True)
-        assert np.array_equal(s3, s2) and np.array_equal(L3.view(np.uint32), L2.view(np.uint32))
-
-
 def test_node_layouts_same_hits(mcpt_mod, oracle, scene_c2):
     """Pair-node numberings 0 (depth-first), 1 (sibling pairs, depth-first), 2 (breadth-first) and
     3 (line pairs with pad nodes) are layout only: bit-identical hits and visibility, also through
