@@ -2,8 +2,11 @@
 states tools/make_golden.py feeds to the oracle's stage restatements (or_stage_logic /
 or_stage_material) and tests/test_gpu.py::test_stage_golden_vectors feeds to mcpt_stage_run.
 
-Scene: sphere.glb + HDR_029 (BASELINE config 1) plus one directional light, so the light choice
-picks the env light (HRDI sampling) or the delta light about half the time each."""
+Scenes (SCENES: fixture suffix -> BASELINE config): sphere.glb + HDR_029 (config 1), and config 2's
+proxy (Cornell-style room, spheres of several materials, night_free_Env.hdr), each plus one
+directional light, so the light choice picks the env light (HRDI sampling) or the delta light
+about half the time each.  Config 2's walls give axis-aligned normals (Appendix A's gram_schmidt
+quirk) and its rays start inside the room."""
 import numpy as np
 
 SPP, DEPTH, RR = 16, 5, 3
@@ -11,28 +14,38 @@ FILM = (17, 17)  # 289 paths, 256 processed (the last row / column never are: :1
 N_MAT = 256
 
 
-def stage_scene(mcpt):
+SCENES = {"c1dir": 1, "c2": 2}
+
+
+def stage_scene(mcpt, cid=1):
     s = mcpt.Scene()
-    s.make_proxy(1)
+    s.make_proxy(cid)
     s.add_dir_light((-0.3, -1.0, -0.2), (1.0, 0.9, 0.8), 2.0)
     s.build(**mcpt.DEFAULT_BVH)
     return s
 
 
-def stage_camera(mcpt):
-    return mcpt.config_camera(mcpt.CONFIGS[1], *FILM)
+def stage_camera(mcpt, cid=1):
+    return mcpt.config_camera(mcpt.CONFIGS[cid], *FILM)
 
 
-def material_state(a, trace_closest):
-    """256 continuing paths: rays from a shell aimed into the unit sphere, at their closest hits
-    (hit_tri = index into the scene arrays), len 1..5, random sample indices and throughputs."""
+def material_state(a, trace_closest, cid=1):
+    """256 continuing paths at their closest hits (hit_tri = index into the scene arrays), len 1..5,
+    random sample indices and throughputs.  Config 1: rays from a shell aimed into the unit sphere;
+    config 2: rays from points inside the room (0.8 of its box) in random directions."""
     rng = np.random.default_rng(2026)
     ro_l, rd_l, tri_l = [], [], []
     inv = np.argsort(a["tri_id"])  # scene triangle id -> array index
+    mn, mx = np.asarray(a["bmin"][0], np.float64), np.asarray(a["bmax"][0], np.float64)
     while sum(len(t) for t in tri_l) < N_MAT:
-        o = rng.normal(size=(512, 3))
-        o = (o / np.linalg.norm(o, axis=1, keepdims=True) * rng.uniform(1.5, 4.0, (512, 1))).astype(np.float32)
-        t = rng.uniform(-0.7, 0.7, (512, 3))
+        if cid == 1:
+            o = rng.normal(size=(512, 3))
+            o = (o / np.linalg.norm(o, axis=1, keepdims=True) * rng.uniform(1.5, 4.0, (512, 1))).astype(np.float32)
+            t = rng.uniform(-0.7, 0.7, (512, 3))
+        else:
+            c, h = (mn + mx) / 2, (mx - mn) / 2 * 0.8
+            o = (c + h * rng.uniform(-1.0, 1.0, (512, 3))).astype(np.float32)
+            t = o + rng.normal(size=(512, 3))
         d = t - o
         d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
         _, _, tri = trace_closest(a, o, d)

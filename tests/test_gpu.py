@@ -1130,24 +1130,27 @@ def _same(a, b):
     return bool(np.array_equal(a, b))
 
 
+@pytest.mark.parametrize("scene", ["c1dir", "c2"])
 @pytest.mark.parametrize("stage", ["logic", "generate", "material"])
-def test_stage_golden_vectors(mcpt_mod, oracle, stage):
+def test_stage_golden_vectors(mcpt_mod, oracle, stage, scene):
     """Per-stage golden vectors: mcpt_stage_run runs the product's
     k_shade (LOGIC / GENERATE: wf_logic + wf_generate, wavefront_kernels.cu:90-251) or k_material
     (MATERIAL: light choice + wf_mat_mix, :207-213, 295-375) on the fixture's path state; every
-    output field equals the oracle's stage restatement (tools/make_golden.py) bit for bit.  Rays
-    the kernels resolve in place because they cannot hit the scene are checked against the
-    oracle's traversal instead of a queue entry."""
+    output field equals the oracle's stage restatement (tools/make_golden.py) bit for bit, on two
+    fixture scenes (config 1's sphere, config 2's room; stage_fixtures.SCENES).  Rays the kernels
+    resolve in place because they cannot hit the scene are checked against the oracle's traversal
+    instead of a queue entry."""
     import stage_fixtures as sf
 
-    g = np.load(os.path.join(GOLDEN, f"stage_{stage}_c1dir.npz"))
+    cid = sf.SCENES[scene]
+    g = np.load(os.path.join(GOLDEN, f"stage_{stage}_{scene}.npz"))
     inp = {k[3:]: g[k] for k in g.files if k.startswith("in_")}
     ref = {k[4:]: g[k] for k in g.files if k.startswith("out_")}
-    s = sf.stage_scene(mcpt_mod)
+    s = sf.stage_scene(mcpt_mod, cid)
     a = s.arrays()
     pt = mcpt_mod.PathTracer(0, mcpt_mod.default_config(spp=sf.SPP, max_depth=sf.DEPTH, rr_depth=sf.RR))
     pt.upload_scene(s)
-    pt.set_camera(sf.stage_camera(mcpt_mod))
+    pt.set_camera(sf.stage_camera(mcpt_mod, cid))
     got = pt.stage(stage, inp, film=sf.FILM if stage != "material" else None)
     pt.close()
     _check_stage(stage, got, ref, a, oracle)

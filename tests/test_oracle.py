@@ -434,21 +434,23 @@ def test_literal_leaf_rule_deviation(mcpt_mod, oracle, scene_c1, scene_cube, sce
         assert n <= 0.01 * tot, (name, n, tot)
 
 
+@pytest.mark.parametrize("scene", ["c1dir", "c2"])
 @pytest.mark.parametrize("stage", ["logic", "generate", "material"])
-def test_stage_golden_vectors_oracle(mcpt_mod, oracle, stage):
+def test_stage_golden_vectors_oracle(mcpt_mod, oracle, stage, scene):
     """The oracle's stage restatements (or_stage_logic / or_stage_material, sharing logic_core,
     mis_terms, pick_light and mat_mix_core with the full render) reproduce the committed per-stage
     golden vectors bit for bit (regression pin; the GPU side is tests/test_gpu.py)."""
     import stage_fixtures as sf
 
-    g = np.load(os.path.join(GOLDEN, f"stage_{stage}_c1dir.npz"))
+    cid = sf.SCENES[scene]
+    g = np.load(os.path.join(GOLDEN, f"stage_{stage}_{scene}.npz"))
     inp = {k[3:]: g[k] for k in g.files if k.startswith("in_")}
-    a = sf.stage_scene(mcpt_mod).arrays()
+    a = sf.stage_scene(mcpt_mod, cid).arrays()
     kw = dict(max_depth=sf.DEPTH, rr_depth=sf.RR)
     if stage == "material":
         out = oracle.stage_material(a, inp, **kw)
     else:
-        out = oracle.stage_logic(a, sf.stage_camera(mcpt_mod), *sf.FILM, inp, sf.SPP, **kw)
+        out = oracle.stage_logic(a, sf.stage_camera(mcpt_mod, cid), *sf.FILM, inp, sf.SPP, **kw)
     for k, v in out.items():
         ref = g["out_" + k]
         assert np.array_equal(np.asarray(v).view(np.uint8), ref.view(np.uint8)), k

@@ -59,28 +59,37 @@ def main():
         pt, nm, tri = op.trace_closest(arr, ro, rd)  # tri: triangle ids (scene order, any BVH)
         vis = op.trace_any(arr, ro, rd)
         np.savez_compressed(os.path.join(OUT, f"trace_{name}_256.npz"), ro=ro, rd=rd, pos_t=pt, nrm_mat=nm, tri=tri, vis=vis)
-    stage_vectors()
+    for suffix in sf.SCENES:
+        stage_vectors(suffix)
     print("golden fixtures written to", OUT)
 
 
-def stage_vectors():
-    """Per-stage golden vectors: inputs from tests/stage_fixtures.py,
-    outputs from the oracle's stage restatements, diffed field by field against mcpt_stage_run
-    by tests/test_gpu.py::test_stage_golden_vectors."""
-    s = sf.stage_scene(mcpt)
+def stage_vectors(suffix):
+    """Per-stage golden vectors of one fixture scene
+    (stage_fixtures.SCENES; round 6 added config 2's proxy): inputs from tests/stage_fixtures.py,
+    outputs from the oracle's stage restatements, diffed field by field against mcpt_stage_run by
+    tests/test_gpu.py::test_stage_golden_vectors.  `python tools/make_golden.py --stages c2` writes
+    one scene's vectors only."""
+    cid = sf.SCENES[suffix]
+    s = sf.stage_scene(mcpt, cid)
     a = s.arrays()
-    cam = sf.stage_camera(mcpt)
+    cam = sf.stage_camera(mcpt, cid)
     W, H = sf.FILM
     kw = dict(max_depth=sf.DEPTH, rr_depth=sf.RR)
     for name, st in (("logic", sf.logic_state(len(a["mat"]))), ("generate", sf.logic_state(len(a["mat"]), True))):
         out = op.stage_logic(a, cam, W, H, st, sf.SPP, **kw)
-        np.savez_compressed(os.path.join(OUT, f"stage_{name}_c1dir.npz"), **{"in_" + k: v for k, v in st.items()},
+        np.savez_compressed(os.path.join(OUT, f"stage_{name}_{suffix}.npz"), **{"in_" + k: v for k, v in st.items()},
                             **{"out_" + k: v for k, v in out.items()})
-    st = sf.material_state(a, op.trace_closest)
+    st = sf.material_state(a, op.trace_closest, cid)
     out = op.stage_material(a, st, **kw)
-    np.savez_compressed(os.path.join(OUT, "stage_material_c1dir.npz"), **{"in_" + k: v for k, v in st.items()},
+    np.savez_compressed(os.path.join(OUT, f"stage_material_{suffix}.npz"), **{"in_" + k: v for k, v in st.items()},
                         **{"out_" + k: v for k, v in out.items()})
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[1] == "--stages":
+        os.makedirs(OUT, exist_ok=True)
+        for suffix in sys.argv[2:]:
+            stage_vectors(suffix)
+    else:
+        main()
