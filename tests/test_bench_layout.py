@@ -4,7 +4,8 @@ bench.py renders each config's full frame with BENCH_SLOTS path slots per pixel 
 in flight per pixel, each slot accumulating its own samples).  Here the GPU renders exactly that
 layout -- full resolution, the bench's slot count, the config's depth -- to high sample counts
 (config 1 whole, 16 spp at its 16 slots; 256 spp for configs 2 and 3, as benched; 16 spp for
-configs 4 and 5, whose full 1024 / 4096 spp would take minutes), and a band of rows re-executed by the oracle (one path per pixel, the
+configs 4 and 5 over the whole frame, and their full 1024 / 4096 spp on ten tiles spread over the
+frame, test_full_spp_tiles_against_oracle), and a band of rows re-executed by the oracle (one path per pixel, the
 reference's layout: wavefront_kernels.cu:90-375) must agree: sample counts exactly, radiance within
 the north star's 1e-4 relative (the slots only change the film's summation order).  High sample
 indices, Russian roulette at depth and the slots' interleaved sample chains are all exercised.
@@ -92,14 +93,16 @@ def test_bench_layout_config2_scattered_rows(mcpt_mod, oracle, scene_c2):
         assert ok, f"row {r}: {nbad} radiance values differ"
 
 
-@pytest.mark.parametrize("cid,tiles", [(4, [(7, 4), (3, 2)]), (5, [(8, 8)])], ids=["config4", "config5"])
+@pytest.mark.parametrize("cid,tiles", [(4, [(7, 4), (3, 2), (0, 0), (14, 8), (10, 6), (5, 7)]),
+                                       (5, [(8, 8), (0, 0), (15, 15), (4, 11)])], ids=["config4", "config5"])
 def test_full_spp_tiles_against_oracle(mcpt_mod, oracle, cid, tiles):
     """Configs 4 and 5 at their full sample counts -- 1024 spp depth 8, 4096 spp depth 12 -- at the
     bench's path slots (24: slot k renders samples k, k + 24, ..., 42-43 / 170-171 of them, sample
     indices up to 4095 keyed into the RNG, wavefront_kernels.cu:124,219-222) on whole 256 x 256
-    tiles (mcpt_set_tiles), one
-    row of each tile against the oracle (the one tile alone: part=(tx + ty, a modulus larger than
-    any tx + ty))."""
+    tiles (mcpt_set_tiles) spread over the frame -- corners, the centre, sky and geometry, the
+    bottom-right tiles with the never-rendered last row and column (:110) and config 4's partial
+    bottom tile row -- two rows of each tile against the oracle (the one tile alone: part=(tx + ty,
+    a modulus larger than any tx + ty))."""
     rc = mcpt_mod.CONFIGS[cid]
     scene = mcpt_mod.build_config_scene(cid)
     arrays = scene.arrays()
@@ -116,17 +119,25 @@ def test_full_spp_tiles_against_oracle(mcpt_mod, oracle, cid, tiles):
     Ld, smp = pt.film()
     pt.close()
     big = rc.width // 256 + rc.height // 256 + 2
+    W, H = rc.width, rc.height
+    lit = 0
     for tx, ty in tiles:
-        assert np.all(smp[ty * 256:(ty + 1) * 256, tx * 256:(tx + 1) * 256] == rc.spp)
-        r = ty * 256 + 128
-        t0 = time.perf_counter()
-        rL, rs, cnt = oracle.render(arrays, cam, rc.width, rc.height, rc.spp, rc.max_depth, rows=(r, r + 1),
-                                    part=(tx + ty, big))
-        t_cpu = time.perf_counter() - t0
-        cols = slice(tx * 256, (tx + 1) * 256)
-        assert np.array_equal(smp[r, cols], rs[r, cols]) and rs[r].sum() == 256 * rc.spp
-        ok, nbad = film_close(Ld[r, cols], rL[r, cols])
-        assert ok, f"config {cid} tile {(tx, ty)} row {r}: {nbad} radiance values differ"
-        assert Ld[r, cols].max() > 0
-        print(f"config {cid} tile {(tx, ty)} row {r}: {rc.spp} spp, {cnt['extend_rays']} oracle extension rays "
-              f"({t_cpu:.1f} s); GPU tiles {t_gpu:.2f} s, {st.rays} rays")
+        y0, y1, x0, x1 = ty * 256, min((ty + 1) * 256, H), tx * 256, min((tx + 1) * 256, W)
+        want = np.full((y1 - y0, x1 - x0), rc.spp, np.uint32)
+        if y1 == H:
+            want[-1] = 0  # the last row and column are never rendered (wavefront_kernels.cu:110)
+        if x1 == W:
+            want[:, -1] = 0
+        assert np.array_equal(smp[y0:y1, x0:x1], want)
+        for r in (y0 + 40, min(y0 + 200, H - 2)):
+            t0 = time.perf_counter()
+            rL, rs, cnt = oracle.render(arrays, cam, W, H, rc.spp, rc.max_depth, rows=(r, r + 1), part=(tx + ty, big))
+            t_cpu = time.perf_counter() - t0
+            cols = slice(x0, x1)
+            assert np.array_equal(smp[r, cols], rs[r, cols]) and rs[r].sum() == want[r - y0].sum()
+            ok, nbad = film_close(Ld[r, cols], rL[r, cols])
+            assert ok, f"config {cid} tile {(tx, ty)} row {r}: {nbad} radiance values differ"
+            lit += int(Ld[r, cols].max() > 0)
+            print(f"config {cid} tile {(tx, ty)} row {r}: {rc.spp} spp, {cnt['extend_rays']} oracle extension rays "
+                  f"({t_cpu:.1f} s); GPU tiles {t_gpu:.2f} s, {st.rays} rays")
+    assert lit >= len(tiles)  # most checked rows carry light
