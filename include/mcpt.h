@@ -275,8 +275,10 @@ float mcpt_debug_last_build_ms(const mcpt_ctx *ctx);  /* device time of the last
 float mcpt_debug_last_env_build_ms(const mcpt_ctx *ctx);
 int mcpt_debug_env_tables(mcpt_ctx *ctx, float *marginal_y, float *conds_y, float *pdf, int32_t *flags);
 /* pair-node numbering of the last uploaded tree: 0 depth-first, 1 depth-first by sibling pairs,
- * 2 breadth-first (default 2 for trees of <= 2 MiB of nodes, else 0; MCPT_SIBLING_LAYOUT=0/1/2
- * at upload forces one; inputs that are not a tree -- a shared child -- always get 0). */
+ * 2 breadth-first, 3 line pairs (a node and its larger-area child per 128-B line, pad nodes where a
+ * node has no interior child; opt-in) (default 2 for trees of <= 2 MiB of nodes, else 0;
+ * MCPT_SIBLING_LAYOUT=0/1/2/3 at upload forces one; inputs that are not a tree -- a shared child --
+ * always get 0). */
 int mcpt_debug_node_layout(const mcpt_ctx *ctx);
 /* any-hit occluder cache: any-hit rays resolved by it since the film was
  * last cleared (counted in shadow_rays / vis_rays as traced rays; they skip the traversal), and
@@ -290,9 +292,16 @@ int mcpt_debug_ray_counts(const mcpt_ctx *ctx, uint64_t *out);
  * since the last film clear or reset (reset = 1 starts a new count after reading): out12[0] loop
  * trips, [1] refills, [2] lanes refilled, [3] node-phase wave iterations, [4] triangle phases,
  * [5] lanes testing a triangle in them, [6] / [7] / [8] lanes with node work / a parked leaf / no
- * ray at a trip's start; [9..11] 0.  With the node steps of mcpt_stage_stats they split the lane
- * utilisation by phase.  Returns the number of words filled (9), 0 when none were recorded. */
+ * ray at a trip's start, [9] trips in which a lane finished its ray, [10] node-phase iterations in
+ * which a lane popped its stack; [11] 0.  With the node steps of mcpt_stage_stats they split the
+ * lane utilisation by phase, and with the kernel's ISA sections its VALU (tools/trace_attrib.py).
+ * Returns the number of words filled (11), 0 when none were recorded. */
 int mcpt_debug_trace_profile(mcpt_ctx *ctx, uint64_t *out12, int reset);
+/* k_shade's per-section wave entries and active lanes, summed over the
+ * launches since the last reset, in a build with -DMCPT_DIAG_SHADE: out[2k] entries and out[2k+1]
+ * lanes of section k (waves, valid paths, logic, MIS terms, generate, continuing, background), up to
+ * n words.  Returns the words available (14); the product build fills zeros and returns 0. */
+int mcpt_debug_shade_sections(mcpt_ctx *ctx, uint64_t *out, int n, int reset);
 /* diagnostics: the kernels' shared-denominator division (mcpt::quot3, mcpt_core.hpp) on the
  * device for n host pairs: out[i] = a[i] / b[i] as the kernels compute it (must equal IEEE fp32). */
 int mcpt_debug_quot(mcpt_ctx *ctx, const float *a, const float *b, uint32_t n, float *out);

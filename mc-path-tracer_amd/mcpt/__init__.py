@@ -151,6 +151,7 @@ ABI = {
     "mcpt_image_write_png": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]),
     "mcpt_image_write_pfm": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_float)]),
     "mcpt_debug_trace_profile": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
+    "mcpt_debug_shade_sections": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int, C.c_int]),
     "mcpt_scene_build_ex": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mcpt_debug_quot": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "mcpt_debug_hbm_copy": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
