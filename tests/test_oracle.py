@@ -467,3 +467,38 @@ def test_udiv_small_exact():
         q = (nf * r).astype(np.uint32)  # v_mul_f32 (RN) then v_cvt_u32_f32 (toward zero)
         q = q + ((n - q * np.uint32(d)) >= d).astype(np.uint32)
         assert np.array_equal(q, n // np.uint32(d)), d
+
+
+def test_traversal_study_model_consistency(oracle, scene_c2):
+    """The round-6 traversal study (oracle/trav_model.c or_model_study / or_lru_sim, tools/trav_study.py,
+    DESIGN.md section 4) records what the model's traversal does without changing it: its hits and
+    visibility equal or_model_trace's, every pair step fetches one line, the origin-box steps are a
+    subset of the steps, and the LRU model is sane (a cache that holds every line misses exactly
+    once per distinct line; a one-line cache misses on every change of line)."""
+    import numpy as np
+    _, a = scene_c2
+    rng = np.random.default_rng(3)
+    n = 2000
+    ro = rng.uniform(-0.9, 0.9, (n, 3)).astype(np.float32)
+    rd = rng.normal(size=(n, 3)).astype(np.float32)
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+    m = oracle.model_margins(a)
+    tri, t, vis, _ = oracle.model_trace(a, ro, rd, 2, m)
+    nn = len(a["nprims"])
+    pair_line = (np.arange(nn) >> 1).astype(np.int32)  # any numbering will do here
+    for kind in (0, 1):
+        st = oracle.model_study(a, ro, rd, 2, kind, pair_line, nn, margins=m)
+        hit = st["hit"].astype(bool)
+        assert np.array_equal(hit, (tri >= 0) if kind == 0 else (vis == 0))
+        assert np.all(st["origin_steps"] <= st["steps"]) and st["steps"].sum() > n
+        interior_lines = (np.diff(st["off"]) >= st["steps"]).all()
+        assert interior_lines
+        lines, off = st["lines"], st["off"]
+        distinct = len(np.unique(lines))
+        assert oracle.lru_sim(lines, off, 1, 1 << 16, 16) == distinct  # everything fits: cold misses only
+        one = oracle.lru_sim(lines, off, 1, 1, 1)
+        changes = sum(1 + int((np.diff(lines[off[i]:off[i + 1]]) != 0).sum()) if off[i + 1] > off[i] else 0
+                      for i in range(n))
+        # rays back to back through one line: a miss on every change, the first of each ray
+        # only when it differs from the previous ray's last line
+        assert changes - n <= one <= changes
