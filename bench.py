@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import argparse
 import glob
+import re
 import json
 import os
 import socket
@@ -198,8 +199,9 @@ def pmc_summary(config, slots, kind="pmc", spp=None):
     for the others) and whether it was measured on this code (source hash) and this workload
     (config, path slots, step, spp: a launch's traffic depends on the spp through the path mix)."""
     pre = f"{kind}_r" if config == 2 else f"{kind}_c{config}_r"
+    # <kind>_rNN.json only: variant summaries (<kind>_rNNoccoff.json: a knob set) are not the product's
     files = sorted(f for f in glob.glob(os.path.join(REPO, "profiles", f"{pre}*.json"))
-                   if os.path.basename(f)[len(pre):][:1].isdigit())
+                   if re.fullmatch(r"\d+\.json", os.path.basename(f)[len(pre):]))
     if not files:
         return None, f"no {kind} summary in profiles/"
     try:
@@ -216,6 +218,9 @@ def pmc_summary(config, slots, kind="pmc", spp=None):
         why.append(f"taken with {stamp.get('step', 'iteration')} steps")
     if spp is not None and "spp" in stamp and stamp["spp"] != spp:
         why.append(f"taken at {stamp['spp']} spp")
+    judged = lambda k: {x: v for x, v in k.items() if x not in NEUTRAL_KNOBS}  # noqa: E731
+    if "knobs" in stamp and judged(stamp["knobs"]) != judged(knobs()):
+        why.append(f"taken with knobs {judged(stamp['knobs'])}")
     return d, ("; ".join(why) or None)
 
 

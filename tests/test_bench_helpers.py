@@ -58,6 +58,17 @@ def test_pmc_summary_stale_detection(tmp_path, monkeypatch):
     assert bench.pmc_summary(5, 24, spp=64)[1] is None
     assert "taken at 64 spp" in bench.pmc_summary(5, 24, spp=4096)[1]
     assert bench.pmc_summary(3, 32, spp=999)[1] is None
+    # a variant pass (a knob set: pmc_r13occoff.json) is never taken for the product's line, and a
+    # summary stamped with knobs other than the run's is stale (neutral knobs aside)
+    (prof / "pmc_r13.json").write_text(json.dumps({"stamp": dict(_stamp(h="def"), knobs={}), "kernels": kern}))
+    (prof / "pmc_r13occoff.json").write_text(json.dumps({"stamp": dict(_stamp(h="def"), knobs={"MCPT_OCC_G": "0"}),
+                                                         "kernels": {}}))
+    d, why = bench.pmc_summary(2, 3)
+    assert why is None and d["kernels"] == kern
+    monkeypatch.setenv("MCPT_DIST_TIMEOUT_S", "30")  # neutral
+    assert bench.pmc_summary(2, 3)[1] is None
+    monkeypatch.setenv("MCPT_OCC_G", "0")
+    assert "taken with knobs {}" in bench.pmc_summary(2, 3)[1]
 
 
 class _St:

@@ -54,7 +54,9 @@ import bench  # noqa: E402  (source_hash only)
 cfg = int(os.environ.get("PMC_CONFIG", "2"))
 stamp = {"source_hash": bench.source_hash(), "config": cfg,
          "slots": int(os.environ.get("PMC_SLOTS", str(bench.BENCH_SLOTS[cfg]))), "step": bench.STEP,
-         "spp": bench.stamp_spp(cfg, os.environ.get("PMC_ARGS", ""))}
+         "spp": bench.stamp_spp(cfg, os.environ.get("PMC_ARGS", "")),
+         # the MCPT_* knobs the profiled runs had (set them here too when summarising elsewhere)
+         "knobs": bench.knobs()}
 out = {"round": tag, "stamp": stamp,
        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on "
        f"'python3 bench.py {os.environ.get('PMC_ARGS', '--no-cpu-baseline')}'; durations from --kernel-trace --stats",

@@ -49,7 +49,8 @@ for k, m in acc.items():
 cfg = int(os.environ.get("PMC_CONFIG", "2"))
 out = {"round": tag, "stamp": {"source_hash": bench.source_hash(), "config": cfg,
                                "slots": int(os.environ.get("PMC_SLOTS", str(bench.BENCH_SLOTS[cfg]))),
-                               "step": bench.STEP, "spp": bench.stamp_spp(cfg, os.environ.get("PMC_ARGS", ""))},
+                               "step": bench.STEP, "spp": bench.stamp_spp(cfg, os.environ.get("PMC_ARGS", "")),
+                               "knobs": bench.knobs()},
        "source": f"tools/gpu/run.sh pmc ({label}): rocprofv3 --pmc passes (one counter group each) over "
                  f"'python3 {os.environ.get('PROG', 'bench.py')}'",
        "formulas": __doc__.split("\n\n")[1].strip(), "kernels": out_k}
