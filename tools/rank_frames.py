@@ -50,9 +50,12 @@ def main():
         t0 = time.perf_counter()
         st = pt.render()
         dt = time.perf_counter() - t0
+        rc_ = pt.ray_counts()  # traversed vs resolved (occluder cache) since the clear
         print(json.dumps({"frame": f, "warmup": f == 0, "wall_ms": round(dt * 1e3, 3), "iterations": st.iterations,
                           "ms_shade": round(st.ms_shade, 3), "ms_trace": round(st.ms_extend, 3), "rays": st.rays,
-                          "slots": slots, "tiles": len(tiles)}), flush=True)
+                          "slots": slots, "tiles": len(tiles), "ray_counts": rc_,
+                          "occ_resolved_frac": round(rc_["any_hit_occluder_cache"] / max(1, rc_["any_hit"]), 4),
+                          "knobs": {k: v for k, v in os.environ.items() if k.startswith("MCPT_")}}), flush=True)
     pt.close()
 
 
