@@ -1001,7 +1001,7 @@ __global__ __launch_bounds__(kBlock) MCPT_MAT_ATTR void k_material(ShadeArgs a_k
     const uint32_t n = sc_ctr[C_MAT];
     const int lane = threadIdx.x & 63;
     uint32_t n_ext = 0, n_any = 0, n_vis = 0, n_occ = 0, occ_try = 0;
-    const bool occ_on = a.scene.occ && a.scene.occ_gate[0] == 0;  // see DevScene::occ_gate
+    const bool occ_on = a.scene.occ && a.scene.occ_gate[0] == 0 && a.scene.occ_gate[2] != 0;  // see DevScene::occ_gate
     // Any-hit rays are staged here (light ray o/d, BRDF visibility ray o/d) and stored after
     // the block push at their queue positions: the block's rays of one kind land contiguously,
     // so k_trace reads them densely and without the queue-entry hop (the pid-indexed layout
@@ -1941,6 +1941,10 @@ __global__ void k_tonemap(TonemapArgs a) {  // draw_to_surface (wavefront_kernel
     a.out[i] = o;
 }
 
+// the occluder gate's first backoff (iterations without lookups after the first that did not pay)
+#ifndef MCPT_OCC_BACKOFF0
+#define MCPT_OCC_BACKOFF0 3
+#endif
 __global__ void k_accumulate(CounterBlock* c, uint32_t nparts, uint32_t* occ_gate) {  // fold per-iteration shard counts into 64-bit totals
     if (c->idle) return;  // nothing ran since the iteration that set it; every counter is zero
     const int t = threadIdx.x;  // one lane per shard
@@ -1994,9 +1998,13 @@ __global__ void k_accumulate(CounterBlock* c, uint32_t nparts, uint32_t* occ_gat
         if (occ_gate) {
             if (occ_gate[0]) {
                 occ_gate[0]--;
+            } else if (!occ_gate[2]) {
+                // the table is empty until the first iteration that traced any-hit rays has
+                // recorded their occluders: k_material starts its lookups after it
+                if (v[C_ANY]) occ_gate[2] = 1;
             } else if (ot >= 4096u) {
                 if ((unsigned long long)oc * kOccMinRate < ot) {
-                    occ_gate[1] = occ_gate[1] ? min(2u * occ_gate[1] + 1u, 255u) : 3u;
+                    occ_gate[1] = occ_gate[1] ? min(2u * occ_gate[1] + 1u, 255u) : (uint32_t)MCPT_OCC_BACKOFF0;
                     occ_gate[0] = occ_gate[1];
                 } else {
                     occ_gate[1] = 0;

@@ -94,11 +94,15 @@ struct DevScene {
     // a hit there is one the traversal would find too, so the ray is resolved as occluded.
     // occ == nullptr: off.
     uint32_t* occ;
-    // The lookup gate, two words kept with the table (both reset at upload and with the film): [0] skip: k_material skips the lookups while nonzero; k_accumulate
+    // The lookup gate, kOccGateWords words kept with the table (all reset at upload and with the film): [0] skip: k_material skips the lookups while nonzero; k_accumulate
     // sets it to [1] after an iteration whose lookups resolved under 1 in kOccMinRate of the rays
     // tested and counts it down one per iteration; k_trace records occluders only while it is <= 1,
     // so the next lookups meet a fresh table.  [1] backoff: 3, 7, 15, ... 255 after consecutive
-    // failed lookup iterations, 0 while they pay.
+    // failed lookup iterations, 0 while they pay.  [2] warm: set by the first iteration that traced
+    // any-hit rays (and so recorded occluders into the table the film clear emptied); k_material
+    // looks nothing up before it.  (Round 6: the lookups against the empty table used to be judged,
+    // which closed the gate for the frame's biggest iterations, 2-4 -- at N = 8 most of a rank's
+    // frame.)
     uint32_t* occ_gate;
     const float4* occ_rec;
     uint32_t ntri;
@@ -114,6 +118,7 @@ struct DevScene {
 constexpr uint32_t kOccEmpty = 0xffffffffu;
 constexpr uint32_t kOccWays = 2;      // entries per cell: k_trace writes way tri mod 2, k_material tests both
                                       // (1 way resolved 52 % of config 2's any-hit rays, 2 ways 64 %)
+constexpr uint32_t kOccGateWords = 3;  // DevScene::occ_gate
 constexpr uint32_t kOccMinRate = 10;  // lookups pay when >= 1 in kOccMinRate resolves a ray (see occ_skip)
 __host__ __device__ constexpr size_t occ_entries(int g, int b) { return (size_t)g * g * g * 6 * b * b * kOccWays; }
 

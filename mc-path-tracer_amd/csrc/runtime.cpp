@@ -41,7 +41,7 @@ struct mcpt_ctx {
     bool has_scene = false;
     bool has_scene_before = false;  // set at the start of a re-upload
     int32_t ntri = 0;               // triangles of the uploaded scene
-    size_t occ_entries_n = 0;       // occluder-cache table entries (DevScene::occ; + 2 gate words)
+    size_t occ_entries_n = 0;       // occluder-cache table entries (DevScene::occ; + kOccGateWords gate words)
     int pair_depth = 0;
     bool cull_ok = true, occ_nest_ok = true;  // last upload: boxes contain their triangles / nest (scene_upload)
     // traversal work counters (mcpt_set_work_counters): k_trace's counting instantiation, whose six
@@ -788,12 +788,12 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             uint32_t* occ;
             const size_t ne = occ_entries(G, B);
             if ((rc = dalloc(c, c->scene_bufs, &lbx, kOccRecF4 * (size_t)d->ntri)) ||
-                (rc = dalloc(c, c->scene_bufs, &occ, ne + 2)))
+                (rc = dalloc(c, c->scene_bufs, &occ, ne + kOccGateWords)))
                 return rc;
             // NaN boxes (all-ones bytes) for a record no leaf holds: occ_test's slab then fails
             HIPCHK(c, hipMemsetAsync(lbx, 0xff, kOccRecF4 * (size_t)d->ntri * sizeof(float4), c->stream));
             HIPCHK(c, hipMemsetAsync(occ, 0xff, ne * sizeof(uint32_t), c->stream));
-            HIPCHK(c, hipMemsetAsync(occ + ne, 0, 2 * sizeof(uint32_t), c->stream));  // the lookup gate: on
+            HIPCHK(c, hipMemsetAsync(occ + ne, 0, kOccGateWords * sizeof(uint32_t), c->stream));  // the lookup gate: on
             launch_occ_records(s, nnodes, lbx, c->stream);
             HIPCHK(c, hipGetLastError());
             HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -931,7 +931,7 @@ int mcpt_film_clear(mcpt_ctx* c) {
     // tests first; the 96 MB fill takes ~0.02 ms.)
     if (c->scene.occ) {
         HIPCHK(c, hipMemsetAsync(c->scene.occ, 0xff, c->occ_entries_n * sizeof(uint32_t), c->stream));
-        HIPCHK(c, hipMemsetAsync(c->scene.occ_gate, 0, 2 * sizeof(uint32_t), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->scene.occ_gate, 0, kOccGateWords * sizeof(uint32_t), c->stream));
     }
     c->film_stale = false;
     c->unpacked.clear();
