@@ -1941,9 +1941,11 @@ __global__ void k_tonemap(TonemapArgs a) {  // draw_to_surface (wavefront_kernel
     a.out[i] = o;
 }
 
-// the occluder gate's first backoff (iterations without lookups after the first that did not pay)
+// the occluder gate's first backoff (iterations without lookups after the first that did not pay):
+// 3 / 7 / 15 measured interleaved (profiles/ab_r06_occ_gate.txt): config 3 247.1 / 245.2 / 244.6 ms,
+// config 5 (64 spp) 729.9 / - / 727.6 ms, config 2 (whose lookups pay) unchanged
 #ifndef MCPT_OCC_BACKOFF0
-#define MCPT_OCC_BACKOFF0 3
+#define MCPT_OCC_BACKOFF0 15
 #endif
 __global__ void k_accumulate(CounterBlock* c, uint32_t nparts, uint32_t* occ_gate) {  // fold per-iteration shard counts into 64-bit totals
     if (c->idle) return;  // nothing ran since the iteration that set it; every counter is zero

@@ -97,7 +97,7 @@ struct DevScene {
     // The lookup gate, kOccGateWords words kept with the table (all reset at upload and with the film): [0] skip: k_material skips the lookups while nonzero; k_accumulate
     // sets it to [1] after an iteration whose lookups resolved under 1 in kOccMinRate of the rays
     // tested and counts it down one per iteration; k_trace records occluders only while it is <= 1,
-    // so the next lookups meet a fresh table.  [1] backoff: 3, 7, 15, ... 255 after consecutive
+    // so the next lookups meet a fresh table.  [1] backoff: 15, 31, 63, ... 255 after consecutive
     // failed lookup iterations, 0 while they pay.  [2] warm: set by the first iteration that traced
     // any-hit rays (and so recorded occluders into the table the film clear emptied); k_material
     // looks nothing up before it.  (Round 6: the lookups against the empty table used to be judged,
