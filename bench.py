@@ -85,6 +85,7 @@ NON_PRODUCT_KNOBS = {
     "MCPT_ENV_GUIDES": "env CDF search guides switched",
     "MCPT_OCC_G": "occluder-table origin grid",
     "MCPT_OCC_B": "occluder-table direction bins",
+    "MCPT_OCC_PREFILL": "occluder-table pre-fill at upload switched",
     "MCPT_WORK_COUNTERS": "counting k_trace build in the timed frames",
     "MCPT_LIB": "another libmcpt build",
     "MCPT_BENCH_SLOTS": "path slots overridden",

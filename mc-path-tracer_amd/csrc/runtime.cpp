@@ -42,6 +42,7 @@ struct mcpt_ctx {
     bool has_scene_before = false;  // set at the start of a re-upload
     int32_t ntri = 0;               // triangles of the uploaded scene
     size_t occ_entries_n = 0;       // occluder-cache table entries (DevScene::occ; + kOccGateWords gate words)
+    uint32_t* occ_init = nullptr;   // the table as the upload's pre-fill left it (film clears restore it); nullptr: empty
     int pair_depth = 0;
     bool cull_ok = true, occ_nest_ok = true;  // last upload: boxes contain their triangles / nest (scene_upload)
     // traversal work counters (mcpt_set_work_counters): k_trace's counting instantiation, whose six
@@ -811,6 +812,44 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
     }
     c->scene = s;
     c->ntri = d->ntri;
+    c->occ_init = nullptr;  // (the previous scene's copy went with scene_bufs)
+    if (s.occ) {
+        // Occluder-table pre-fill: one any-hit probe ray per table key (origin cell centre, direction
+        // bin centre; k_occ_probes) traced with occluder recording on, so every key whose probe is
+        // occluded starts with a triangle -- derived from the scene alone, like the BVH.  Film
+        // clears restore this table, so every frame starts from the same one and no frame depends
+        // on another.  MCPT_OCC_PREFILL=0: frames start from an empty table.
+        const char* pe = getenv("MCPT_OCC_PREFILL");
+        if (!(pe && pe[0] == '0' && pe[1] == 0)) {
+            const uint32_t nkeys = (uint32_t)(c->occ_entries_n / kOccWays);
+            float4 *pro, *prd;
+            uint8_t* pvis;
+            free_list(c->tmp_bufs);
+            if ((rc = dalloc(c, c->tmp_bufs, &pro, nkeys)) || (rc = dalloc(c, c->tmp_bufs, &prd, nkeys)) ||
+                (rc = dalloc(c, c->tmp_bufs, &pvis, nkeys)) || (rc = dalloc(c, c->scene_bufs, &c->occ_init, c->occ_entries_n)))
+                return rc;
+            launch_occ_probes(s, pro, prd, nkeys, c->stream);
+            TraceArgs ta{};
+            ta.scene = s;  // occ on, gate words 0: the finish records the occluder of every occluded probe
+            ta.nshards = 1;
+            TraceSet& ts = ta.set[1];
+            ts.ro = pro;
+            ts.rd = prd;
+            ts.count = nkeys;
+            ts.shard_cap = nkeys;
+            ta.vis = pvis;
+            ta.grab = &c->cnt->grab[0][0];
+            launch_trace(ta, c->geom, c->stream);
+            HIPCHK(c, hipMemsetAsync(c->cnt->grab, 0, sizeof(c->cnt->grab), c->stream));  // hand-out counters back to 0
+            HIPCHK(c, hipMemcpyAsync(c->occ_init, s.occ, c->occ_entries_n * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                     c->stream));
+            const uint32_t warm[kOccGateWords] = {0u, 0u, 1u};  // the table holds occluders: lookups from the start
+            HIPCHK(c, hipMemcpyAsync(s.occ_gate, warm, sizeof(warm), hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipGetLastError());
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            free_list(c->tmp_bufs);
+        }
+    }
     if (c->has_scene_before) c->film_stale = true;  // a re-upload notifies the film
     c->has_scene = true;
     return MCPT_OK;
@@ -926,12 +965,19 @@ int mcpt_film_clear(mcpt_ctx* c) {
         HIPCHK(c, hipMemsetAsync(c->film_samples, 0, c->P * sizeof(uint32_t), c->stream));
     }
     if (c->blk_done) HIPCHK(c, hipMemsetAsync(c->blk_done, 0, c->blk_done_n, c->stream));
-    // The occluder cache starts empty with every film (and its lookup gate on), so a frame's work
-    // never depends on the frames before it.  (It only ever chose which triangle an any-hit ray
-    // tests first; the 96 MB fill takes ~0.02 ms.)
+    // The occluder cache starts every film from the same table -- the upload's pre-fill, or empty --
+    // with its lookup gate on, so a frame's work never depends on the frames before it.  (It only
+    // ever chooses which triangle an any-hit ray tests first; the 96 MB copy takes ~0.04 ms.)
     if (c->scene.occ) {
-        HIPCHK(c, hipMemsetAsync(c->scene.occ, 0xff, c->occ_entries_n * sizeof(uint32_t), c->stream));
-        HIPCHK(c, hipMemsetAsync(c->scene.occ_gate, 0, kOccGateWords * sizeof(uint32_t), c->stream));
+        if (c->occ_init) {  // the upload's pre-filled table (scene-derived), the same for every frame
+            HIPCHK(c, hipMemcpyAsync(c->scene.occ, c->occ_init, c->occ_entries_n * sizeof(uint32_t),
+                                     hipMemcpyDeviceToDevice, c->stream));
+            static const uint32_t warm[kOccGateWords] = {0u, 0u, 1u};
+            HIPCHK(c, hipMemcpyAsync(c->scene.occ_gate, warm, sizeof(warm), hipMemcpyHostToDevice, c->stream));
+        } else {
+            HIPCHK(c, hipMemsetAsync(c->scene.occ, 0xff, c->occ_entries_n * sizeof(uint32_t), c->stream));
+            HIPCHK(c, hipMemsetAsync(c->scene.occ_gate, 0, kOccGateWords * sizeof(uint32_t), c->stream));
+        }
     }
     c->film_stale = false;
     c->unpacked.clear();
