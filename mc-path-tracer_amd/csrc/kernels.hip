@@ -2318,19 +2318,9 @@ void launch_cull_margins(float4* nodes, uint32_t npairs, const float4* tri, uint
 // the key's origin cell along the centre of its direction bin, so that occ_index maps the probe back
 // to its own key.  Tracing the probes as any-hit rays records an occluder in every key whose probe
 // is occluded -- a property of the scene alone, like the BVH.
-// MCPT_OCC_PROBES probes per key: probe p > 0 starts a quarter cell off the centre (the signs of
-// p's bits per axis) along a direction a quarter bin off the bin's centre, inside the same key.
-#ifndef MCPT_OCC_PROBES
-#define MCPT_OCC_PROBES 1
-#endif
-constexpr uint32_t kOccProbes = MCPT_OCC_PROBES;
 __global__ void k_occ_probes(DevScene sc, float4* ro, float4* rd, uint32_t nkeys) {
-    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= nkeys * kOccProbes) return;
-    const uint32_t key = idx / kOccProbes, p = idx % kOccProbes;
-    const float jo[3] = {p == 0u ? 0.f : ((p & 1u) ? 0.25f : -0.25f), p == 0u ? 0.f : ((p & 2u) ? 0.25f : -0.25f),
-                         p == 0u ? 0.f : ((p & 4u) ? -0.25f : 0.25f)};
-    const float jd = p == 0u ? 0.f : ((p & 1u) ? 0.25f : -0.25f), je = p == 0u ? 0.f : ((p & 2u) ? -0.25f : 0.25f);
+    const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
+    if (key >= nkeys) return;
     const uint32_t G = (uint32_t)sc.occ_g, B = (uint32_t)sc.occ_b;
     uint32_t t = key, cx, cy, cz, face, ub, vb;
 #if MCPT_OCC_LAYOUT == 1
@@ -2341,23 +2331,21 @@ __global__ void k_occ_probes(DevScene sc, float4* ro, float4* rd, uint32_t nkeys
     const uint32_t c[3] = {cx, cy, cz};
     float o[3];
     for (int k = 0; k < 3; k++)
-        o[k] = sc.occ_inv[k] > 0.f ? sc.root_mn[k] + ((float)c[k] + 0.5f + jo[k]) / sc.occ_inv[k] : sc.root_mn[k];
+        o[k] = sc.occ_inv[k] > 0.f ? sc.root_mn[k] + ((float)c[k] + 0.5f) / sc.occ_inv[k] : sc.root_mn[k];
     const float hb = 0.5f * (float)B;
-    const float u = ((float)ub + 0.5f + jd) / hb - 1.f, v = ((float)vb + 0.5f + je) / hb - 1.f;
+    const float u = ((float)ub + 0.5f) / hb - 1.f, v = ((float)vb + 0.5f) / hb - 1.f;
     const float sg = (face & 1u) ? -1.f : 1.f;
     float d[3];
     if (face < 2u) { d[0] = sg; d[1] = u; d[2] = v; }
     else if (face < 4u) { d[0] = u; d[1] = sg; d[2] = v; }
     else { d[0] = u; d[1] = v; d[2] = sg; }
     const float inv_n = 1.f / __builtin_sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-    ro[idx] = make_float4(o[0], o[1], o[2], 0.f);
-    rd[idx] = make_float4(d[0] * inv_n, d[1] * inv_n, d[2] * inv_n, 0.f);
+    ro[key] = make_float4(o[0], o[1], o[2], 0.f);
+    rd[key] = make_float4(d[0] * inv_n, d[1] * inv_n, d[2] * inv_n, 0.f);
 }
-uint32_t occ_probes_per_key() { return kOccProbes; }
 void launch_occ_probes(const DevScene& sc, float4* ro, float4* rd, uint32_t nkeys, hipStream_t s) {
     if (nkeys == 0) return;
-    const uint32_t n = nkeys * kOccProbes;
-    hipLaunchKernelGGL(k_occ_probes, dim3((n + 255) / 256), dim3(256), 0, s, sc, ro, rd, nkeys);
+    hipLaunchKernelGGL(k_occ_probes, dim3((nkeys + 255) / 256), dim3(256), 0, s, sc, ro, rd, nkeys);
 }
 void launch_occ_records(const DevScene& sc, uint32_t nnodes, float4* rec, hipStream_t s) {
     hipLaunchKernelGGL(k_occ_records, dim3(nnodes / 256 + 1), dim3(256), 0, s, sc, nnodes, rec);

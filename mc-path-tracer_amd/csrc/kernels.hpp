@@ -273,8 +273,7 @@ void launch_clear(const ClearArgs& a, hipStream_t s);
 // width; a root that is itself a leaf gets the root box)
 constexpr int kOccRecF4 = 4;
 void launch_occ_records(const DevScene& sc, uint32_t nnodes, float4* rec, hipStream_t s);
-void launch_occ_probes(const DevScene& sc, float4* ro, float4* rd, uint32_t nkeys, hipStream_t s);  // nkeys * occ_probes_per_key() rays
-uint32_t occ_probes_per_key();
+void launch_occ_probes(const DevScene& sc, float4* ro, float4* rd, uint32_t nkeys, hipStream_t s);
 // Culling margins of a child-pair tree (mcpt_core.hpp cull_*): tri_w[t] = W'_T of record t,
 // *pmax = the far coefficient P's bits (max), then `passes` bottom-up passes writing every
 // child's subtree maximum into q3.z / q3.w (passes >= tree depth + 1 reach the fixed point).

@@ -822,12 +822,11 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
         const char* pe = getenv("MCPT_OCC_PREFILL");
         if (!(pe && pe[0] == '0' && pe[1] == 0)) {
             const uint32_t nkeys = (uint32_t)(c->occ_entries_n / kOccWays);
-            const uint32_t nprobe = nkeys * occ_probes_per_key();
             float4 *pro, *prd;
             uint8_t* pvis;
             free_list(c->tmp_bufs);
-            if ((rc = dalloc(c, c->tmp_bufs, &pro, nprobe)) || (rc = dalloc(c, c->tmp_bufs, &prd, nprobe)) ||
-                (rc = dalloc(c, c->tmp_bufs, &pvis, nprobe)) || (rc = dalloc(c, c->scene_bufs, &c->occ_init, c->occ_entries_n)))
+            if ((rc = dalloc(c, c->tmp_bufs, &pro, nkeys)) || (rc = dalloc(c, c->tmp_bufs, &prd, nkeys)) ||
+                (rc = dalloc(c, c->tmp_bufs, &pvis, nkeys)) || (rc = dalloc(c, c->scene_bufs, &c->occ_init, c->occ_entries_n)))
                 return rc;
             launch_occ_probes(s, pro, prd, nkeys, c->stream);
             TraceArgs ta{};
@@ -836,8 +835,8 @@ static int scene_upload(mcpt_ctx* c, const mcpt_scene_desc* d, bool gpu_bvh) {
             TraceSet& ts = ta.set[1];
             ts.ro = pro;
             ts.rd = prd;
-            ts.count = nprobe;
-            ts.shard_cap = nprobe;
+            ts.count = nkeys;
+            ts.shard_cap = nkeys;
             ta.vis = pvis;
             ta.grab = &c->cnt->grab[0][0];
             launch_trace(ta, c->geom, c->stream);
